@@ -1,0 +1,124 @@
+// pybind11 bindings for the deep_go_amd HIP kernels (module `_dghip`).
+//
+// Tensors cross the boundary as raw device addresses (tensor.data_ptr()) and the HIP
+// stream as its handle (torch.cuda.current_stream().cuda_stream): the Python layer
+// (deep_go_amd/ops) owns allocation, shape checks and stream choice, and every launcher
+// here validates the shape invariants it relies on before touching the GPU.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+extern "C" {
+hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, int M, int Mpad,
+                      const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
+                      const float* bias, const float* posb, const void* aux, int aux_pad,
+                      hipStream_t stream);
+hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
+                         int x_pad, int x_C, int Npix, int KP, int splits, float* slab,
+                         hipStream_t stream);
+hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
+                           int taps, int cin, int cinp, hipStream_t stream);
+hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
+                   const float* bias, const float* posb, const int* labels, float* loss,
+                   int* pred, float* logp_out, void* dZ, int dz_pad, float* gw, float* gbias,
+                   float* gposb, int head_relu, float grad_scale, hipStream_t stream);
+hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, const uint8_t* rank,
+                              void* out, int B, int pad, int CP, hipStream_t s);
+hipError_t dg_bias_grad(const void* dZ, int B, int C, int pad, float* gposb, float* gbias,
+                        hipStream_t s);
+hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
+                  hipStream_t s);
+hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
+                      float decay, float gscale, hipStream_t s);
+hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
+hipError_t dg_weight_refresh(const long long* table, int n, hipStream_t s);
+}
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_dghip, m) {
+  m.doc() = "deep_go_amd CDNA4 (gfx950) HIP kernels";
+  m.attr("EPI_LINEAR") = 0;
+  m.attr("EPI_FWD") = 1;
+  m.attr("EPI_DGRAD") = 2;
+
+  m.def("conv_nt",
+        [](int epi, int kw, int bm, int bn, uintptr_t A, int KP, int M, int Mpad, uintptr_t X,
+           int x_pad, int x_C, int Npix, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
+           uintptr_t aux, int aux_pad, uintptr_t stream) {
+          check(dg_conv_nt(epi, kw, bm, bn, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C,
+                           Npix, P<void>(Y), y_pad, P<float>(bias), P<float>(posb), P<void>(aux),
+                           aux_pad, S(stream)),
+                "conv_nt");
+        });
+  m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
+                         int x_pad, int x_C, int Npix, int KP, int splits, uintptr_t slab,
+                         uintptr_t stream) {
+    check(dg_conv_wgrad(kw, P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, Npix, KP,
+                        splits, P<float>(slab), S(stream)),
+          "conv_wgrad");
+  });
+  m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
+                           int taps, int cin, int cinp, uintptr_t stream) {
+    check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
+                          S(stream)),
+          "wgrad_reduce");
+  });
+  m.def("head", [](int kw, uintptr_t X, int x_pad, int C, int B, uintptr_t w, uintptr_t bias,
+                   uintptr_t posb, uintptr_t labels, uintptr_t loss, uintptr_t pred,
+                   uintptr_t logp, uintptr_t dZ, int dz_pad, uintptr_t gw, uintptr_t gbias,
+                   uintptr_t gposb, int head_relu, float grad_scale, uintptr_t stream) {
+    check(dg_head(kw, P<void>(X), x_pad, C, B, P<float>(w), P<float>(bias), P<float>(posb),
+                  P<int>(labels), P<float>(loss), P<int>(pred), P<float>(logp), P<void>(dZ),
+                  dz_pad, P<float>(gw), P<float>(gbias), P<float>(gposb), head_relu, grad_scale,
+                  S(stream)),
+          "head");
+  });
+  m.def("expand_features", [](uintptr_t planes, uintptr_t player, uintptr_t rank, uintptr_t out,
+                              int B, int pad, int CP, uintptr_t stream) {
+    check(dg_expand_features(P<uint8_t>(planes), P<uint8_t>(player), P<uint8_t>(rank),
+                             P<void>(out), B, pad, CP, S(stream)),
+          "expand_features");
+  });
+  m.def("bias_grad", [](uintptr_t dZ, int B, int C, int pad, uintptr_t gposb, uintptr_t gbias,
+                        uintptr_t stream) {
+    check(dg_bias_grad(P<void>(dZ), B, C, pad, P<float>(gposb), P<float>(gbias), S(stream)),
+          "bias_grad");
+  });
+  m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
+                  uintptr_t stream) {
+    check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, S(stream)), "sgd");
+  });
+  m.def("rmsprop", [](uintptr_t p, uintptr_t g, uintptr_t ms, size_t n, uintptr_t lr,
+                      float decay, float gscale, uintptr_t stream) {
+    check(dg_rmsprop(P<float>(p), P<float>(g), P<float>(ms), n, P<double>(lr), decay, gscale,
+                     S(stream)),
+          "rmsprop");
+  });
+  m.def("lr_decay", [](uintptr_t lr, double decay, uintptr_t step, uintptr_t stream) {
+    check(dg_lr_decay(P<double>(lr), decay, P<long long>(step), S(stream)), "lr_decay");
+  });
+  m.def("weight_refresh", [](uintptr_t table, int n, uintptr_t stream) {
+    check(dg_weight_refresh(P<long long>(table), n, S(stream)), "weight_refresh");
+  });
+  m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+  m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
+}

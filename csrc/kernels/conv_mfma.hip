@@ -1,0 +1,495 @@
+// Implicit-GEMM 19x19 convolutions on CDNA4 MFMA (bf16 in, fp32 accumulate).
+//
+// Replaces the reference's nn.SpatialZeroPadding + nn.SpatialConvolutionMM (+ nn.Add +
+// nn.ReLU) stack (experiments.lua:137-147; im2col + cuBLAS SGEMM in cunn, EXTERNAL).
+//
+// Design (MI355X-first, not a port):
+//  * Activations live in zero-bordered NHWC frames [B][19+2p][19+2p][C] (bf16), so a
+//    conv tap is a constant byte offset from the output pixel's centre and halo loads
+//    need no predicates (zero padding = the frame border, written once, never touched).
+//  * The GEMM N dimension is the flattened valid pixel index n = b*361 + h*19 + w
+//    (no frame-border compute waste); every lane computes its own pixel's frame offset,
+//    so im2col is implicit in the per-lane SOURCE address of global_load_lds_dwordx4.
+//  * K = (tap, channel) in 8-channel (16 B) groups.  LDS tiles are lane-linear 128-B rows
+//    (64 k) with an XOR swizzle applied on the source side (slot ^= row&7): conflict-free
+//    ds_read_b128 for the 16x16x32 fragment pattern (checked with tools/lds_banks.py).
+//  * conv_nt_kernel: D[co][n] = sum_k W[co][k] * im2col(X)[n][k]  (forward and dgrad).
+//      EPI_FWD   : + bias[co] + pos_bias[p][co], ReLU, bf16 store into the output frame.
+//      EPI_DGRAD : * (aux_activation > 0)  (ReLU backward fused), bf16 store.
+//      EPI_LINEAR: plain store (tests).
+//  * conv_wgrad_kernel: dW[co][k] = sum_n dZ[n][co] * im2col(X)[n][k] with split-K over
+//    pixels into fp32 slabs; both operands are staged pixel-major and read with the
+//    CDNA4 transposing LDS read ds_read_b64_tr_b16.
+#include "dg_common.h"
+
+using namespace dg;
+
+namespace {
+
+constexpr int EPI_LINEAR = 0;
+constexpr int EPI_FWD = 1;
+constexpr int EPI_DGRAD = 2;
+
+struct ConvNTArgs {
+  const bf16_t* A;     // [Mpad][KP] bf16 weights (K contiguous)
+  const char* X;       // input frame (bytes)
+  char* Y;             // output frame (bytes)
+  const float* bias;   // [M]           (EPI_FWD)
+  const float* posb;   // [361][M]      (EPI_FWD)
+  const char* aux;     // mask frame    (EPI_DGRAD), channels = M
+  int KP;              // padded K (multiple of 64)
+  int M;               // real output channels
+  int Npix;            // B*361
+  int x_pad, x_C;      // input frame pad and channels (multiple of 8)
+  int y_pad;           // output frame pad (channels = M)
+  int aux_pad;
+  int ngroups;         // valid k-groups = KW*KW*x_C/8
+  int gpt;             // k-groups per tap = x_C/8
+  uint32_t gpt_magic;  // floor(2^32/gpt)+1
+};
+
+// Byte offset (relative to the pixel centre) of k-group kg.
+template <int KW>
+DG_DEV int koff_of(int kg, const ConvNTArgs& a) {
+  if (kg >= a.ngroups) return 0;
+  const int t = (int)__umulhi((uint32_t)kg, a.gpt_magic);
+  const int c8 = kg - t * a.gpt;
+  constexpr int R = (KW - 1) / 2;
+  const int dh = t / KW - R;
+  const int dw = t % KW - R;
+  const int F = BOARD + 2 * a.x_pad;
+  return ((dh * F + dw) * a.x_C + c8 * 8) * 2;
+}
+
+// MF: 16-row fragments per wave along M (BM = 2*16*MF); NF: along N (BN = 2*16*NF).
+template <int KW, int MF, int NF, int EPI>
+__global__ void __launch_bounds__(256)
+conv_nt_kernel(ConvNTArgs a) {
+  constexpr int BM = 32 * MF;
+  constexpr int BN = 32 * NF;
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 32;  // glds per wave per K-step (BM rows / 8 rows / 4 waves)
+  constexpr int B_INSTR = BN / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n_tile = blockIdx.x * BN;
+  const int m_tile = blockIdx.y * BM;
+
+  // ---- per-lane staging constants ----
+  const int g_src = (lane & 7) ^ (lane >> 3);   // k-group this lane fetches (source swizzle)
+  const int row_in_instr = lane >> 3;
+  uint32_t pix_off[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int r = (wave * B_INSTR + i) * 8 + row_in_instr;
+    int n = n_tile + r;
+    if (n >= a.Npix) n = 0;
+    pix_off[i] = pixel_frame_off(n, a.x_pad, a.x_C);
+  }
+  const char* a_row[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int r = (wave * A_INSTR + i) * 8 + row_in_instr;
+    a_row[i] = (const char*)a.A + (size_t)(m_tile + r) * a.KP * 2 + g_src * 16;
+  }
+
+  auto stage = [&](int buf, int ks) {
+    char* sA = smem + buf * STAGE;
+    char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i)
+      glds16(a_row[i] + ks * 128, (LDS_AS void*)(sA + (wave * A_INSTR + i) * 1024));
+    const int ko = koff_of<KW>(ks * 8 + g_src, a);
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      glds16(a.X + (int)pix_off[i] + ko, (LDS_AS void*)(sB + (wave * B_INSTR + i) * 1024));
+  };
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.KP / 64;
+  stage(0, 0);
+  __syncthreads();
+
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) stage(buf ^ 1, ks + 1);
+    const char* sA = smem + buf * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int slot = ((kk * 4 + lq) ^ (lane & 7)) * 16;
+      bf16x8 af[MF], bfr[NF];
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+        af[i] = lds_read_b128((const LDS_AS char*)(sA + (wm * MF * 16 + i * 16 + lr) * 128 + slot));
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        bfr[j] = lds_read_b128((const LDS_AS char*)(sB + (wn * NF * 16 + j * 16 + lr) * 128 + slot));
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const int y_C = a.M;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int n = n_tile + wn * NF * 16 + j * 16 + lr;
+    if (n >= a.Npix) continue;
+    const int b = n / NPTS;
+    const int p = n - b * NPTS;
+    const int h = p / BOARD;
+    const int w = p - h * BOARD;
+    const uint32_t yo = frame_off(b, h, w, a.y_pad, y_C);
+    uint32_t ao = 0;
+    if constexpr (EPI == EPI_DGRAD) ao = frame_off(b, h, w, a.aux_pad, y_C);
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int co = m_tile + wm * MF * 16 + i * 16 + lq * 4;
+      if (co >= a.M) continue;
+      f32x4 v = acc[i][j];
+      if constexpr (EPI == EPI_FWD) {
+        const f32x4 bb = *(const f32x4*)(a.bias + co);
+        const f32x4 pb = *(const f32x4*)(a.posb + p * a.M + co);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bb[r] + pb[r], 0.f);
+      } else if constexpr (EPI == EPI_DGRAD) {
+        const uint2 m = *(const uint2*)(a.aux + ao + co * 2);
+        // bf16 > 0  <=>  sign bit clear and non-zero
+        const uint32_t m01 = m.x, m23 = m.y;
+        if ((m01 & 0xFFFFu) == 0 || (m01 & 0x8000u)) v[0] = 0.f;
+        if ((m01 >> 16) == 0 || (m01 & 0x80000000u)) v[1] = 0.f;
+        if ((m23 & 0xFFFFu) == 0 || (m23 & 0x8000u)) v[2] = 0.f;
+        if ((m23 >> 16) == 0 || (m23 & 0x80000000u)) v[3] = 0.f;
+      }
+      uint2 o;
+      o.x = pack_bf16x2(v[0], v[1]);
+      o.y = pack_bf16x2(v[2], v[3]);
+      *(uint2*)(a.Y + yo + co * 2) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient: dW[co][k] = sum_n dZ[n][co] * im2col(X)[n][k]
+// Tile: BM co x BN k per workgroup, 4 waves (2x2), each 64x64 (4x4 fragments).
+// Reduction over pixels in steps of 64, split across blockIdx.z into fp32 slabs
+// slab[z][co][k] (co < Mpad, k < KP).
+struct WgradArgs {
+  const char* dZ;   // gradient frame, channels = M
+  const char* X;    // input frame of the layer
+  float* slab;      // [splits][Mpad][KP]
+  int dz_pad;
+  int M, Mpad;      // output channels (real, padded to 128)
+  int KP;           // padded K (multiple of 128)
+  int Npix;
+  int px_per_split; // multiple of 64
+  int x_pad, x_C;
+  int ngroups, gpt;
+  uint32_t gpt_magic;
+};
+
+DG_DEV int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+template <int KW>
+DG_DEV int koff_wg(int kg, const WgradArgs& a) {
+  if (kg >= a.ngroups) return 0;
+  const int t = (int)__umulhi((uint32_t)kg, a.gpt_magic);
+  const int c8 = kg - t * a.gpt;
+  constexpr int R = (KW - 1) / 2;
+  const int dh = t / KW - R;
+  const int dw = t % KW - R;
+  const int F = BOARD + 2 * a.x_pad;
+  return ((dh * F + dw) * a.x_C + c8 * 8) * 2;
+}
+
+template <int KW>
+__global__ void __launch_bounds__(256)
+conv_wgrad_kernel(WgradArgs a) {
+  constexpr int BM = 128, BN = 128, BKN = 64;  // BKN pixels per step
+  constexpr int T_BYTES = BKN * 256;           // 64 rows x 256 B
+  constexpr int STAGE = 2 * T_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int k_tile = blockIdx.x * BN;
+  const int m_tile = blockIdx.y * BM;
+  const int n_begin = blockIdx.z * a.px_per_split;
+  int n_end = n_begin + a.px_per_split;
+  if (n_end > a.Npix) n_end = a.Npix;
+  const int nsteps = (n_end - n_begin + BKN - 1) / BKN;
+
+  // staging: each wave-instruction = 4 rows x 16 slots of 16 B; 4 instr per wave per tile
+  const int r_in = lane >> 4;
+  const int slot = lane & 15;
+  // source chunk (16 B unit along the 256-B row) for each of the 4 rows this lane fills
+  int koffs[4];
+  int dz_chunk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (wave * 4 + i) * 4 + r_in;  // row within tile (pixel)
+    const int c = slot ^ wg_swz(r);
+    dz_chunk[i] = (m_tile * 2) + c * 16;
+    koffs[i] = koff_wg<KW>(k_tile / 8 + c, a);
+  }
+
+  auto stage = [&](int buf, int step) {
+    char* sA = smem + buf * STAGE;
+    char* sB = sA + T_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (wave * 4 + i) * 4 + r_in;
+      int n = n_begin + step * BKN + r;
+      const bool ok = n < n_end;
+      if (!ok) n = n_begin;  // valid address; contribution zeroed below via dz row mask
+      const int b = n / NPTS;
+      const int p = n - b * NPTS;
+      const int h = p / BOARD;
+      const int w = p - h * BOARD;
+      const uint32_t dzo = frame_off(b, h, w, a.dz_pad, a.M);
+      const uint32_t xo = frame_off(b, h, w, a.x_pad, a.x_C);
+      // out-of-range rows read the zero border (offset 0 of the frame is border) for dZ
+      const char* src_dz = ok ? (a.dZ + dzo + dz_chunk[i]) : (a.dZ + (slot * 16));
+      glds16(src_dz, (LDS_AS void*)(sA + (wave * 4 + i) * 1024));
+      glds16(a.X + xo + koffs[i], (LDS_AS void*)(sB + (wave * 4 + i) * 1024));
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    stage(0, 0);
+    __syncthreads();
+  }
+  const int li = lane & 15;
+  const int g = lane >> 4;
+  const int q = li >> 2, pp = li & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) stage(buf ^ 1, st + 1);
+    const char* sA = smem + buf * STAGE;
+    const char* sB = sA + T_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int row = kk * 32 + 8 * g + 4 * half + q;
+        const int sw = wg_swz(row);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = (wm * 64 + i * 16) / 8 + (pp >> 1);
+          const s16x4 t = lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+          s16x8 tmp = __builtin_bit_cast(s16x8, af[i]);
+          tmp[4 * half + 0] = t[0]; tmp[4 * half + 1] = t[1];
+          tmp[4 * half + 2] = t[2]; tmp[4 * half + 3] = t[3];
+          af[i] = __builtin_bit_cast(bf16x8, tmp);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = (wn * 64 + j * 16) / 8 + (pp >> 1);
+          const s16x4 t = lds_read_tr((const LDS_AS char*)(sB + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+          s16x8 tmp = __builtin_bit_cast(s16x8, bfr[j]);
+          tmp[4 * half + 0] = t[0]; tmp[4 * half + 1] = t[1];
+          tmp[4 * half + 2] = t[2]; tmp[4 * half + 3] = t[3];
+          bfr[j] = __builtin_bit_cast(bf16x8, tmp);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  // slab store: D rows = co, cols = k
+  float* slab = a.slab + (size_t)blockIdx.z * a.Mpad * a.KP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m_tile + wm * 64 + i * 16 + g * 4 + r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k_tile + wn * 64 + j * 16 + li;
+        slab[(size_t)co * a.KP + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// Sum the split-K slabs and scatter into the fp32 master-gradient layout OHWI
+// [co][kh][kw][ci] (only ci < Cin, co < M).  out is overwritten.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                    int splits, int M, int Mpad, int KP, int taps, int cin,
+                                    int cinp) {
+  const int total = M * taps * cin;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int co = idx / (taps * cin);
+    const int rem = idx - co * taps * cin;
+    const int t = rem / cin;
+    const int ci = rem - t * cin;
+    const size_t src = (size_t)co * KP + t * cinp + ci;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * Mpad * KP + src];
+    out[idx] = s;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// Host launchers (C ABI used by the pybind11 module).
+
+static uint32_t magic_for(int d) { return (uint32_t)((0x100000000ull / (uint64_t)d) + 1); }
+
+// Allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); set once per kernel.
+template <typename K>
+static void allow_lds(K kernel, size_t bytes) {
+  static bool done = false;  // one flag per template instantiation
+  if (!done && bytes > 65536) {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = true;
+  }
+}
+
+template <int KW, int MF, int NF, int EPI>
+static void launch_nt_epi(const ConvNTArgs& a, int Mpad, hipStream_t s) {
+  constexpr int BM = 32 * MF, BN = 32 * NF;
+  const size_t lds = 2 * (size_t)(BM * 128 + BN * 128);
+  dim3 grid((a.Npix + BN - 1) / BN, Mpad / BM);
+  allow_lds(conv_nt_kernel<KW, MF, NF, EPI>, lds);
+  hipLaunchKernelGGL((conv_nt_kernel<KW, MF, NF, EPI>), grid, dim3(256), lds, s, a);
+}
+
+template <int KW, int MF, int NF>
+static hipError_t launch_nt(int epi, const ConvNTArgs& a, int Mpad, hipStream_t s) {
+  switch (epi) {
+    case EPI_FWD: launch_nt_epi<KW, MF, NF, EPI_FWD>(a, Mpad, s); break;
+    case EPI_DGRAD: launch_nt_epi<KW, MF, NF, EPI_DGRAD>(a, Mpad, s); break;
+    default: launch_nt_epi<KW, MF, NF, EPI_LINEAR>(a, Mpad, s);
+  }
+  return hipGetLastError();
+}
+
+template <int KW>
+static hipError_t dispatch_tile(int epi, const ConvNTArgs& a, int Mpad, int bm, int bn,
+                                hipStream_t s) {
+  if (bm == 128 && bn == 128) return launch_nt<KW, 4, 4>(epi, a, Mpad, s);
+  if (bm == 128 && bn == 192) return launch_nt<KW, 4, 6>(epi, a, Mpad, s);
+  if (bm == 64 && bn == 128) return launch_nt<KW, 2, 4>(epi, a, Mpad, s);
+  if (bm == 64 && bn == 256) return launch_nt<KW, 2, 8>(epi, a, Mpad, s);
+  return hipErrorInvalidValue;
+}
+
+extern "C" {
+
+// Conv (forward / dgrad / linear) via the NT implicit-GEMM kernel.
+hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, int M, int Mpad,
+                      const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
+                      const float* bias, const float* posb, const void* aux, int aux_pad,
+                      hipStream_t stream) {
+  if (KP % 64 != 0 || x_C % 8 != 0 || M % 4 != 0 || Mpad % bm != 0 || Npix <= 0)
+    return hipErrorInvalidValue;
+  ConvNTArgs a;
+  a.A = (const bf16_t*)A;
+  a.X = (const char*)X;
+  a.Y = (char*)Y;
+  a.bias = bias;
+  a.posb = posb;
+  a.aux = (const char*)aux;
+  a.KP = KP;
+  a.M = M;
+  a.Npix = Npix;
+  a.x_pad = x_pad;
+  a.x_C = x_C;
+  a.y_pad = y_pad;
+  a.aux_pad = aux_pad;
+  a.gpt = x_C / 8;
+  a.ngroups = kw * kw * a.gpt;
+  a.gpt_magic = magic_for(a.gpt);
+  if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
+  switch (kw) {
+    case 1: return dispatch_tile<1>(epi, a, Mpad, bm, bn, stream);
+    case 3: return dispatch_tile<3>(epi, a, Mpad, bm, bn, stream);
+    case 5: return dispatch_tile<5>(epi, a, Mpad, bm, bn, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
+                         int x_pad, int x_C, int Npix, int KP, int splits, float* slab,
+                         hipStream_t stream) {
+  if (KP % 128 != 0 || Mpad % 128 != 0 || x_C % 8 != 0 || M % 8 != 0 || splits <= 0)
+    return hipErrorInvalidValue;
+  WgradArgs a;
+  a.dZ = (const char*)dZ;
+  a.X = (const char*)X;
+  a.slab = slab;
+  a.dz_pad = dz_pad;
+  a.M = M;
+  a.Mpad = Mpad;
+  a.KP = KP;
+  a.Npix = Npix;
+  int per = (Npix + splits - 1) / splits;
+  per = (per + 63) / 64 * 64;
+  a.px_per_split = per;
+  a.x_pad = x_pad;
+  a.x_C = x_C;
+  a.gpt = x_C / 8;
+  a.ngroups = kw * kw * a.gpt;
+  a.gpt_magic = magic_for(a.gpt);
+  if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
+  // dZ channel tile must stay inside the dZ rows: for M < Mpad the extra co rows read
+  // neighbouring channels/pixels of valid memory and land in unused slab rows.
+  dim3 grid(KP / 128, Mpad / 128, splits);
+  const size_t lds = 2 * 2 * 64 * 256;
+  switch (kw) {
+    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), lds, stream, a); break;
+    case 3: hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), lds, stream, a); break;
+    case 5:
+      allow_lds(conv_wgrad_kernel<5>, lds);
+      hipLaunchKernelGGL(conv_wgrad_kernel<5>, grid, dim3(256), lds, stream, a);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
+                           int taps, int cin, int cinp, hipStream_t stream) {
+  const int total = M * taps * cin;
+  int blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, slab, out, splits,
+                     M, Mpad, KP, taps, cin, cinp);
+  return hipGetLastError();
+}
+
+}  // extern "C"

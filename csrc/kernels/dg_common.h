@@ -1,0 +1,76 @@
+// Common device helpers for the deep_go_amd CDNA4 (gfx950) kernels.
+//
+// Everything here is written for 64-lane wavefronts, bf16 MFMA (v_mfma_f32_16x16x32_bf16)
+// and LDS-DMA staging (global_load_lds_dwordx4).  No CUDA/HIP dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DG_DEV __device__ __forceinline__
+#define LDS_AS __attribute__((address_space(3)))
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef uint16_t bf16_t;  // storage type for bf16 in global memory
+
+namespace dg {
+
+constexpr int BOARD = 19;
+constexpr int NPTS = 361;
+
+// f32 -> bf16 round-to-nearest-even (NaN kept NaN via the compiler's v_cvt_pk_bf16_f32).
+DG_DEV bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+DG_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+DG_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// Async 16-byte global->LDS copy.  The LDS destination is (wave-uniform base) + lane*16.
+DG_DEV void glds16(const void* gsrc, LDS_AS void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, lds_wave_base, 16, 0, 0);
+}
+
+DG_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+DG_DEV bf16x8 lds_read_b128(const LDS_AS char* p) { return *(const LDS_AS bf16x8*)p; }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies &row q, cols 4p..4p+3;
+// lane i receives column i of the 4 rows (row q in element q).
+DG_DEV s16x4 lds_read_tr(const LDS_AS char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)p);
+}
+
+DG_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DG_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Byte offset of board pixel (b, h, w) inside a zero-bordered NHWC frame
+// [B][19+2pad][19+2pad][C] of bf16.
+DG_DEV uint32_t frame_off(int b, int h, int w, int pad, int C) {
+  const int F = BOARD + 2 * pad;
+  return (uint32_t)(((b * F + h + pad) * F + (w + pad)) * C) * 2u;
+}
+DG_DEV uint32_t pixel_frame_off(int n, int pad, int C) {
+  const int b = n / NPTS;
+  const int p = n - b * NPTS;
+  const int h = p / BOARD;
+  const int w = p - h * BOARD;
+  return frame_off(b, h, w, pad, C);
+}
+
+}  // namespace dg

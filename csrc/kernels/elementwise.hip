@@ -1,0 +1,258 @@
+// Memory-bound helper kernels: GPU feature expansion, per-channel / per-position bias
+// gradients, fused SGD / RMSProp updates, device-side LR decay and the bf16 weight
+// refresh that re-lays the fp32 OHWI master weights into the two MFMA operand layouts.
+#include "dg_common.h"
+
+using namespace dg;
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// 9 stored uint8 planes -> 37 network planes (padded to CP channels) written straight
+// into the first layer's zero-bordered NHWC frame.  Reference: preprocess()
+// (dataloader.lua:50-92), which builds float64 planes on 32 CPU threads.
+// planes: [B][9][361] uint8, player: [B] (1 black / 2 white), rank: [B] (dan of the
+// player to move, 1..9).  One thread per (board, point).
+__global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
+                                       const uint8_t* __restrict__ player,
+                                       const uint8_t* __restrict__ rank, char* __restrict__ out,
+                                       int B, int pad, int CP) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * NPTS) return;
+  const int b = idx / NPTS;
+  const int p = idx - b * NPTS;
+  const uint8_t* pl = planes + (size_t)b * 9 * NPTS + p;
+  const int pi = player[b];
+  const int op = 3 - pi;
+  const int stone = pl[0 * NPTS];
+  const int lib = pl[1 * NPTS];
+  const int la = pl[(pi == 1 ? 2 : 3) * NPTS];
+  const int kill = pl[(pi == 1 ? 4 : 5) * NPTS];
+  const int age = pl[6 * NPTS];
+  const int lad = pl[(pi == 1 ? 7 : 8) * NPTS];
+  const int rk = rank[b];
+  float v[48];
+#pragma unroll
+  for (int c = 0; c < 48; ++c) v[c] = 0.f;
+  v[0] = stone == 0;
+  v[1] = stone == pi;
+  v[2] = stone == op;
+#pragma unroll
+  for (int i = 1; i <= 3; ++i) v[2 + i] = lib == i;
+  v[6] = lib >= 4;
+  v[7] = (stone == 0) && (la == 0);
+#pragma unroll
+  for (int i = 1; i <= 5; ++i) v[7 + i] = la == i;
+  v[13] = la >= 6;
+#pragma unroll
+  for (int i = 1; i <= 6; ++i) v[13 + i] = kill == i;
+  v[20] = kill >= 7;
+#pragma unroll
+  for (int i = 1; i <= 5; ++i) v[20 + i] = age == i;
+  v[26] = lad >= 1;
+  // v[27] stays 0: the reference's dead plane 28 (RANK + rank, rank in 1..9)
+#pragma unroll
+  for (int r = 1; r <= 9; ++r) v[27 + r] = (rk == r);
+  const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+  char* dst = out + frame_off(b, h, w, pad, CP);
+#pragma unroll
+  for (int c = 0; c < 48; c += 8) {
+    if (c >= CP) break;
+    uint4 o;
+    o.x = pack_bf16x2(v[c + 0], v[c + 1]);
+    o.y = pack_bf16x2(v[c + 2], v[c + 3]);
+    o.z = pack_bf16x2(v[c + 4], v[c + 5]);
+    o.w = pack_bf16x2(v[c + 6], v[c + 7]);
+    *(uint4*)(dst + c * 2) = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Bias gradients of a conv layer from its pre-activation gradient frame dZ:
+//   gposb[p][c] = sum_b dZ[b][p][c]   (untied nn.Add bias, experiments.lua:144)
+//   gbias[c]   += sum_p gposb[p][c]   (per-channel conv bias)
+// One workgroup per board point p; threads = (C/8 groups) x (256/(C/8) board lanes).
+__global__ void __launch_bounds__(256)
+bias_grad_kernel(const char* __restrict__ dZ, int B, int C, int pad, float* __restrict__ gposb,
+                 float* __restrict__ gbias) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][8]
+  const int p = blockIdx.x;
+  const int G = C / 8;
+  const int tid = threadIdx.x;
+  const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+  const int F = BOARD + 2 * pad;
+  const int lanes_b = 256 / G;  // >= 1 since C <= 2048
+  const int g = tid % G;
+  const int lb = tid / G;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (lb < lanes_b) {
+    for (int b = lb; b < B; b += lanes_b) {
+      const uint4 v =
+          *(const uint4*)(dZ + ((size_t)((b * F + h + pad) * F + w + pad) * C + g * 8) * 2);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(u[e] << 16);
+        acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sred[tid * 8 + e] = acc[e];
+  __syncthreads();
+  if (tid < G) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < lanes_b; ++l)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += sred[(l * G + tid) * 8 + e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gposb[(size_t)p * C + tid * 8 + e] = s[e];
+      atomicAdd(gbias + tid * 8 + e, s[e]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// SGD (optimizer.lua:24-27): theta -= lr * g over the flat fp32 master buffer.  lr lives
+// on the device (double) so the step can be replayed inside a hipGraph.
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n,
+                           const double* __restrict__ lr, float gscale) {
+  const float l = (float)(*lr) * gscale;
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    f32x4 pv = ((f32x4*)p)[i];
+    const f32x4 gv = ((const f32x4*)g)[i];
+    pv -= l * gv;
+    ((f32x4*)p)[i] = pv;
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    p[i] -= l * g[i];
+}
+
+// RMSProp-style update (the reference's misnamed AdagradOptimizer, optimizer.lua:1-14):
+// ms = decay*ms + (1-decay)*g^2 ; theta -= lr * g / sqrt(ms); ms initialised to 1.
+__global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
+                               float* __restrict__ ms, size_t n, const double* __restrict__ lr,
+                               float decay, float gscale) {
+  const float l = (float)(*lr);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    const float m = decay * ms[i] + (1.f - decay) * gi * gi;
+    ms[i] = m;
+    p[i] -= l * gi * rsqrtf(m);
+  }
+}
+
+__global__ void lr_decay_kernel(double* lr, double decay, long long* step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    *lr = *lr * (1.0 - decay);
+    if (step) *step += 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// fp32 OHWI master -> bf16 operand layouts, all layers in one launch (grid.y = layer):
+//   fwd  : Wf[co][t*cinp + ci]          (A operand of the forward NT GEMM)
+//   dgrad: Wd[ci][(T-1-t)*cout + co]    (A operand of the dgrad NT GEMM, flipped taps)
+struct WRefreshLayer {
+  const float* w;
+  bf16_t* wf;
+  bf16_t* wd;  // may be null (first layer / head)
+  int cout, cin, taps, cinp, kpf, kpd;
+};
+constexpr int MAX_REFRESH = 48;
+struct WRefreshArgs {
+  int n;
+  WRefreshLayer L[MAX_REFRESH];
+};
+
+__global__ void weight_refresh_kernel(WRefreshArgs a) {
+  const WRefreshLayer L = a.L[blockIdx.y];
+  const int total = L.cout * L.taps * L.cin;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int co = idx / (L.taps * L.cin);
+    const int rem = idx - co * L.taps * L.cin;
+    const int t = rem / L.cin;
+    const int ci = rem - t * L.cin;
+    const bf16_t v = f2bf(L.w[idx]);
+    L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = v;
+    if (L.wd) L.wd[(size_t)ci * L.kpd + (L.taps - 1 - t) * L.cout + co] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, const uint8_t* rank,
+                              void* out, int B, int pad, int CP, hipStream_t s) {
+  if (CP % 8 != 0 || CP < 40 || CP > 48) return hipErrorInvalidValue;
+  const int n = B * NPTS;
+  hipLaunchKernelGGL(expand_features_kernel, dim3((n + 255) / 256), dim3(256), 0, s, planes,
+                     player, rank, (char*)out, B, pad, CP);
+  return hipGetLastError();
+}
+
+hipError_t dg_bias_grad(const void* dZ, int B, int C, int pad, float* gposb, float* gbias,
+                        hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bias_grad_kernel, dim3(NPTS), dim3(256), 256 * 8 * sizeof(float), s,
+                     (const char*)dZ, B, C, pad, gposb, gbias);
+  return hipGetLastError();
+}
+
+hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
+                  hipStream_t s) {
+  int blocks = (int)((n / 4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sgd_kernel, dim3(blocks), dim3(256), 0, s, p, g, n, lr, gscale);
+  return hipGetLastError();
+}
+
+hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
+                      float decay, float gscale, hipStream_t s) {
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, s, p, g, ms, n, lr, decay,
+                     gscale);
+  return hipGetLastError();
+}
+
+hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s) {
+  hipLaunchKernelGGL(lr_decay_kernel, dim3(1), dim3(64), 0, s, lr, decay, step);
+  return hipGetLastError();
+}
+
+// layers: n entries of 10 int64 words {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused}
+hipError_t dg_weight_refresh(const long long* table, int n, hipStream_t s) {
+  if (n <= 0 || n > MAX_REFRESH) return hipErrorInvalidValue;
+  WRefreshArgs a;
+  a.n = n;
+  int maxtotal = 1;
+  for (int i = 0; i < n; ++i) {
+    const long long* t = table + 10 * i;
+    a.L[i].w = (const float*)t[0];
+    a.L[i].wf = (bf16_t*)t[1];
+    a.L[i].wd = (bf16_t*)t[2];
+    a.L[i].cout = (int)t[3];
+    a.L[i].cin = (int)t[4];
+    a.L[i].taps = (int)t[5];
+    a.L[i].cinp = (int)t[6];
+    a.L[i].kpf = (int)t[7];
+    a.L[i].kpd = (int)t[8];
+    const int tot = a.L[i].cout * a.L[i].cin * a.L[i].taps;
+    if (tot > maxtotal) maxtotal = tot;
+  }
+  int blocks = (maxtotal + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(weight_refresh_kernel, dim3(blocks, n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,400 @@
+"""GoCNN on MI355X: a native training-step executor over the hand-written HIP kernels.
+
+This replaces the reference's nn.Sequential + cunn execution (``experiments.lua:97-107``,
+``train.lua:4-12``) with an explicit, pre-planned launch sequence:
+
+  zero grads -> expand features (uint8 planes -> bf16 frame) -> conv fwd x (L-1)
+  -> fused head (conv + biases + ReLU + log-softmax + NLL + argmax + its backward)
+  -> for each layer, last to first: bias grads, wgrad (split-K slabs + reduce), dgrad
+     with the ReLU mask fused
+  -> [DP: bucketed gradient all-reduce hooks] -> SGD/RMSProp -> LR decay -> bf16 refresh
+
+Every launch's arguments are resolved once at construction (``self._fwd``, ``self._bwd``
+lists) so a step is a flat loop of native calls; the whole step, or the segments between
+collectives, is then captured into a hipGraph (``torch.cuda.CUDAGraph``) and replayed.
+
+Buffers are static (allocated once, sized for the per-GPU batch): the 12x256 config at
+batch 256 needs < 1 GB of HBM, so nothing is ever re-allocated in the step.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..config import NUM_POINTS, ExperimentConfig
+from ..ops import layouts as LY
+from ..ops.native import hip, stream_handle
+from .gocnn import ParamLayout, init_params
+
+INPUT_CP = 40  # 37 planes padded to 5 x 8-channel groups
+
+
+@dataclass
+class ConvPlan:
+    index: int
+    k: int
+    pad: int
+    cin: int
+    cinp: int        # channels of the input frame
+    cout: int
+    bm: int
+    bn: int
+    KP: int          # fwd K (multiple of 64)
+    Mpad: int        # fwd M padding
+    KPw: int         # wgrad K (multiple of 128)
+    Mpad_w: int
+    splits: int
+    KPd: int = 0     # dgrad K
+    Mpad_d: int = 0
+    bm_d: int = 128
+    bn_d: int = 128
+
+
+class HipGoNet:
+    """Static-buffer GoCNN executor for one GPU (one rank)."""
+
+    def __init__(self, cfg: ExperimentConfig, batch: int, device="cuda",
+                 flat_params: Optional[torch.Tensor] = None, num_cus: Optional[int] = None,
+                 global_batch: Optional[int] = None):
+        if cfg.numLayers < 2:
+            raise ValueError("HIP executor needs >= 2 layers (conv stack + head)")
+        self.cfg = cfg
+        self.B = batch
+        self.global_batch = global_batch or batch
+        self.device = torch.device(device)
+        self.h = hip()
+        self.layout = ParamLayout(cfg)
+        if num_cus is None:
+            num_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        self.num_cus = num_cus
+        L = self.layout.layers
+        self.L = len(L)
+        npix = batch * NUM_POINTS
+        self.npix = npix
+        dev = self.device
+
+        # ---- parameters / optimizer state ----
+        if flat_params is None:
+            flat_params = init_params(self.layout, cfg.seed)
+        self.params = flat_params.to(dev, torch.float32).contiguous()
+        self.grads = torch.zeros_like(self.params)
+        self.lr = torch.tensor([cfg.rate], dtype=torch.float64, device=dev)
+        self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ms = None
+        if cfg.optimizer == "rmsprop":
+            self.ms = torch.ones_like(self.params)
+
+        # ---- per-layer plans + bf16 operand weights ----
+        self.plans: List[ConvPlan] = []
+        self.wf: List[torch.Tensor] = []
+        self.wd: List[Optional[torch.Tensor]] = []
+        for spec in L[:-1]:
+            cinp = INPUT_CP if spec.index == 0 else spec.cin
+            bm, bn = LY.pick_tiles(npix, spec.cout, num_cus)
+            KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
+            Mpad_w = LY.round_up(spec.cout, 128)
+            splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
+            p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
+                         Mpad, KPw, Mpad_w, splits)
+            self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
+            if spec.index > 0:
+                bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
+                KPd, _, Mpad_d = LY.conv_dims(spec.k, spec.cout, spec.cin, bm_d)
+                p.KPd, p.Mpad_d, p.bm_d, p.bn_d = KPd, Mpad_d, bm_d, bn_d
+                self.wd.append(torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=dev))
+            else:
+                self.wd.append(None)
+            self.plans.append(p)
+        self.head = L[-1]
+
+        # ---- activation / gradient frames ----
+        B = batch
+        pads = [s.pad for s in L]
+        self.x0 = LY.alloc_frame(B, INPUT_CP, pads[0], dev)
+        # act[i]: output of layer i, framed with the pad of layer i+1
+        self.act = [LY.alloc_frame(B, L[i].cout, pads[i + 1], dev) for i in range(self.L - 1)]
+        # dz[i]: d loss / d pre-activation of layer i, framed with layer i's pad (>=1)
+        self.dz = [LY.alloc_frame(B, L[i].cout, max(1, pads[i]), dev) for i in range(self.L - 1)]
+        slab = max(p.splits * p.Mpad_w * p.KPw for p in self.plans)
+        self.slab = torch.empty(slab, dtype=torch.float32, device=dev)
+
+        # ---- step I/O ----
+        self.planes = torch.zeros((B, 9, NUM_POINTS), dtype=torch.uint8, device=dev)
+        self.player = torch.ones(B, dtype=torch.uint8, device=dev)
+        self.rank = torch.ones(B, dtype=torch.uint8, device=dev)
+        self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.loss = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.pred = torch.zeros(B, dtype=torch.int32, device=dev)
+
+        self._refresh_table = self._build_refresh_table()
+        self._build_plans()
+        self.refresh_weights()
+        self.grad_hooks: List[Tuple[int, Callable[[], None]]] = []  # (after bwd layer i, fn)
+
+    # ------------------------------------------------------------------ planning
+    def _build_refresh_table(self) -> np.ndarray:
+        rows = []
+        for p, wf, wd in zip(self.plans, self.wf, self.wd):
+            spec = self.layout.layers[p.index]
+            w = self.params[spec.w_off:spec.w_off + spec.w_numel]
+            rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0,
+                         p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd, 0])
+        return np.ascontiguousarray(np.array(rows, dtype=np.int64))
+
+    def _build_plans(self):
+        h, lay = self.h, self.layout
+        P = self.params.data_ptr()
+        G = self.grads.data_ptr()
+        f4 = 4
+        self._pre: List[Tuple[Callable, tuple]] = []
+        self._fwd: List[Tuple[Callable, tuple]] = []
+        self._bwd: List[List[Tuple[Callable, tuple]]] = []  # per layer (index order)
+        self._pre.append((h.expand_features, (self.planes.data_ptr(), self.player.data_ptr(),
+                                              self.rank.data_ptr(), self.x0.data_ptr(), self.B,
+                                              self.plans[0].pad, INPUT_CP)))
+        for p in self.plans:
+            spec = lay.layers[p.index]
+            xin = self.x0 if p.index == 0 else self.act[p.index - 1]
+            x_pad = spec.pad
+            y_pad = lay.layers[p.index + 1].pad
+            self._fwd.append((h.conv_nt, (h.EPI_FWD, p.k, p.bm, p.bn, self.wf[p.index].data_ptr(),
+                                          p.KP, p.cout, p.Mpad, xin.data_ptr(), x_pad, p.cinp,
+                                          self.npix, self.act[p.index].data_ptr(), y_pad,
+                                          P + spec.b_off * f4, P + spec.pos_off * f4, 0, 0)))
+        hd = self.head
+        hx = self.act[-1]
+        self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
+                                     P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
+                                     self.labels.data_ptr(), self.loss.data_ptr(),
+                                     self.pred.data_ptr(), 0, self.dz[-1].data_ptr(),
+                                     max(1, lay.layers[-2].pad), G + hd.w_off * f4,
+                                     G + hd.b_off * f4, G + hd.pos_off * f4,
+                                     int(self.cfg.head_relu), 1.0 / self.global_batch))
+        self._head_eval = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
+                                    P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
+                                    self.labels.data_ptr(), self.loss.data_ptr(),
+                                    self.pred.data_ptr(), 0, 0, 0, 0, 0, 0,
+                                    int(self.cfg.head_relu), 1.0 / self.global_batch))
+        for p in self.plans:
+            spec = lay.layers[p.index]
+            i = p.index
+            ops = []
+            dzp = max(1, spec.pad)
+            ops.append((h.bias_grad, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
+                                      G + spec.pos_off * f4, G + spec.b_off * f4)))
+            xin = self.x0 if i == 0 else self.act[i - 1]
+            ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                       xin.data_ptr(), spec.pad, p.cinp, self.npix, p.KPw,
+                                       p.splits, self.slab.data_ptr())))
+            ops.append((h.wgrad_reduce, (self.slab.data_ptr(), G + spec.w_off * f4, p.splits,
+                                         p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp)))
+            if i > 0:
+                prev = lay.layers[i - 1]
+                ops.append((h.conv_nt, (h.EPI_DGRAD, p.k, p.bm_d, p.bn_d,
+                                        self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
+                                        self.dz[i].data_ptr(), dzp, p.cout, self.npix,
+                                        self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
+                                        self.act[i - 1].data_ptr(), spec.pad)))
+            self._bwd.append(ops)
+
+    # ------------------------------------------------------------------ execution
+    @staticmethod
+    def _run(ops, s):
+        for f, a in ops:
+            f(*a, s)
+
+    def set_batch(self, planes: torch.Tensor, player: torch.Tensor, rank: torch.Tensor,
+                  labels: torch.Tensor, non_blocking: bool = True):
+        """Copy one batch into the static input buffers (device or pinned host tensors)."""
+        self.planes.copy_(planes.reshape(self.B, 9, NUM_POINTS), non_blocking=non_blocking)
+        self.player.copy_(player, non_blocking=non_blocking)
+        self.rank.copy_(rank, non_blocking=non_blocking)
+        self.labels.copy_(labels, non_blocking=non_blocking)
+
+    def forward(self):
+        s = stream_handle()
+        self._run(self._pre, s)
+        self._run(self._fwd, s)
+
+    def forward_backward(self):
+        """Loss/pred into self.loss/self.pred; gradients (mean over global batch) in
+        self.grads.  Registered grad hooks fire right after their layer's wgrad."""
+        s = stream_handle()
+        self.grads.zero_()
+        self._run(self._pre, s)
+        self._run(self._fwd, s)
+        f, a = self._head_train
+        f(*a, s)
+        hooks = dict()
+        for li, fn in self.grad_hooks:
+            hooks.setdefault(li, []).append(fn)
+        for fn in hooks.get(self.L - 1, []):
+            fn()
+        for i in range(self.L - 2, -1, -1):
+            ops = self._bwd[i]
+            self._run(ops[:3], s)          # bias grads + wgrad + reduce: layer i grads final
+            for fn in hooks.get(i, []):
+                fn()
+            self._run(ops[3:], s)          # dgrad into layer i-1
+
+    def evaluate(self):
+        s = stream_handle()
+        self._run(self._pre, s)
+        self._run(self._fwd, s)
+        f, a = self._head_eval
+        f(*a, s)
+
+    def optimizer_step(self, grad_scale: float = 1.0):
+        s = stream_handle()
+        n = self.layout.numel
+        if self.ms is not None:
+            self.h.rmsprop(self.params.data_ptr(), self.grads.data_ptr(), self.ms.data_ptr(), n,
+                           self.lr.data_ptr(), float(self.cfg.rmsprop_decay), grad_scale, s)
+        else:
+            self.h.sgd(self.params.data_ptr(), self.grads.data_ptr(), n, self.lr.data_ptr(),
+                       grad_scale, s)
+        self.h.lr_decay(self.lr.data_ptr(), float(self.cfg.rateDecay),
+                        self.step_count.data_ptr(), s)
+        self.refresh_weights()
+
+    def refresh_weights(self):
+        self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table),
+                              stream_handle())
+
+    def train_step(self):
+        self.forward_backward()
+        self.optimizer_step()
+
+    # ------------------------------------------------------------------ helpers
+    def mean_loss(self) -> torch.Tensor:
+        return self.loss.sum() / self.B
+
+    def correct(self) -> torch.Tensor:
+        return (self.pred == self.labels).sum()
+
+    def load_params(self, flat: torch.Tensor):
+        self.params.copy_(flat.to(self.params.device, torch.float32))
+        self.refresh_weights()
+
+    def state_tensors(self):
+        return {"params": self.params, "lr": self.lr, "step": self.step_count}
+
+    def memory_bytes(self) -> int:
+        ts = [self.params, self.grads, self.slab, self.x0, *self.act, *self.dz, *self.wf,
+              *[w for w in self.wd if w is not None]]
+        return sum(t.numel() * t.element_size() for t in ts)
+
+
+class GraphedStep:
+    """Capture HipGoNet.train_step (fwd+bwd+optimizer) into one hipGraph and replay it.
+
+    Inputs must be written into ``net.planes/player/rank/labels`` before ``replay()``."""
+
+    def __init__(self, net: HipGoNet, warmup: int = 2, with_optimizer: bool = True):
+        self.net = net
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                net.forward_backward()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            net.forward_backward()
+            if with_optimizer:
+                net.optimizer_step()
+        torch.cuda.synchronize()
+
+    def replay(self):
+        self.graph.replay()
+
+
+class SegmentedStep:
+    """Training step as hipGraph segments with gradient-bucket collectives between them.
+
+    Segment boundaries sit right after the wgrad of the lowest layer of each DP bucket
+    (see ``parallel.dp.make_buckets``); the bucket's all-reduce is issued between two
+    segment replays so RCCL (own stream) overlaps the next segment's backward.  With no
+    bucketer the whole step is one graph (same as ``GraphedStep``)."""
+
+    def __init__(self, net: HipGoNet, bucketer=None, use_graphs: bool = True, warmup: int = 1):
+        self.net = net
+        self.bucketer = bucketer
+        fire_after = {}
+        if bucketer is not None:
+            for bi, (_, _, first_layer) in enumerate(bucketer.buckets):
+                fire_after.setdefault(first_layer, []).append(bi)
+        segs: List[Tuple[List[Callable[[], None]], List[int]]] = []
+        cur: List[Callable[[], None]] = []
+
+        def emit(fn):
+            cur.append(fn)
+
+        emit(lambda: net.grads.zero_())
+        emit(lambda: net._run(net._pre, stream_handle()))
+        emit(lambda: net._run(net._fwd, stream_handle()))
+        emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
+        if net.L - 1 in fire_after:
+            segs.append((cur, fire_after[net.L - 1]))
+            cur = []
+        for i in range(net.L - 2, -1, -1):
+            ops = net._bwd[i]
+            emit(lambda ops=ops: net._run(ops[:3], stream_handle()))
+            if i in fire_after:
+                segs.append((cur, fire_after[i]))
+                cur = []
+            if len(ops) > 3:
+                emit(lambda ops=ops: net._run(ops[3:], stream_handle()))
+        if cur:
+            segs.append((cur, []))
+        self.segments = segs
+        self.use_graphs = use_graphs
+        self.graphs = []
+        self.opt_graph = None
+        if use_graphs:
+            self._capture(warmup)
+
+    @staticmethod
+    def _call_all(fns):
+        for f in fns:
+            f()
+
+    def _capture(self, warmup: int):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                for fns, _ in self.segments:
+                    self._call_all(fns)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for fns, _ in self.segments:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._call_all(fns)
+            self.graphs.append(g)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.net.optimizer_step()
+        self.opt_graph = g
+        torch.cuda.synchronize()
+
+    def __call__(self):
+        for si, (fns, fire) in enumerate(self.segments):
+            if self.use_graphs:
+                self.graphs[si].replay()
+            else:
+                self._call_all(fns)
+            if self.bucketer is not None:
+                for b in fire:
+                    self.bucketer.fire(b)
+        if self.bucketer is not None:
+            self.bucketer.wait()
+        if self.use_graphs:
+            self.opt_graph.replay()
+        else:
+            self.net.optimizer_step()

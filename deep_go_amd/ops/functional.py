@@ -1,0 +1,169 @@
+"""Functional (allocate-and-call) wrappers around the HIP kernels.
+
+Used by the kernel unit tests and by ad-hoc tools; the training executor
+(``models/hip_model.py``) calls the same kernels with pre-planned static buffers.
+Inputs/outputs here are ordinary NCHW / OHWI tensors so each op can be compared with a
+plain PyTorch fp32 oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import layouts as LY
+from .native import hip, stream_handle
+
+NPTS = 361
+
+
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def conv_forward(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: str = "fwd",
+                 tiles=None, cinp: int | None = None) -> torch.Tensor:
+    """x [B,Cin,19,19] (any float), w OHWI fp32 [Cout,k,k,Cin] -> fp32 NCHW output.
+
+    epi='fwd': relu(conv + bias[co] + posb[p][co]);  epi='linear': conv only."""
+    h = hip()
+    dev = w.device
+    B, cin = x.shape[:2]
+    cout, k, _, _ = w.shape
+    pad = (k - 1) // 2
+    cinp = cinp or LY.round_up(cin, 8)
+    npix = B * NPTS
+    bm, bn = tiles or LY.pick_tiles(npix, cout)
+    KP, _, Mpad = LY.conv_dims(k, cinp, cout, bm)
+    xf = LY.to_frame(x.to(dev), pad, cinp)
+    yf = LY.alloc_frame(B, cout, 1, dev)
+    A = LY.fwd_weight(w.float(), cinp, KP, Mpad)
+    e = {"fwd": h.EPI_FWD, "linear": h.EPI_LINEAR}[epi]
+    if e == h.EPI_FWD:
+        bias = bias.float().contiguous().to(dev)
+        posb = posb.float().contiguous().to(dev)
+    h.conv_nt(e, k, bm, bn, A.data_ptr(), KP, cout, Mpad, xf.data_ptr(), pad, cinp, npix,
+              yf.data_ptr(), 1, _ptr(bias), _ptr(posb), 0, 0, stream_handle())
+    return LY.from_frame(yf, 1, cout)
+
+
+def conv_dgrad(dz: torch.Tensor, w: torch.Tensor, aux: torch.Tensor, tiles=None) -> torch.Tensor:
+    """dz [B,Cout,19,19], w OHWI [Cout,k,k,Cin], aux [B,Cin,19,19] (activation whose >0
+    mask gates the result) -> dX*(aux>0) fp32 NCHW [B,Cin,19,19]."""
+    h = hip()
+    dev = w.device
+    B, cout = dz.shape[:2]
+    _, k, _, cin = w.shape
+    pad = (k - 1) // 2
+    npix = B * NPTS
+    bm, bn = tiles or LY.pick_tiles(npix, cin)
+    KPd, _, Mpad = LY.conv_dims(k, cout, cin, bm)
+    dzf = LY.to_frame(dz.to(dev), max(1, pad))
+    auxf = LY.to_frame(aux.to(dev), pad)
+    out = LY.alloc_frame(B, cin, 1, dev)
+    A = LY.dgrad_weight(w.float(), KPd, Mpad)
+    h.conv_nt(h.EPI_DGRAD, k, bm, bn, A.data_ptr(), KPd, cin, Mpad, dzf.data_ptr(), max(1, pad),
+              cout, npix, out.data_ptr(), 1, 0, 0, auxf.data_ptr(), pad, stream_handle())
+    return LY.from_frame(out, 1, cin)
+
+
+def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = None,
+               cinp: int | None = None) -> torch.Tensor:
+    """dW[co][kh][kw][ci] = sum_{b,p} dz[b,co,p] * x[b,ci,p+off] (fp32 OHWI)."""
+    h = hip()
+    dev = dz.device
+    B, cout = dz.shape[:2]
+    cin = x.shape[1]
+    cinp = cinp or LY.round_up(cin, 8)
+    pad = (k - 1) // 2
+    npix = B * NPTS
+    _, KPw, _ = LY.conv_dims(k, cinp, cout, 128)
+    Mpad = LY.round_up(cout, 128)
+    splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad)
+    dzf = LY.to_frame(dz, max(1, pad))
+    xf = LY.to_frame(x.to(dev), pad, cinp)
+    slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)
+    out = torch.empty((cout, k, k, cin), dtype=torch.float32, device=dev)
+    s = stream_handle()
+    h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, npix, KPw,
+                 splits, slab.data_ptr(), s)
+    h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp, s)
+    return out
+
+
+def head(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: torch.Tensor,
+         labels: torch.Tensor | None, head_relu: bool = True, train: bool = True,
+         grad_scale: float | None = None):
+    """Fused head.  x [B,C,19,19]; w [1,k,k,C].  Returns dict with loss[B], pred[B],
+    logp[B,361] and (train) dz [B,C,19,19] (masked by x>0), gw, gbias, gposb."""
+    h = hip()
+    dev = w.device
+    B, C = x.shape[:2]
+    k = w.shape[1]
+    pad = (k - 1) // 2
+    xf = LY.to_frame(x.to(dev), pad)
+    loss = torch.zeros(B, dtype=torch.float32, device=dev)
+    pred = torch.zeros(B, dtype=torch.int32, device=dev)
+    logp = torch.zeros((B, NPTS), dtype=torch.float32, device=dev)
+    lab = labels.to(dev, torch.int32).contiguous() if labels is not None else None
+    out = {"loss": loss, "pred": pred, "logp": logp}
+    dzf = gw = gb = gp = None
+    if train:
+        dzf = LY.alloc_frame(B, C, 1, dev)
+        gw = torch.zeros(k * k * C, dtype=torch.float32, device=dev)
+        gb = torch.zeros(1, dtype=torch.float32, device=dev)
+        gp = torch.zeros(NPTS, dtype=torch.float32, device=dev)
+    h.head(k, xf.data_ptr(), pad, C, B, w.float().contiguous().data_ptr(),
+           bias.float().contiguous().data_ptr(), posb.float().contiguous().data_ptr(), _ptr(lab),
+           loss.data_ptr(), pred.data_ptr(), logp.data_ptr(), _ptr(dzf), 1, _ptr(gw), _ptr(gb),
+           _ptr(gp), int(head_relu), float(grad_scale if grad_scale is not None else 1.0 / B),
+           stream_handle())
+    if train:
+        out.update(dz=LY.from_frame(dzf, 1, C), gw=gw.view(1, k, k, C), gbias=gb, gposb=gp)
+    return out
+
+
+def expand_features(planes: torch.Tensor, player: torch.Tensor, rank: torch.Tensor,
+                    pad: int = 2, CP: int = 40) -> torch.Tensor:
+    """planes uint8 [B,9,19,19] -> float NCHW [B,CP,19,19] via the GPU expansion kernel."""
+    h = hip()
+    dev = torch.device("cuda")
+    B = planes.shape[0]
+    pl = planes.to(dev, torch.uint8).contiguous()
+    py = player.to(dev, torch.uint8).contiguous()
+    rk = rank.to(dev, torch.uint8).contiguous()
+    out = LY.alloc_frame(B, CP, pad, dev)
+    h.expand_features(pl.data_ptr(), py.data_ptr(), rk.data_ptr(), out.data_ptr(), B, pad, CP,
+                      stream_handle())
+    return LY.from_frame(out, pad, CP)
+
+
+def bias_grad(dz: torch.Tensor):
+    h = hip()
+    B, C = dz.shape[:2]
+    dzf = LY.to_frame(dz, 1)
+    gp = torch.zeros((NPTS, C), dtype=torch.float32, device=dz.device)
+    gb = torch.zeros(C, dtype=torch.float32, device=dz.device)
+    h.bias_grad(dzf.data_ptr(), B, C, 1, gp.data_ptr(), gb.data_ptr(), stream_handle())
+    return gp, gb
+
+
+def sgd_(p: torch.Tensor, g: torch.Tensor, lr: float, decay: float, steps: int = 1):
+    h = hip()
+    lrt = torch.tensor([lr], dtype=torch.float64, device=p.device)
+    s = stream_handle()
+    for _ in range(steps):
+        h.sgd(p.data_ptr(), g.data_ptr(), p.numel(), lrt.data_ptr(), 1.0, s)
+        h.lr_decay(lrt.data_ptr(), decay, 0, s)
+    return lrt
+
+
+def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0, Mpad_d: int = 0):
+    h = hip()
+    cout, k, _, cin = w.shape
+    wf = torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=w.device)
+    wd = torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=w.device) if KPd else None
+    tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0]],
+                   dtype=np.int64)
+    h.weight_refresh(tbl.ctypes.data, 1, stream_handle())
+    torch.cuda.synchronize()
+    return wf, wd

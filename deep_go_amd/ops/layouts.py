@@ -1,0 +1,103 @@
+"""Tensor layouts shared by the HIP kernels and their tests.
+
+* Activation frames: zero-bordered NHWC bf16 ``[B][19+2p][19+2p][C]``.  The border is
+  the conv zero padding (the reference's ``nn.SpatialZeroPadding``,
+  ``experiments.lua:137``); kernels only ever write the 19x19 interior.
+* Forward weights (MFMA A operand): bf16 ``[Mpad][KP]`` with ``k = tap*cinp + ci``.
+* Dgrad weights: bf16 ``[CinPad][KPd]`` with ``k = (T-1-tap)*cout + co`` (flipped taps).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+BOARD = 19
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def frame_dim(pad: int) -> int:
+    return BOARD + 2 * pad
+
+
+def alloc_frame(B: int, C: int, pad: int, device, dtype=torch.bfloat16) -> torch.Tensor:
+    F = frame_dim(pad)
+    return torch.zeros((B, F, F, C), dtype=dtype, device=device)
+
+
+def frame_interior(frame: torch.Tensor, pad: int) -> torch.Tensor:
+    return frame[:, pad:pad + BOARD, pad:pad + BOARD, :]
+
+
+def to_frame(x_nchw: torch.Tensor, pad: int, C: int | None = None, device=None) -> torch.Tensor:
+    B, c = x_nchw.shape[:2]
+    C = C or c
+    fr = alloc_frame(B, C, pad, device or x_nchw.device)
+    frame_interior(fr, pad)[..., :c] = x_nchw.permute(0, 2, 3, 1).to(fr.dtype)
+    return fr
+
+
+def from_frame(frame: torch.Tensor, pad: int, C: int) -> torch.Tensor:
+    return frame_interior(frame, pad)[..., :C].permute(0, 3, 1, 2).float()
+
+
+def fwd_weight(w_ohwi: torch.Tensor, cinp: int, KP: int, Mpad: int) -> torch.Tensor:
+    cout, kh, kw, cin = w_ohwi.shape
+    out = torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=w_ohwi.device)
+    tmp = torch.zeros((cout, kh * kw, cinp), dtype=torch.float32, device=w_ohwi.device)
+    tmp[:, :, :cin] = w_ohwi.reshape(cout, kh * kw, cin)
+    out[:cout, :kh * kw * cinp] = tmp.reshape(cout, -1).to(torch.bfloat16)
+    return out
+
+
+def dgrad_weight(w_ohwi: torch.Tensor, KPd: int, Mpad: int) -> torch.Tensor:
+    cout, kh, kw, cin = w_ohwi.shape
+    T = kh * kw
+    out = torch.zeros((Mpad, KPd), dtype=torch.bfloat16, device=w_ohwi.device)
+    # [ci][T-1-t][co]
+    t = w_ohwi.reshape(cout, T, cin).flip(1).permute(2, 1, 0).reshape(cin, T * cout)
+    out[:cin, :T * cout] = t.to(torch.bfloat16)
+    return out
+
+
+def conv_dims(k: int, cin_frame: int, cout: int, bm: int):
+    """K/M padding for a conv whose input frame has ``cin_frame`` channels."""
+    ngroups = k * k * cin_frame // 8
+    KP = round_up(ngroups * 8, 64)
+    KPw = round_up(ngroups * 8, 128)
+    Mpad = round_up(cout, bm)
+    return KP, KPw, Mpad
+
+
+def gpt_magic(d: int) -> int:
+    return (1 << 32) // d + 1
+
+
+def pick_tiles(npix: int, cout: int, num_cus: int = 256) -> tuple[int, int]:
+    """Choose (BM, BN) for the NT conv kernel: minimise quantised rounds x tile cost.
+
+    2 workgroups fit per CU (64-80 KiB LDS each); a partially filled last round costs a
+    whole round.  Larger tiles have better arithmetic intensity (eff factor)."""
+    cands = [(128, 128, 1.0), (128, 192, 1.06), (64, 128, 0.8), (64, 256, 0.9)]
+    best, best_cost = None, math.inf
+    for bm, bn, eff in cands:
+        if cout > 64 and bm == 64:
+            continue
+        if cout <= 64 and bm == 128:
+            continue
+        tiles = math.ceil(npix / bn) * math.ceil(cout / bm)
+        rounds = math.ceil(tiles / (2 * num_cus))
+        cost = rounds * bm * bn / eff
+        if cost < best_cost:
+            best, best_cost = (bm, bn), cost
+    return best
+
+
+def pick_wgrad_splits(npix: int, KPw: int, Mpad: int, num_cus: int = 256) -> int:
+    tiles = (KPw // 128) * (Mpad // 128)
+    target = max(1, (2 * num_cus) // tiles)
+    max_split = max(1, npix // 256)
+    return max(1, min(target, max_split))

@@ -1,0 +1,164 @@
+"""HIP kernel numerics vs plain PyTorch fp32 oracles (SURVEY.md §4.3 'Kernel unit tests').
+
+Inputs are rounded to bf16 first so the oracle sees exactly what the MFMA sees; the
+remaining error is fp32-accumulation order + the bf16 rounding of the output.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def rel_err(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def conv_ref(x, w_ohwi, k):
+    return F.conv2d(x, w_ohwi.permute(0, 3, 1, 2), padding=(k - 1) // 2)
+
+
+@pytest.mark.parametrize("B,cin,cout,k,tiles", [
+    (2, 64, 64, 3, None), (7, 128, 128, 3, None), (3, 40, 128, 5, None), (1, 16, 16, 3, None),
+    (5, 128, 128, 3, (128, 128)), (5, 128, 128, 3, (128, 192)), (4, 256, 256, 3, None),
+    (3, 64, 64, 3, (64, 256)), (2, 128, 128, 1, None)])
+def test_conv_forward_linear(B, cin, cout, k, tiles):
+    torch.manual_seed(0)
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) / (k * (cin ** 0.5)))
+    from deep_go_amd.ops import functional as Fn
+    y = Fn.conv_forward(x, w, epi="linear", tiles=tiles)
+    ref = conv_ref(x, w, k)
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (2, 40, 128, 5), (6, 128, 128, 3)])
+def test_conv_forward_bias_relu(B, cin, cout, k):
+    torch.manual_seed(1)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5))
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y = Fn.conv_forward(x, w, b, pb, epi="fwd")
+    ref = F.relu(conv_ref(x, w, k) + b.view(1, -1, 1, 1) + pb.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (7, 128, 128, 3), (2, 256, 256, 3),
+                                          (2, 16, 16, 3), (4, 128, 64, 3)])
+def test_conv_dgrad(B, cin, cout, k):
+    torch.manual_seed(2)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5))
+    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+    aux = bf(torch.relu(torch.randn(B, cin, 19, 19, device=DEV)))
+    got = Fn.conv_dgrad(dz, w, aux)
+    xr = x.clone().requires_grad_(True)
+    y = conv_ref(xr, w, k)
+    (gx,) = torch.autograd.grad(y, xr, dz)
+    ref = gx * (aux > 0)
+    assert rel_err(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,cin,cout,k,splits", [(3, 64, 64, 3, None), (7, 128, 128, 3, None),
+                                                 (2, 40, 128, 5, 3), (5, 256, 256, 3, None),
+                                                 (1, 16, 16, 3, 1), (2, 128, 128, 1, 2)])
+def test_conv_wgrad(B, cin, cout, k, splits):
+    torch.manual_seed(3)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+    got = Fn.conv_wgrad(dz, x, k, splits=splits)
+    w0 = torch.zeros(cout, k, k, cin, device=DEV, requires_grad=True)
+    y = conv_ref(x, w0, k)
+    (gw,) = torch.autograd.grad(y, w0, dz)
+    assert rel_err(got, gw) < 1e-3
+
+
+@pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True), (2, 32, 1, False),
+                                        (4, 256, 3, True)])
+def test_head(B, C, k, relu):
+    torch.manual_seed(4)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.relu(torch.randn(B, C, 19, 19, device=DEV)))
+    w = torch.randn(1, k, k, C, device=DEV) * 0.05
+    b = torch.randn(1, device=DEV) * 0.1
+    pb = torch.randn(361, device=DEV) * 0.1
+    labels = torch.randint(0, 361, (B,), device=DEV)
+    out = Fn.head(x, w, b, pb, labels, head_relu=relu)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    pr = pb.clone().requires_grad_(True)
+    z = conv_ref(xr, wr, k) + br.view(1, 1, 1, 1) + pr.view(1, 1, 19, 19)
+    if relu:
+        z = torch.relu(z)
+    logp = F.log_softmax(z.reshape(B, 361), 1)
+    loss = F.nll_loss(logp, labels)
+    gx, gw, gb, gp = torch.autograd.grad(loss, [xr, wr, br, pr])
+    assert rel_err(out["logp"], logp) < 1e-4
+    assert torch.allclose(out["loss"].mean(), loss, rtol=1e-4, atol=1e-5)
+    assert (out["pred"].long() == logp.argmax(1)).float().mean() > 0.99
+    assert rel_err(out["dz"], gx * (x > 0)) < 1e-2
+    assert rel_err(out["gw"], gw) < 1e-3
+    assert rel_err(out["gbias"], gb.view(1)) < 1e-3
+    assert rel_err(out["gposb"], gp.view(-1)) < 1e-3
+
+
+def test_expand_features():
+    from deep_go_amd.data.features import expand_batch
+    from deep_go_amd.ops import functional as Fn
+    rng = np.random.default_rng(0)
+    B = 9
+    planes = np.zeros((B, 9, 19, 19), np.uint8)
+    planes[:, 0] = rng.integers(0, 3, (B, 19, 19))
+    for c in range(1, 9):
+        planes[:, c] = rng.integers(0, 12, (B, 19, 19))
+    player = rng.integers(1, 3, B).astype(np.uint8)
+    rank = rng.integers(1, 10, B).astype(np.uint8)
+    got = Fn.expand_features(torch.from_numpy(planes), torch.from_numpy(player),
+                             torch.from_numpy(rank))
+    ref = expand_batch(planes, player, rank)
+    assert torch.equal(got[:, :37].cpu(), torch.from_numpy(ref))
+    assert got[:, 37:].abs().sum().item() == 0
+
+
+def test_bias_grad():
+    from deep_go_amd.ops import functional as Fn
+    dz = bf(torch.randn(13, 128, 19, 19, device=DEV))
+    gp, gb = Fn.bias_grad(dz)
+    ref_p = dz.sum(0).reshape(128, 361).t()
+    assert rel_err(gp, ref_p) < 1e-5
+    assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
+
+
+def test_sgd_and_lr_decay():
+    from deep_go_amd.ops import functional as Fn
+    p = torch.randn(1001, device=DEV)
+    g = torch.randn(1001, device=DEV)
+    p0 = p.clone()
+    lr = Fn.sgd_(p, g, 0.5, 0.1, steps=3)
+    lrs = [0.5, 0.45, 0.405]
+    ref = p0 - sum(lrs) * g
+    assert torch.allclose(p, ref, atol=1e-5)
+    assert abs(lr.item() - 0.5 * 0.9 ** 3) < 1e-12
+
+
+def test_weight_refresh():
+    from deep_go_amd.ops import functional as Fn
+    from deep_go_amd.ops import layouts as LY
+    w = torch.randn(64, 3, 3, 32, device=DEV)
+    KP, _, Mpad = LY.conv_dims(3, 32, 64, 64)
+    KPd, _, Mpad_d = LY.conv_dims(3, 64, 32, 64)
+    wf, wd = Fn.weight_refresh(w, 32, KP, Mpad, KPd, Mpad_d)
+    assert torch.equal(wf, LY.fwd_weight(w, 32, KP, Mpad))
+    assert torch.equal(wd, LY.dgrad_weight(w, KPd, Mpad_d))

@@ -1,0 +1,107 @@
+"""Whole-model checks on the GPU: HipGoNet fwd/bwd vs the fp32 PyTorch oracle with the
+same weights, graph replay == eager, and loss decreasing (SURVEY.md §4.3 model-level)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(layers=4, ch=64, B=5, seed=0, **kw):
+    from deep_go_amd.config import ExperimentConfig
+    from deep_go_amd.data.synthetic import random_planes
+    from deep_go_amd.models.hip_model import HipGoNet
+    cfg = ExperimentConfig(numLayers=layers, channelSize=ch, batchSize=B, seed=seed, **kw)
+    net = HipGoNet(cfg, B, device="cuda")
+    planes, player, rank, labels = random_planes(B, seed=seed + 7)
+    net.set_batch(torch.from_numpy(planes).cuda(), torch.from_numpy(player).cuda(),
+                  torch.from_numpy(rank).cuda(), torch.from_numpy(labels).cuda())
+    return cfg, net, (planes, player, rank, labels)
+
+
+def _oracle(net, data):
+    from deep_go_amd.data.features import expand_batch
+    from deep_go_amd.models.gocnn import reference_forward
+    planes, player, rank, labels = data
+    x = torch.from_numpy(expand_batch(planes, player, rank))
+    # oracle sees the bf16-rounded weights the kernels use
+    flat = net.params.detach().cpu().clone()
+    for spec in net.layout.layers[:-1]:
+        w = flat[spec.w_off:spec.w_off + spec.w_numel]
+        w.copy_(w.to(torch.bfloat16).float())
+    flat.requires_grad_(True)
+    logp = reference_forward(net.layout, flat, x, head_relu=net.cfg.head_relu)
+    loss = F.nll_loss(logp, torch.from_numpy(labels).long())
+    (g,) = torch.autograd.grad(loss, flat)
+    return loss.item(), logp.argmax(1), g
+
+
+@pytest.mark.parametrize("layers,ch,B", [(3, 64, 5), (4, 128, 3), (6, 64, 8)])
+def test_model_matches_oracle(layers, ch, B):
+    cfg, net, data = _setup(layers, ch, B)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, pred_ref, g_ref = _oracle(net, data)
+    assert abs(net.mean_loss().item() - loss_ref) < 2e-2 * max(1.0, abs(loss_ref))
+    g = net.grads.cpu()
+    lay = net.layout
+    for name, off, n in lay.tensor_ranges():
+        a, b = g[off:off + n], g_ref[off:off + n]
+        err = (a - b).norm() / (b.norm() + 1e-12)
+        assert err < 0.08, (name, err.item())
+
+
+def test_graph_replay_matches_eager():
+    from deep_go_amd.models.hip_model import SegmentedStep
+    cfg, net, data = _setup(4, 64, 6)
+    p0 = net.params.clone()
+    net.train_step()
+    torch.cuda.synchronize()
+    p_eager = net.params.clone()
+    lr_eager = net.lr.item()
+    # reset and replay through graphs
+    net.params.copy_(p0)
+    net.lr.fill_(cfg.rate)
+    net.refresh_weights()
+    step = SegmentedStep(net, None, use_graphs=True)
+    net.params.copy_(p0)
+    net.lr.fill_(cfg.rate)
+    net.refresh_weights()
+    step()
+    torch.cuda.synchronize()
+    # atomics make the sums order-dependent: compare with a tolerance
+    d = (net.params - p_eager).abs().max().item()
+    assert d < 1e-5, d
+    assert abs(net.lr.item() - lr_eager) < 1e-15
+
+
+def test_loss_decreases():
+    cfg, net, data = _setup(4, 64, 16, rate=0.2)
+    losses = []
+    for _ in range(40):
+        net.train_step()
+        losses.append(net.mean_loss().item())
+    assert np.isfinite(losses).all()
+    assert losses[-1] < 0.8 * losses[0], (losses[0], losses[-1])
+
+
+def test_rmsprop_step_runs():
+    cfg, net, data = _setup(3, 64, 4, optimizer="rmsprop", rate=1e-3)
+    p0 = net.params.clone()
+    net.train_step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(net.params).all()
+    assert (net.params - p0).abs().max() > 0
+
+
+def test_eval_matches_train_forward():
+    cfg, net, data = _setup(3, 64, 7)
+    net.evaluate()
+    torch.cuda.synchronize()
+    l1 = net.loss.clone()
+    p1 = net.pred.clone()
+    net.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(l1, net.loss)
+    assert torch.equal(p1, net.pred)
