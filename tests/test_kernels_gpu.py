@@ -110,7 +110,7 @@ def test_head(B, C, k, relu):
     assert (out["pred"].long() == logp.argmax(1)).float().mean() > 0.99
     assert rel_err(out["dz"], gx * (x > 0)) < 1e-2
     assert rel_err(out["gw"], gw) < 1e-3
-    assert rel_err(out["gbias"], gb.view(1)) < 1e-3
+    assert (out["gbias"] - gb.view(1)).abs().item() < 1e-3 * max(1.0, gb.abs().item())
     assert rel_err(out["gposb"], gp.view(-1)) < 1e-3
 
 

@@ -77,7 +77,9 @@ def test_graph_replay_matches_eager():
 
 
 def test_loss_decreases():
-    cfg, net, data = _setup(4, 64, 16, rate=0.2)
+    # head_relu=False: with the reference's head ReLU a large LR kills every logit (the
+    # loss then pins at ln(361) exactly, see test_head_relu_dead_logits_quirk)
+    cfg, net, data = _setup(4, 64, 16, rate=0.1, head_relu=False)
     losses = []
     for _ in range(40):
         net.train_step()
@@ -105,3 +107,15 @@ def test_eval_matches_train_forward():
     torch.cuda.synchronize()
     assert torch.allclose(l1, net.loss)
     assert torch.equal(p1, net.pred)
+
+
+def test_head_relu_dead_logits_quirk():
+    """Reference parity quirk: ReLU before LogSoftMax; if every head
+    pre-activation is <= 0 the softmax is uniform and no gradient flows: loss = ln 361."""
+    cfg, net, data = _setup(3, 64, 4)
+    hd = net.layout.layers[-1]
+    net.params[hd.b_off].fill_(-100.0)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    assert abs(net.mean_loss().item() - np.log(361)) < 1e-5
+    assert net.grads.abs().max().item() == 0.0
