@@ -18,19 +18,30 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
                       const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
                       const float* bias, const float* posb, const void* aux, int aux_pad,
                       hipStream_t stream);
+hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
+                         const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
+                         const float* bias, const float* posb, const void* aux, int aux_pad,
+                         hipStream_t stream);
+void dg_conv_board_set_ablate(int mode);
+void dg_conv_wgrad_set_ablate(int mode);
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
-                         int x_pad, int x_C, int Npix, int KP, int splits, float* slab,
+                         int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
-                           int taps, int cin, int cinp, hipStream_t stream);
+                           int taps, int cin, int cinp, const float* bpart, int bchunks,
+                           float* gposb, float* gbias, hipStream_t stream);
+hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n, float* gw,
+                          float* gbias, float* gposb, hipStream_t stream);
 hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                    const float* bias, const float* posb, const int* labels, float* loss,
-                   int* pred, float* logp_out, void* dZ, int dz_pad, float* gw, float* gbias,
-                   float* gposb, int head_relu, float grad_scale, hipStream_t stream);
+                   int* pred, float* logp_out, void* dZ, int dz_pad, float* gw_part,
+                   float* unused, float* dzb, int head_relu, float grad_scale,
+                   hipStream_t stream);
 hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, const uint8_t* rank,
                               void* out, int B, int pad, int CP, hipStream_t s);
-hipError_t dg_bias_grad(const void* dZ, int B, int C, int pad, float* gposb, float* gbias,
-                        hipStream_t s);
+hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* part,
+                                hipStream_t s);
+int dg_bias_chunks(int B);
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
                   hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
@@ -69,18 +80,34 @@ PYBIND11_MODULE(_dghip, m) {
                            aux_pad, S(stream)),
                 "conv_nt");
         });
+  m.def("conv_board",
+        [](int epi, int kw, int bm, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
+           int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb, uintptr_t aux,
+           int aux_pad, uintptr_t stream) {
+          check(dg_conv_board(epi, kw, bm, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C, B,
+                              P<void>(Y), y_pad, P<float>(bias), P<float>(posb), P<void>(aux),
+                              aux_pad, S(stream)),
+                "conv_board");
+        });
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
-                         int x_pad, int x_C, int Npix, int KP, int splits, uintptr_t slab,
+                         int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {
-    check(dg_conv_wgrad(kw, P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, Npix, KP,
+    check(dg_conv_wgrad(kw, P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, B, KP,
                         splits, P<float>(slab), S(stream)),
           "conv_wgrad");
   });
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
-                           int taps, int cin, int cinp, uintptr_t stream) {
+                           int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
+                           uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {
     check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
-                          S(stream)),
+                          P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias), S(stream)),
           "wgrad_reduce");
+  });
+  m.def("head_reduce", [](uintptr_t dzb, uintptr_t gw_part, int B, int n, uintptr_t gw,
+                          uintptr_t gbias, uintptr_t gposb, uintptr_t stream) {
+    check(dg_head_reduce(P<float>(dzb), P<float>(gw_part), B, n, P<float>(gw), P<float>(gbias),
+                         P<float>(gposb), S(stream)),
+          "head_reduce");
   });
   m.def("head", [](int kw, uintptr_t X, int x_pad, int C, int B, uintptr_t w, uintptr_t bias,
                    uintptr_t posb, uintptr_t labels, uintptr_t loss, uintptr_t pred,
@@ -98,11 +125,12 @@ PYBIND11_MODULE(_dghip, m) {
                              P<void>(out), B, pad, CP, S(stream)),
           "expand_features");
   });
-  m.def("bias_grad", [](uintptr_t dZ, int B, int C, int pad, uintptr_t gposb, uintptr_t gbias,
-                        uintptr_t stream) {
-    check(dg_bias_grad(P<void>(dZ), B, C, pad, P<float>(gposb), P<float>(gbias), S(stream)),
-          "bias_grad");
+  m.def("bias_grad_partial", [](uintptr_t dZ, int B, int C, int pad, uintptr_t part,
+                                uintptr_t stream) {
+    check(dg_bias_grad_partial(P<void>(dZ), B, C, pad, P<float>(part), S(stream)),
+          "bias_grad_partial");
   });
+  m.def("bias_chunks", [](int B) { return dg_bias_chunks(B); });
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
                   uintptr_t stream) {
     check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, S(stream)), "sgd");
@@ -119,6 +147,9 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("weight_refresh", [](uintptr_t table, int n, uintptr_t stream) {
     check(dg_weight_refresh(P<long long>(table), n, S(stream)), "weight_refresh");
   });
+  m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
+        "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
+  m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
 }

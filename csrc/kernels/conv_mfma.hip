@@ -45,14 +45,14 @@ struct ConvNTArgs {
   int aux_pad;
   int ngroups;         // valid k-groups = KW*KW*x_C/8
   int gpt;             // k-groups per tap = x_C/8
-  uint32_t gpt_magic;  // floor(2^32/gpt)+1
+  uint64_t gpt_magic;  // fastdiv magic for gpt
 };
 
 // Byte offset (relative to the pixel centre) of k-group kg.
 template <int KW>
 DG_DEV int koff_of(int kg, const ConvNTArgs& a) {
   if (kg >= a.ngroups) return 0;
-  const int t = (int)__umulhi((uint32_t)kg, a.gpt_magic);
+  const int t = (int)fastdiv((uint32_t)kg, a.gpt_magic);
   const int c8 = kg - t * a.gpt;
   constexpr int R = (KW - 1) / 2;
   const int dh = t / KW - R;
@@ -147,36 +147,56 @@ conv_nt_kernel(ConvNTArgs a) {
   }
 
   // ---- epilogue ----
+  // all global loads (bias / pos_bias / ReLU mask) issued before any use (see conv_board)
   const int y_C = a.M;
+  int pb_[NF], bb_[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     const int n = n_tile + wn * NF * 16 + j * 16 + lr;
-    if (n >= a.Npix) continue;
-    const int b = n / NPTS;
-    const int p = n - b * NPTS;
+    const int nn = n < a.Npix ? n : 0;
+    bb_[j] = nn / NPTS;
+    pb_[j] = n < a.Npix ? nn - bb_[j] * NPTS : -1;
+  }
+  f32x4 bias_v[MF];
+  f32x4 pos_v[NF][MF];
+  uint2 mask_v[NF][MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int co = m_tile + wm * MF * 16 + i * 16 + lq * 4;
+    const int coc = co < a.M ? co : 0;
+    if constexpr (EPI == EPI_FWD) bias_v[i] = *(const f32x4*)(a.bias + coc);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = pb_[j] < 0 ? 0 : pb_[j];
+      if constexpr (EPI == EPI_FWD) pos_v[j][i] = *(const f32x4*)(a.posb + p * a.M + coc);
+      if constexpr (EPI == EPI_DGRAD) {
+        const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+        mask_v[j][i] = *(const uint2*)(a.aux + frame_off(bb_[j], h, w, a.aux_pad, y_C) + coc * 2);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    if (pb_[j] < 0) continue;
+    const int b = bb_[j];
+    const int p = pb_[j];
     const int h = p / BOARD;
     const int w = p - h * BOARD;
     const uint32_t yo = frame_off(b, h, w, a.y_pad, y_C);
-    uint32_t ao = 0;
-    if constexpr (EPI == EPI_DGRAD) ao = frame_off(b, h, w, a.aux_pad, y_C);
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       const int co = m_tile + wm * MF * 16 + i * 16 + lq * 4;
       if (co >= a.M) continue;
       f32x4 v = acc[i][j];
       if constexpr (EPI == EPI_FWD) {
-        const f32x4 bb = *(const f32x4*)(a.bias + co);
-        const f32x4 pb = *(const f32x4*)(a.posb + p * a.M + co);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bb[r] + pb[r], 0.f);
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bias_v[i][r] + pos_v[j][i][r], 0.f);
       } else if constexpr (EPI == EPI_DGRAD) {
-        const uint2 m = *(const uint2*)(a.aux + ao + co * 2);
-        // bf16 > 0  <=>  sign bit clear and non-zero
-        const uint32_t m01 = m.x, m23 = m.y;
-        if ((m01 & 0xFFFFu) == 0 || (m01 & 0x8000u)) v[0] = 0.f;
-        if ((m01 >> 16) == 0 || (m01 & 0x80000000u)) v[1] = 0.f;
-        if ((m23 & 0xFFFFu) == 0 || (m23 & 0x8000u)) v[2] = 0.f;
-        if ((m23 >> 16) == 0 || (m23 & 0x80000000u)) v[3] = 0.f;
+        const uint2 m = mask_v[j][i];
+        if ((m.x & 0xFFFFu) == 0 || (m.x & 0x8000u)) v[0] = 0.f;
+        if ((m.x >> 16) == 0 || (m.x & 0x80000000u)) v[1] = 0.f;
+        if ((m.y & 0xFFFFu) == 0 || (m.y & 0x8000u)) v[2] = 0.f;
+        if ((m.y >> 16) == 0 || (m.y & 0x80000000u)) v[3] = 0.f;
       }
       uint2 o;
       o.x = pack_bf16x2(v[0], v[1]);
@@ -202,7 +222,9 @@ struct WgradArgs {
   int px_per_split; // multiple of 64
   int x_pad, x_C;
   int ngroups, gpt;
-  uint32_t gpt_magic;
+  uint64_t gpt_magic;
+  int ablate;  // diagnostics: 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no slab store, 16 no barrier
+  int ktiles, mtiles, splits;  // logical grid (launched flat, XCD-remapped)
 };
 
 DG_DEV int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
@@ -210,7 +232,7 @@ DG_DEV int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 template <int KW>
 DG_DEV int koff_wg(int kg, const WgradArgs& a) {
   if (kg >= a.ngroups) return 0;
-  const int t = (int)__umulhi((uint32_t)kg, a.gpt_magic);
+  const int t = (int)fastdiv((uint32_t)kg, a.gpt_magic);
   const int c8 = kg - t * a.gpt;
   constexpr int R = (KW - 1) / 2;
   const int dh = t / KW - R;
@@ -231,9 +253,22 @@ conv_wgrad_kernel(WgradArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int k_tile = blockIdx.x * BN;
-  const int m_tile = blockIdx.y * BM;
-  const int n_begin = blockIdx.z * a.px_per_split;
+  // XCD-aware remap (cdna guide T1): hardware dispatch round-robins flat block ids over the
+  // 8 XCDs (private L2 each).  Give every XCD a contiguous range of logical work items so
+  // the k-tiles sharing a pixel split (same dZ rows, overlapping X rows) run together on
+  // one XCD and hit its L2, instead of re-streaming from the Infinity Cache.
+  const int nwg = a.ktiles * a.mtiles * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, slot = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int kt = lid % a.ktiles;
+  const int rest = lid / a.ktiles;
+  const int mt = rest % a.mtiles;
+  const int zsplit = rest / a.mtiles;
+  const int k_tile = kt * BN;
+  const int m_tile = mt * BM;
+  const int n_begin = zsplit * a.px_per_split;
   int n_end = n_begin + a.px_per_split;
   if (n_end > a.Npix) n_end = a.Npix;
   const int nsteps = (n_end - n_begin + BKN - 1) / BKN;
@@ -253,6 +288,7 @@ conv_wgrad_kernel(WgradArgs a) {
   }
 
   auto stage = [&](int buf, int step) {
+    if (a.ablate & 4) return;
     char* sA = smem + buf * STAGE;
     char* sB = sA + T_BYTES;
 #pragma unroll
@@ -260,7 +296,7 @@ conv_wgrad_kernel(WgradArgs a) {
       const int r = (wave * 4 + i) * 4 + r_in;
       int n = n_begin + step * BKN + r;
       const bool ok = n < n_end;
-      if (!ok) n = n_begin;  // valid address; contribution zeroed below via dz row mask
+      if (!ok) n = n_begin;  // valid address; the dZ row reads the zero border instead
       const int b = n / NPTS;
       const int p = n - b * NPTS;
       const int h = p / BOARD;
@@ -292,9 +328,19 @@ conv_wgrad_kernel(WgradArgs a) {
     if (st + 1 < nsteps) stage(buf ^ 1, st + 1);
     const char* sA = smem + buf * STAGE;
     const char* sB = sA + T_BYTES;
+    // all 32 transposed fragment reads of the step first (distinct registers), then the
+    // 32 MFMAs: the scheduler may not interleave them back into read->wait->mfma bursts.
+    s16x4 ta[2][2][4], tb[2][2][4];
+    if (a.ablate & 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ta[kk][half][i] = tb[kk][half][i] = s16x4{};
+    } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int row = kk * 32 + 8 * g + 4 * half + q;
@@ -302,32 +348,61 @@ conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = (wm * 64 + i * 16) / 8 + (pp >> 1);
-          const s16x4 t = lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
-          s16x8 tmp = __builtin_bit_cast(s16x8, af[i]);
-          tmp[4 * half + 0] = t[0]; tmp[4 * half + 1] = t[1];
-          tmp[4 * half + 2] = t[2]; tmp[4 * half + 3] = t[3];
-          af[i] = __builtin_bit_cast(bf16x8, tmp);
+          ta[kk][half][i] =
+              lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int c = (wn * 64 + j * 16) / 8 + (pp >> 1);
-          const s16x4 t = lds_read_tr((const LDS_AS char*)(sB + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
-          s16x8 tmp = __builtin_bit_cast(s16x8, bfr[j]);
-          tmp[4 * half + 0] = t[0]; tmp[4 * half + 1] = t[1];
-          tmp[4 * half + 2] = t[2]; tmp[4 * half + 3] = t[3];
-          bfr[j] = __builtin_bit_cast(bf16x8, tmp);
+          tb[kk][half][j] =
+              lds_read_tr((const LDS_AS char*)(sB + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
         }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (a.ablate & 1) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(ta[kk][half][i]), "v"(tb[kk][half][i]));
+    } else
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s16x4 lo = ta[kk][0][i], hi = ta[kk][1][i];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x4 lo = tb[kk][0][j], hi = tb[kk][1][j];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);  // DMA wait + barrier stay below the MFMAs
+    if (!(a.ablate & 16)) __syncthreads();
+  }
+  if (a.ablate & 8) {
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) keep += acc[i][j][0];
+    if (keep == 1234.5f) a.slab[0] = keep;
+    return;
   }
 
   // slab store: D rows = co, cols = k
-  float* slab = a.slab + (size_t)blockIdx.z * a.Mpad * a.KP;
+  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -343,21 +418,71 @@ conv_wgrad_kernel(WgradArgs a) {
 }
 
 // Sum the split-K slabs and scatter into the fp32 master-gradient layout OHWI
-// [co][kh][kw][ci] (only ci < Cin, co < M).  out is overwritten.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                    int splits, int M, int Mpad, int KP, int taps, int cin,
-                                    int cinp) {
-  const int total = M * taps * cin;
+// [co][kh][kw][ci] (only ci < Cin, co < M).  out is overwritten.  Each thread owns 4
+// consecutive k of one co (16-byte slab loads), the split loop is unrolled by 4 so
+// several loads are in flight; the slabs are normally still resident in the Infinity
+// Cache when this runs.
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits, int M,
+                    int Mpad, int KP, int taps, int cin, int cinp, const float* __restrict__ bpart,
+                    int bchunks, float* __restrict__ gposb, float* __restrict__ gbias,
+                    int main_blocks) {
+  const int pos_blocks = (NPTS * M + 255) / 256;
+  if ((int)blockIdx.x >= main_blocks + pos_blocks) {
+    // gbias[c] = sum over (chunk, row) of rowpart; one workgroup per channel
+    __shared__ float s_r[4];
+    const int c = blockIdx.x - main_blocks - pos_blocks;
+    const float* rp = bpart + (size_t)bchunks * NPTS * M;  // rowpart [bchunks][19][M]
+    float s0 = 0.f;
+    for (int r = threadIdx.x; r < bchunks * BOARD; r += 256) s0 += rp[(size_t)r * M + c];
+    s0 = wave_sum(s0);
+    if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = s0;
+    __syncthreads();
+    if (threadIdx.x == 0) gbias[c] = (s_r[0] + s_r[1]) + (s_r[2] + s_r[3]);
+    return;
+  }
+  if ((int)blockIdx.x >= main_blocks) {
+    // second pass of the bias gradients (see bias_grad_partial_kernel):
+    //   gposb[p][c] = sum_chunks part[chunk][p][c]; gbias[c] = sum_{chunk,h} rowpart[chunk][h][c]
+    const int j = (blockIdx.x - main_blocks) * 256 + threadIdx.x;
+    const int np = NPTS * M;
+    if (j < np) {
+      float s0 = 0.f, s1 = 0.f;
+      int z = 0;
+      for (; z + 2 <= bchunks; z += 2) {
+        s0 += bpart[(size_t)z * np + j];
+        s1 += bpart[(size_t)(z + 1) * np + j];
+      }
+      for (; z < bchunks; ++z) s0 += bpart[(size_t)z * np + j];
+      gposb[j] = s0 + s1;
+    }
+    return;
+  }
+  const int kq = KP / 4;
+  const int total = M * kq;
+  const size_t zstride = (size_t)Mpad * KP;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
-    const int co = idx / (taps * cin);
-    const int rem = idx - co * taps * cin;
-    const int t = rem / cin;
-    const int ci = rem - t * cin;
-    const size_t src = (size_t)co * KP + t * cinp + ci;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * Mpad * KP + src];
-    out[idx] = s;
+       idx += main_blocks * blockDim.x) {
+    const int co = idx / kq;
+    const int k = (idx - co * kq) * 4;
+    const float* src = slab + (size_t)co * KP + k;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {
+      s0 += *(const f32x4*)(src + (z + 0) * zstride);
+      s1 += *(const f32x4*)(src + (z + 1) * zstride);
+      s2 += *(const f32x4*)(src + (z + 2) * zstride);
+      s3 += *(const f32x4*)(src + (z + 3) * zstride);
+    }
+    for (; z < splits; ++z) s0 += *(const f32x4*)(src + z * zstride);
+    const f32x4 s = (s0 + s1) + (s2 + s3);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k + e;
+      const int t = kk / cinp;
+      const int ci = kk - t * cinp;
+      if (t < taps && ci < cin) out[((size_t)co * taps + t) * cin + ci] = s[e];
+    }
   }
 }
 
@@ -366,7 +491,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
 // ------------------------------------------------------------------------------------
 // Host launchers (C ABI used by the pybind11 module).
 
-static uint32_t magic_for(int d) { return (uint32_t)((0x100000000ull / (uint64_t)d) + 1); }
+static uint64_t magic_for(int d) { return fastdiv_magic((uint32_t)d); }
 
 // Allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); set once per kernel.
 template <typename K>
@@ -443,9 +568,13 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
   }
 }
 
+static int g_wgrad_ablate = 0;
+void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
+
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
-                         int x_pad, int x_C, int Npix, int KP, int splits, float* slab,
+                         int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream) {
+  const int Npix = B * NPTS;
   if (KP % 128 != 0 || Mpad % 128 != 0 || x_C % 8 != 0 || M % 8 != 0 || splits <= 0)
     return hipErrorInvalidValue;
   WgradArgs a;
@@ -465,10 +594,14 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
   a.gpt = x_C / 8;
   a.ngroups = kw * kw * a.gpt;
   a.gpt_magic = magic_for(a.gpt);
+  a.ablate = g_wgrad_ablate;
   if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
   // dZ channel tile must stay inside the dZ rows: for M < Mpad the extra co rows read
   // neighbouring channels/pixels of valid memory and land in unused slab rows.
-  dim3 grid(KP / 128, Mpad / 128, splits);
+  a.ktiles = KP / 128;
+  a.mtiles = Mpad / 128;
+  a.splits = splits;
+  dim3 grid(a.ktiles * a.mtiles * splits);
   const size_t lds = 2 * 2 * 64 * 256;
   switch (kw) {
     case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), lds, stream, a); break;
@@ -483,12 +616,14 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
 }
 
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
-                           int taps, int cin, int cinp, hipStream_t stream) {
-  const int total = M * taps * cin;
+                           int taps, int cin, int cinp, const float* bpart, int bchunks,
+                           float* gposb, float* gbias, hipStream_t stream) {
+  const int total = M * (KP / 4);
   int blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, slab, out, splits,
-                     M, Mpad, KP, taps, cin, cinp);
+  if (blocks > 8192) blocks = 8192;
+  const int extra = bpart ? (NPTS * M + 255) / 256 + M : 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra), dim3(256), 0, stream, slab, out,
+                     splits, M, Mpad, KP, taps, cin, cinp, bpart, bchunks, gposb, gbias, blocks);
   return hipGetLastError();
 }
 

@@ -59,6 +59,11 @@ DG_DEV float wave_max(float v) {
   return v;
 }
 
+// Exact floor(n / d) for 0 <= n < 2^22 and 1 <= d <= 4096 via a 64-bit magic
+// m = floor(2^32 / d) + 1 (host computes it; checked exhaustively in tests/tools).
+DG_DEV uint32_t fastdiv(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }
+inline uint64_t fastdiv_magic(uint32_t d) { return (0x100000000ull / d) + 1; }
+
 // Byte offset of board pixel (b, h, w) inside a zero-bordered NHWC frame
 // [B][19+2pad][19+2pad][C] of bf16.
 DG_DEV uint32_t frame_off(int b, int h, int w, int pad, int C) {

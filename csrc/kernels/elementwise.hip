@@ -68,48 +68,61 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
 }
 
 // ------------------------------------------------------------------------------------
-// Bias gradients of a conv layer from its pre-activation gradient frame dZ:
-//   gposb[p][c] = sum_b dZ[b][p][c]   (untied nn.Add bias, experiments.lua:144)
-//   gbias[c]   += sum_p gposb[p][c]   (per-channel conv bias)
-// One workgroup per board point p; threads = (C/8 groups) x (256/(C/8) board lanes).
+// Bias gradients of a conv layer from its pre-activation gradient frame dZ, pass 1:
+//   part[chunk][p][c]     = sum_{b in chunk} dZ[b][p][c]
+//   rowpart[chunk][h][c]  = sum_{w} part[chunk][h*19+w][c]
+// Grid: (board row h) x (chunk of BG_BT boards).  A workgroup streams the 19*C contiguous
+// values of row h for each of its boards with independent 16-byte loads (unrolled over
+// the chunk) and writes plain coalesced partials — no atomics, deterministic.  Pass 2
+// (sum over chunks -> gposb, gbias) runs inside the wgrad slab-reduce launch.
+// Reference: nn.Add / conv bias backward (experiments.lua:138,144).
+constexpr int BG_BT = 16;
 __global__ void __launch_bounds__(256)
-bias_grad_kernel(const char* __restrict__ dZ, int B, int C, int pad, float* __restrict__ gposb,
-                 float* __restrict__ gbias) {
-  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][8]
-  const int p = blockIdx.x;
+bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
+                         float* __restrict__ part, int nchunks) {
+  extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
+  const int h = blockIdx.x;
+  const int chunk = blockIdx.y;
+  const int b0 = chunk * BG_BT;
   const int G = C / 8;
-  const int tid = threadIdx.x;
-  const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
   const int F = BOARD + 2 * pad;
-  const int lanes_b = 256 / G;  // >= 1 since C <= 2048
-  const int g = tid % G;
-  const int lb = tid / G;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (lb < lanes_b) {
-    for (int b = lb; b < B; b += lanes_b) {
-      const uint4 v =
-          *(const uint4*)(dZ + ((size_t)((b * F + h + pad) * F + w + pad) * C + g * 8) * 2);
-      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+  const int items = BOARD * G;  // (w, g) pairs of the row
+  const int tid = threadIdx.x;
+  const size_t board_stride = (size_t)F * F * C * 2;
+  const char* row0 = dZ + ((size_t)((h + pad) * F + pad) * C) * 2;
+  float* prow = part + ((size_t)chunk * NPTS + h * BOARD) * C;
+  for (int it = tid; it < items; it += 256) {
+    const int w = it / G, g = it - (it / G) * G;
+    const char* src = row0 + ((size_t)w * C + g * 8) * 2;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 v[BG_BT];
+#pragma unroll
+    for (int j = 0; j < BG_BT; ++j) {
+      const int b = b0 + j;
+      v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < BG_BT; ++j) {
+      const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         acc[2 * e] += __uint_as_float(u[e] << 16);
         acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
       }
     }
+    f32x4* dst = (f32x4*)(prow + w * C + g * 8);
+    dst[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    dst[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+    float* sr = s_row + w * C + g * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sr[e] = acc[e];
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) sred[tid * 8 + e] = acc[e];
   __syncthreads();
-  if (tid < G) {
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < lanes_b; ++l)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += sred[(l * G + tid) * 8 + e];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      gposb[(size_t)p * C + tid * 8 + e] = s[e];
-      atomicAdd(gbias + tid * 8 + e, s[e]);
-    }
+  float* rowpart = part + (size_t)nchunks * NPTS * C + ((size_t)chunk * BOARD + h) * C;
+  for (int c = tid; c < C; c += 256) {
+    float sc = 0.f;
+    for (int w = 0; w < BOARD; ++w) sc += s_row[w * C + c];
+    rowpart[c] = sc;
   }
 }
 
@@ -198,13 +211,17 @@ hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, cons
   return hipGetLastError();
 }
 
-hipError_t dg_bias_grad(const void* dZ, int B, int C, int pad, float* gposb, float* gbias,
-                        hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bias_grad_kernel, dim3(NPTS), dim3(256), 256 * 8 * sizeof(float), s,
-                     (const char*)dZ, B, C, pad, gposb, gbias);
+// part must hold nchunks*(361 + 19)*C floats, nchunks = ceil(B / 16)
+hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* part,
+                                hipStream_t s) {
+  if (C % 8 != 0 || C > 2048) return hipErrorInvalidValue;
+  const int nchunks = (B + BG_BT - 1) / BG_BT;
+  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks), dim3(256),
+                     (size_t)BOARD * C * sizeof(float), s, (const char*)dZ, B, C, pad, part,
+                     nchunks);
   return hipGetLastError();
 }
+int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
 
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
                   hipStream_t s) {

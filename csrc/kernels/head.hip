@@ -7,15 +7,23 @@
 // ne / sum for accuracy (train.lua:29,36).  The reference runs these as ~8 separate
 // cunn kernels; here they are a single pass over the board held on-chip.
 //
-// M = 1 makes MFMA pointless (GEMV-shaped), so the dot products run on the VALU with
-// 16-byte vector loads; the 361 logits / probabilities stay in LDS.
+// M = 1 makes MFMA pointless (GEMV-shaped), so the dot products run on the VALU.  The
+// board's zero-bordered activation frame is staged into LDS in 128-channel chunks with
+// wide independent loads (one HBM pass per chunk); the forward dots, the input gradient
+// and the weight-gradient partials all read it from LDS.  Lane mapping: 16 lanes cover
+// the 16 8-channel groups of one pixel (256 contiguous bytes -> conflict-free
+// ds_read_b128), 4 pixels per wave.
 #include "dg_common.h"
 
 using namespace dg;
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+
 namespace {
 
-constexpr int HT = 256;  // threads per board
+constexpr int HT = 512;      // threads per board (8 waves: 2 per SIMD)
+constexpr int CCH = 128;     // channels staged per chunk
+constexpr int GC = CCH / 8;  // 8-channel groups per chunk (16)
 
 struct HeadArgs {
   const char* X;        // last hidden activation frame [B][F][F][C] bf16
@@ -27,9 +35,9 @@ struct HeadArgs {
   int* pred;            // [B]  argmax
   float* logp_out;      // [B][361] optional (null = skip)
   char* dZ;             // gradient frame of the last hidden layer (null = eval only)
-  float* gw;            // grad of head weights [KW*KW*C] (atomic accumulate)
-  float* gbias;         // [1] (atomic)
-  float* gposb;         // [361] (atomic)
+  float* gw_part;       // [B][KW*KW*C] per-board weight-grad partials (plain stores)
+  float* gbias;         // unused (head_reduce computes it)
+  float* dzb;           // [B][361] per-board d loss / d z (plain stores)
   int B;
   int C;
   int x_pad;
@@ -38,51 +46,109 @@ struct HeadArgs {
   float grad_scale;     // 1 / global batch (mean NLL)
 };
 
+DG_DEV float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, a),
+                                         __builtin_bit_cast(bf16x2v, b), c, false);
+}
+
+DG_DEV void unpack8(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xFFFF0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
+}
+
 template <int KW>
 __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
   constexpr int R = (KW - 1) / 2;
   constexpr int T = KW * KW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* s_w = (float*)smem;                 // [T*C]
-  float* s_z = s_w + T * a.C;                // [361] pre-activation
-  float* s_dz = s_z + 384;                   // [361] d loss / d z
-  float* s_red = s_dz + 384;                 // [HT] scratch
-  int* s_redi = (int*)(s_red + HT);          // [HT]
+  const int C = a.C;
+  const int F = BOARD + 2 * a.x_pad;
+  const int FF = F * F;
+  const int cc = C < CCH ? C : CCH;         // channels per chunk
+  const int gcc = cc / 8;                   // groups per chunk
+  const int nchunk = C / cc;
+  // LDS carve (16-B aligned pieces)
+  char* s_x = smem;                                   // [FF][cc] bf16
+  // s_x is padded to whole 1-KiB DMA wave-instructions (64 pieces of 16 B): the tail
+  // instruction writes all 64 lanes' destinations.
+  const int xbytes = ((FF * gcc + 63) / 64) * 64 * 16;
+  float* s_w = (float*)(smem + xbytes);               // [T][C]
+  float* s_z = s_w + T * C;                           // [384]
+  float* s_dz = s_z + 384;                            // [384]
+  float* s_gw = s_dz + 384;                           // [T][cc] dw partial (chunk)
+  float* s_red = s_gw + T * CCH;                      // [HT]
+  int* s_redi = (int*)(s_red + HT);                   // [HT]
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int C = a.C;
-  const int G = C / 8;                       // 8-channel groups
-  const int F = BOARD + 2 * a.x_pad;
+  const char* Xb = a.X + (size_t)b * FF * C * 2;
 
   for (int i = tid; i < T * C; i += HT) s_w[i] = a.w[i];
-  __syncthreads();
+  for (int p = tid; p < 384; p += HT) s_z[p] = 0.f;
 
-  // ---- forward: z[p] = sum_{t,c} w[t][c] * X[p + off(t)][c] ----
-  const char* Xb = a.X + (size_t)b * F * F * C * 2;
-  for (int p = wave; p < NPTS; p += HT / 64) {
-    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
-    float acc = 0.f;
-    for (int idx = lane; idx < T * G; idx += 64) {
-      const int t = idx / G, g = idx - (idx / G) * G;
-      const int hh = h + t / KW - R + a.x_pad, ww = w + t % KW - R + a.x_pad;
-      const uint4 v = *(const uint4*)(Xb + ((hh * F + ww) * C + g * 8) * 2);
-      const float* wt = s_w + t * C + g * 8;
-      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+  auto stage_chunk = [&](int ch) {
+    // LDS-DMA: piece i (frame pixel f = i / gcc, group g) lands at byte 16*i of s_x, which is
+    // exactly the lane-linear destination of global_load_lds_dwordx4 (base + lane*16).
+    const int pieces = FF * gcc;
+    for (int i0 = wave * 64; i0 < pieces; i0 += HT) {
+      int i = i0 + lane;
+      if (i >= pieces) i = pieces - 1;  // duplicate last piece: same bytes, same address
+      const int f = i / gcc, g = i - (i / gcc) * gcc;
+      glds16(Xb + ((size_t)f * C + ch * cc + g * 8) * 2, (LDS_AS void*)(s_x + i0 * 16));
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt=0) this wave's DMA landed; barrier follows
+  };
+
+  // lane -> (pixel slot, group): 16 lanes per pixel when gcc == 16
+  const int lg = lane % gcc;                 // group within chunk
+  const int lpix = lane / gcc;               // pixel slot within wave
+  const int ppw = 64 / gcc;                  // pixels per wave-iteration
+  const int lanes_used = ppw * gcc;
+
+  // ---------------- forward: z[p] = sum_{t,c} w[t][c] X[p+off(t)][c] ----------------
+  // weights of this lane's channel group live in registers as packed bf16 pairs;
+  // v_dot2_f32_bf16 consumes the staged bf16 activations without unpacking.
+  for (int ch = 0; ch < nchunk; ++ch) {
+    __syncthreads();
+    stage_chunk(ch);
+    __syncthreads();
+    uint32_t wp[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        acc += wt[2 * e] * __uint_as_float(u[e] << 16);
-        acc += wt[2 * e + 1] * __uint_as_float(u[e] & 0xFFFF0000u);
+        const float* wt = s_w + t * C + ch * cc + lg * 8 + 2 * e;
+        wp[t][e] = pack_bf16x2(wt[0], wt[1]);
       }
+    for (int p0 = wave * ppw; p0 < NPTS; p0 += (HT / 64) * ppw) {
+      const int p = p0 + lpix;
+      float acc = 0.f;
+      if (p < NPTS && lane < lanes_used) {
+        const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int f = (h + a.x_pad + t / KW - R) * F + (w + a.x_pad + t % KW - R);
+          const uint4 xv = *(const uint4*)(s_x + (f * cc + lg * 8) * 2);
+          acc = dot2(xv.x, wp[t][0], acc);
+          acc = dot2(xv.y, wp[t][1], acc);
+          acc = dot2(xv.z, wp[t][2], acc);
+          acc = dot2(xv.w, wp[t][3], acc);
+        }
+      }
+      // reduce over the gcc lanes of this pixel
+      for (int o = gcc / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (p < NPTS && lg == 0 && lane < lanes_used) s_z[p] += acc;
     }
-    acc = wave_sum(acc);
-    if (lane == 0) s_z[p] = acc + a.bias[0] + a.posb[p];
   }
   __syncthreads();
+  for (int p = tid; p < NPTS; p += HT) s_z[p] += a.bias[0] + a.posb[p];
+  __syncthreads();
 
-  // ---- log-softmax over 361 logits (logit = relu(z) if head_relu) ----
+  // ---------------- log-softmax over 361 logits (logit = relu(z) if head_relu) --------
   float m = -INFINITY;
   int am = 0;
   for (int p = tid; p < NPTS; p += HT) {
@@ -134,88 +200,182 @@ __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
   }
   if (a.dZ == nullptr) return;
 
-  // ---- backward: dlogit = (softmax - onehot) * scale ; dz = dlogit * relu'(z) ----
-  float dsum = 0.f;
-  for (int p = tid; p < NPTS; p += HT) {
-    const float z = s_z[p];
-    const float l = a.head_relu ? fmaxf(z, 0.f) : z;
-    float d = __expf(l - lse) - (p == y ? 1.f : 0.f);
-    d *= a.grad_scale;
-    if (a.head_relu && !(z > 0.f)) d = 0.f;
+  // ---------------- backward: dz = (softmax - onehot) * scale * relu'(z) --------------
+  for (int p = tid; p < 384; p += HT) {
+    float d = 0.f;
+    if (p < NPTS) {
+      const float z = s_z[p];
+      const float l = a.head_relu ? fmaxf(z, 0.f) : z;
+      d = (__expf(l - lse) - (p == y ? 1.f : 0.f)) * a.grad_scale;
+      if (a.head_relu && !(z > 0.f)) d = 0.f;
+      a.dzb[(size_t)b * NPTS + p] = d;
+    }
     s_dz[p] = d;
-    dsum += d;
-    atomicAdd(a.gposb + p, d);
   }
-  dsum = wave_sum(dsum);
-  if (lane == 0) atomicAdd(a.gbias, dsum);
-  __syncthreads();
 
-  // ---- dX[q][c] = sum_t w[t][c] * dz[q - off(t)], masked by X[q][c] > 0 ----
-  char* dZb = a.dZ + (size_t)b * (BOARD + 2 * a.dz_pad) * (BOARD + 2 * a.dz_pad) * C * 2;
   const int Fd = BOARD + 2 * a.dz_pad;
-  for (int idx = tid; idx < NPTS * G; idx += HT) {
-    const int q = idx / G, g = idx - (idx / G) * G;
-    const int h = q / BOARD, w = q - (q / BOARD) * BOARD;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  char* dZb = a.dZ + (size_t)b * Fd * Fd * C * 2;
+  // chunk order: the last staged chunk is still in LDS; walk chunks backwards
+  for (int ci = nchunk - 1; ci >= 0; --ci) {
+    __syncthreads();
+    if (ci != nchunk - 1) stage_chunk(ci);
+    for (int i = tid; i < T * CCH; i += HT) s_gw[i] = 0.f;
+    __syncthreads();
+    // ---- dX[q][c] = sum_t w[t][c] dz[q - off(t)], masked by X[q][c] > 0 ----
+    {
+      const int g = tid % gcc;  // HT is a multiple of gcc: fixed group per thread
+      float wr[T][8];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int ph = h - (t / KW - R), pw = w - (t % KW - R);
-      if (ph < 0 || ph >= BOARD || pw < 0 || pw >= BOARD) continue;
-      const float d = s_dz[ph * BOARD + pw];
-      const float* wt = s_w + t * C + g * 8;
+      for (int t = 0; t < T; ++t)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += d * wt[e];
-    }
-    const uint4 xm = *(const uint4*)(Xb + (((h + a.x_pad) * F + (w + a.x_pad)) * C + g * 8) * 2);
-    const uint32_t u[4] = {xm.x, xm.y, xm.z, xm.w};
-    uint32_t o[4];
+        for (int e = 0; e < 8; ++e) wr[t][e] = s_w[t * C + ci * cc + g * 8 + e];
+      for (int idx = tid; idx < NPTS * gcc; idx += HT) {
+        const int q = idx / gcc;
+        const int h = q / BOARD, w = q - (q / BOARD) * BOARD;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float lo = __uint_as_float(u[e] << 16) > 0.f ? v[2 * e] : 0.f;
-      const float hi = __uint_as_float(u[e] & 0xFFFF0000u) > 0.f ? v[2 * e + 1] : 0.f;
-      o[e] = pack_bf16x2(lo, hi);
-    }
-    *(uint4*)(dZb + (((h + a.dz_pad) * Fd + (w + a.dz_pad)) * C + g * 8) * 2) =
-        uint4{o[0], o[1], o[2], o[3]};
-  }
-
-  // ---- dw[t][c] += sum_p dz[p] * X[p + off(t)][c] ----
-  for (int idx = tid; idx < T * G; idx += HT) {
-    const int t = idx / G, g = idx - (idx / G) * G;
-    const int dh = t / KW - R, dw = t % KW - R;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < NPTS; ++p) {
-      const float d = s_dz[p];
-      if (d == 0.f) continue;
-      const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
-      const uint4 xv = *(const uint4*)(Xb + (((h + dh + a.x_pad) * F + (w + dw + a.x_pad)) * C + g * 8) * 2);
-      const uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
+        for (int t = 0; t < T; ++t) {
+          const int ph = h - (t / KW - R), pw = w - (t % KW - R);
+          const bool in = ph >= 0 && ph < BOARD && pw >= 0 && pw < BOARD;
+          const float d = in ? s_dz[ph * BOARD + pw] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] += d * __uint_as_float(u[e] << 16);
-        v[2 * e + 1] += d * __uint_as_float(u[e] & 0xFFFF0000u);
+          for (int e = 0; e < 8; ++e) v[e] += d * wr[t][e];
+        }
+        float xm[8];
+        unpack8(*(const uint4*)(s_x + (((h + a.x_pad) * F + (w + a.x_pad)) * cc + g * 8) * 2), xm);
+        uint4 o;
+        o.x = pack_bf16x2(xm[0] > 0.f ? v[0] : 0.f, xm[1] > 0.f ? v[1] : 0.f);
+        o.y = pack_bf16x2(xm[2] > 0.f ? v[2] : 0.f, xm[3] > 0.f ? v[3] : 0.f);
+        o.z = pack_bf16x2(xm[4] > 0.f ? v[4] : 0.f, xm[5] > 0.f ? v[5] : 0.f);
+        o.w = pack_bf16x2(xm[6] > 0.f ? v[6] : 0.f, xm[7] > 0.f ? v[7] : 0.f);
+        *(uint4*)(dZb + ((size_t)((h + a.dz_pad) * Fd + (w + a.dz_pad)) * C + ci * cc + g * 8) * 2) = o;
       }
     }
+    // ---- dw[t][c] += sum_p dz[p] X[p + off(t)][c]: lanes (group, pixel slice) ----
+    {
+      const int g = tid % gcc;
+      const int slice = tid / gcc;
+      const int nslice = HT / gcc;
+      float v[T][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(a.gw + t * C + g * 8 + e, v[e]);
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[t][e] = 0.f;
+      for (int p = slice; p < NPTS; p += nslice) {
+        const float d = s_dz[p];
+        const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int f = (h + a.x_pad + t / KW - R) * F + (w + a.x_pad + t % KW - R);
+          float xv[8];
+          unpack8(*(const uint4*)(s_x + (f * cc + g * 8) * 2), xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[t][e] += d * xv[e];
+        }
+      }
+      // lanes l, l+gcc, l+2gcc.. of a wave share g: fold them with shuffles first
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = v[t][e];
+          for (int o = gcc; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+          v[t][e] = x;
+        }
+      if (lane < gcc) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(s_gw + t * CCH + g * 8 + e, v[t][e]);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < T * cc; i += HT) {
+      const int t = i / cc, c = i - (i / cc) * cc;
+      a.gw_part[(size_t)b * T * C + t * C + ci * cc + c] = s_gw[t * CCH + c];
+    }
   }
+}
+
+// Deterministic-order batch reduction of the head's per-board partials:
+//   gposb[p] = sum_b dzb[b][p], gbias = sum_p gposb[p], gw[i] = sum_b gw_part[b][i].
+// grid.x covers the n weight columns then the 361 position columns; grid.y = chunks of
+// 32 boards whose partial sums are combined with (8-way, low contention) float atomics.
+constexpr int HR_BT = 32;
+__global__ void __launch_bounds__(256)
+head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_part, int B, int n,
+                   float* __restrict__ gw, float* __restrict__ gbias, float* __restrict__ gposb) {
+  __shared__ float s_red[256];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = blockIdx.y * HR_BT;
+  const int b1 = min(B, b0 + HR_BT);
+  float s = 0.f;
+  bool pos = false;
+  if (j < n) {
+    for (int b = b0; b < b1; ++b) s += gw_part[(size_t)b * n + j];
+    atomicAdd(gw + j, s);
+  } else if (j - n < NPTS) {
+    const int p = j - n;
+    for (int b = b0; b < b1; ++b) s += dzb[(size_t)b * NPTS + p];
+    atomicAdd(gposb + p, s);
+    pos = true;
+  }
+  s_red[threadIdx.x] = pos ? s : 0.f;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s_red[threadIdx.x] += s_red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && (blockIdx.x + 1) * 256 > n) atomicAdd(gbias, s_red[0]);
 }
 
 }  // namespace
 
+extern "C" hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n,
+                                     float* gw, float* gbias, float* gposb, hipStream_t stream) {
+  dim3 grid((n + NPTS + 255) / 256, (B + HR_BT - 1) / HR_BT);
+  hipLaunchKernelGGL(head_reduce_kernel, grid, dim3(256), 0, stream, dzb, gw_part, B, n, gw,
+                     gbias, gposb);
+  return hipGetLastError();
+}
+
+template <typename K>
+static void allow_lds_once(K kernel, size_t bytes) {
+  static size_t done = 0;  // one per instantiation; raise when a larger frame appears
+  if (bytes > done) {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = bytes;
+  }
+}
+
 extern "C" hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                               const float* bias, const float* posb, const int* labels,
                               float* loss, int* pred, float* logp_out, void* dZ, int dz_pad,
-                              float* gw, float* gbias, float* gposb, int head_relu,
+                              float* gw_part, float* unused, float* dzb, int head_relu,
                               float grad_scale, hipStream_t stream) {
   if (C % 8 != 0 || B <= 0) return hipErrorInvalidValue;
-  HeadArgs a{(const char*)X, w, bias, posb, labels, loss, pred, logp_out, (char*)dZ, gw, gbias,
-             gposb, B, C, x_pad, dz_pad, head_relu, grad_scale};
-  const size_t lds = (size_t)(kw * kw * C + 384 + 384 + HT) * 4 + HT * 4;
+  if (C > CCH && C % CCH != 0) return hipErrorInvalidValue;
+  if (C < CCH && (64 % (C / 8)) != 0) return hipErrorInvalidValue;  // lanes per pixel
+  HeadArgs a{(const char*)X, w, bias, posb, labels, loss, pred, logp_out, (char*)dZ, gw_part,
+             unused, dzb, B, C, x_pad, dz_pad, head_relu, grad_scale};
+  const int F = 19 + 2 * x_pad;
+  const int cc = C < CCH ? C : CCH;
+  const size_t lds = (size_t)((F * F * (cc / 8) + 63) / 64) * 64 * 16 +
+                     (size_t)(kw * kw * C + 384 + 384 + kw * kw * CCH + HT) * 4 + HT * 4;
   switch (kw) {
-    case 1: hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(HT), lds, stream, a); break;
-    case 3: hipLaunchKernelGGL(head_kernel<3>, dim3(B), dim3(HT), lds, stream, a); break;
-    case 5: hipLaunchKernelGGL(head_kernel<5>, dim3(B), dim3(HT), lds, stream, a); break;
+    case 1:
+      allow_lds_once(head_kernel<1>, lds);
+      hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(HT), lds, stream, a);
+      break;
+    case 3:
+      allow_lds_once(head_kernel<3>, lds);
+      hipLaunchKernelGGL(head_kernel<3>, dim3(B), dim3(HT), lds, stream, a);
+      break;
+    case 5:
+      allow_lds_once(head_kernel<5>, lds);
+      hipLaunchKernelGGL(head_kernel<5>, dim3(B), dim3(HT), lds, stream, a);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -51,6 +51,8 @@ class ConvPlan:
     Mpad_d: int = 0
     bm_d: int = 128
     bn_d: int = 128
+    board: bool = False    # fwd uses the board-tiled kernel
+    board_d: bool = False  # dgrad uses the board-tiled kernel
 
 
 class HipGoNet:
@@ -93,15 +95,21 @@ class HipGoNet:
         self.wd: List[Optional[torch.Tensor]] = []
         for spec in L[:-1]:
             cinp = INPUT_CP if spec.index == 0 else spec.cin
+            board = LY.board_ok(spec.k, cinp)
             bm, bn = LY.pick_tiles(npix, spec.cout, num_cus)
+            if board:
+                bm = LY.board_bm(spec.cout)
             KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
             Mpad_w = LY.round_up(spec.cout, 128)
             splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
-                         Mpad, KPw, Mpad_w, splits)
+                         Mpad, KPw, Mpad_w, splits, board=board)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
             if spec.index > 0:
                 bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
+                p.board_d = LY.board_ok(spec.k, spec.cout)
+                if p.board_d:
+                    bm_d = LY.board_bm(spec.cin)
                 KPd, _, Mpad_d = LY.conv_dims(spec.k, spec.cout, spec.cin, bm_d)
                 p.KPd, p.Mpad_d, p.bm_d, p.bn_d = KPd, Mpad_d, bm_d, bn_d
                 self.wd.append(torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=dev))
@@ -120,6 +128,10 @@ class HipGoNet:
         self.dz = [LY.alloc_frame(B, L[i].cout, max(1, pads[i]), dev) for i in range(self.L - 1)]
         slab = max(p.splits * p.Mpad_w * p.KPw for p in self.plans)
         self.slab = torch.empty(slab, dtype=torch.float32, device=dev)
+        self.bchunks = self.h.bias_chunks(batch)
+        cmax = max(p.cout for p in self.plans)
+        self.bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
+                                 device=dev)
 
         # ---- step I/O ----
         self.planes = torch.zeros((B, 9, NUM_POINTS), dtype=torch.uint8, device=dev)
@@ -128,6 +140,10 @@ class HipGoNet:
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.loss = torch.zeros(B, dtype=torch.float32, device=dev)
         self.pred = torch.zeros(B, dtype=torch.int32, device=dev)
+        hdl = L[-1]
+        self.head_gw_part = torch.zeros((B, hdl.k * hdl.k * hdl.cin), dtype=torch.float32,
+                                        device=dev)
+        self.head_dzb = torch.zeros((B, NUM_POINTS), dtype=torch.float32, device=dev)
 
         self._refresh_table = self._build_refresh_table()
         self._build_plans()
@@ -160,19 +176,30 @@ class HipGoNet:
             xin = self.x0 if p.index == 0 else self.act[p.index - 1]
             x_pad = spec.pad
             y_pad = lay.layers[p.index + 1].pad
-            self._fwd.append((h.conv_nt, (h.EPI_FWD, p.k, p.bm, p.bn, self.wf[p.index].data_ptr(),
-                                          p.KP, p.cout, p.Mpad, xin.data_ptr(), x_pad, p.cinp,
-                                          self.npix, self.act[p.index].data_ptr(), y_pad,
-                                          P + spec.b_off * f4, P + spec.pos_off * f4, 0, 0)))
+            if p.board:
+                self._fwd.append((h.conv_board, (h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(),
+                                                 p.KP, p.cout, p.Mpad, xin.data_ptr(), x_pad,
+                                                 p.cinp, self.B, self.act[p.index].data_ptr(),
+                                                 y_pad, P + spec.b_off * f4,
+                                                 P + spec.pos_off * f4, 0, 0)))
+            else:
+                self._fwd.append((h.conv_nt, (h.EPI_FWD, p.k, p.bm, p.bn,
+                                              self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
+                                              xin.data_ptr(), x_pad, p.cinp, self.npix,
+                                              self.act[p.index].data_ptr(), y_pad,
+                                              P + spec.b_off * f4, P + spec.pos_off * f4, 0, 0)))
         hd = self.head
         hx = self.act[-1]
         self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
                                      P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
                                      self.labels.data_ptr(), self.loss.data_ptr(),
                                      self.pred.data_ptr(), 0, self.dz[-1].data_ptr(),
-                                     max(1, lay.layers[-2].pad), G + hd.w_off * f4,
-                                     G + hd.b_off * f4, G + hd.pos_off * f4,
+                                     max(1, lay.layers[-2].pad), self.head_gw_part.data_ptr(),
+                                     0, self.head_dzb.data_ptr(),
                                      int(self.cfg.head_relu), 1.0 / self.global_batch))
+        self._head_red = (h.head_reduce, (self.head_dzb.data_ptr(), self.head_gw_part.data_ptr(),
+                                          self.B, hd.k * hd.k * hd.cin, G + hd.w_off * f4,
+                                          G + hd.b_off * f4, G + hd.pos_off * f4))
         self._head_eval = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
                                     P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
                                     self.labels.data_ptr(), self.loss.data_ptr(),
@@ -183,21 +210,32 @@ class HipGoNet:
             i = p.index
             ops = []
             dzp = max(1, spec.pad)
-            ops.append((h.bias_grad, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
-                                      G + spec.pos_off * f4, G + spec.b_off * f4)))
             xin = self.x0 if i == 0 else self.act[i - 1]
+            # bias grads: pass 1 (per board-chunk partials); pass 2 runs inside the slab
+            # reduce launch, which also finalises the weight grad
+            ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
+                                              self.bpart.data_ptr())))
             ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                       xin.data_ptr(), spec.pad, p.cinp, self.npix, p.KPw,
+                                       xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
                                        p.splits, self.slab.data_ptr())))
             ops.append((h.wgrad_reduce, (self.slab.data_ptr(), G + spec.w_off * f4, p.splits,
-                                         p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp)))
+                                         p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp,
+                                         self.bpart.data_ptr(), self.bchunks,
+                                         G + spec.pos_off * f4, G + spec.b_off * f4)))
             if i > 0:
                 prev = lay.layers[i - 1]
-                ops.append((h.conv_nt, (h.EPI_DGRAD, p.k, p.bm_d, p.bn_d,
-                                        self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
-                                        self.dz[i].data_ptr(), dzp, p.cout, self.npix,
-                                        self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
-                                        self.act[i - 1].data_ptr(), spec.pad)))
+                if p.board_d:
+                    ops.append((h.conv_board, (h.EPI_DGRAD, p.k, p.bm_d, self.wd[i].data_ptr(),
+                                               p.KPd, p.cin, p.Mpad_d, self.dz[i].data_ptr(),
+                                               dzp, p.cout, self.B, self.dz[i - 1].data_ptr(),
+                                               max(1, prev.pad), 0, 0,
+                                               self.act[i - 1].data_ptr(), spec.pad)))
+                else:
+                    ops.append((h.conv_nt, (h.EPI_DGRAD, p.k, p.bm_d, p.bn_d,
+                                            self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
+                                            self.dz[i].data_ptr(), dzp, p.cout, self.npix,
+                                            self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
+                                            self.act[i - 1].data_ptr(), spec.pad)))
             self._bwd.append(ops)
 
     # ------------------------------------------------------------------ execution
@@ -227,6 +265,8 @@ class HipGoNet:
         self._run(self._pre, s)
         self._run(self._fwd, s)
         f, a = self._head_train
+        f(*a, s)
+        f, a = self._head_red
         f(*a, s)
         hooks = dict()
         for li, fn in self.grad_hooks:
@@ -338,6 +378,7 @@ class SegmentedStep:
         emit(lambda: net._run(net._pre, stream_handle()))
         emit(lambda: net._run(net._fwd, stream_handle()))
         emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
+        emit(lambda: net._head_red[0](*net._head_red[1], stream_handle()))
         if net.L - 1 in fire_after:
             segs.append((cur, fire_after[net.L - 1]))
             cur = []

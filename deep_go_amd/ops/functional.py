@@ -46,6 +46,42 @@ def conv_forward(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: st
     return LY.from_frame(yf, 1, cout)
 
 
+def conv_board(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: str = "fwd",
+               aux=None) -> torch.Tensor:
+    """Board-tiled kernel (1x1/3x3, Cin % 64 == 0).  epi='fwd'|'linear' as conv_forward;
+    epi='dgrad': x is dZ [B,Cout,19,19], w is the forward OHWI weight [Cout,k,k,Cin],
+    aux [B,Cin,19,19] gates the result (ReLU backward)."""
+    h = hip()
+    dev = w.device
+    B = x.shape[0]
+    cout, k, _, cin = w.shape
+    pad = (k - 1) // 2
+    if epi == "dgrad":
+        M, xc = cin, cout
+        bm = LY.board_bm(M)
+        KP, _, Mpad = LY.conv_dims(k, xc, M, bm)
+        A = LY.dgrad_weight(w.float(), KP, Mpad)
+        xf = LY.to_frame(x.to(dev), max(1, pad))
+        auxf = LY.to_frame(aux.to(dev), pad)
+        out = LY.alloc_frame(B, M, 1, dev)
+        h.conv_board(h.EPI_DGRAD, k, bm, A.data_ptr(), KP, M, Mpad, xf.data_ptr(), max(1, pad),
+                     xc, B, out.data_ptr(), 1, 0, 0, auxf.data_ptr(), pad, stream_handle())
+        return LY.from_frame(out, 1, M)
+    M, xc = cout, cin
+    bm = LY.board_bm(M)
+    KP, _, Mpad = LY.conv_dims(k, xc, M, bm)
+    A = LY.fwd_weight(w.float(), xc, KP, Mpad)
+    xf = LY.to_frame(x.to(dev), pad, xc)
+    out = LY.alloc_frame(B, M, 1, dev)
+    e = {"fwd": h.EPI_FWD, "linear": h.EPI_LINEAR}[epi]
+    if e == h.EPI_FWD:
+        bias = bias.float().contiguous().to(dev)
+        posb = posb.float().contiguous().to(dev)
+    h.conv_board(e, k, bm, A.data_ptr(), KP, M, Mpad, xf.data_ptr(), pad, xc, B, out.data_ptr(),
+                 1, _ptr(bias), _ptr(posb), 0, 0, stream_handle())
+    return LY.from_frame(out, 1, M)
+
+
 def conv_dgrad(dz: torch.Tensor, w: torch.Tensor, aux: torch.Tensor, tiles=None) -> torch.Tensor:
     """dz [B,Cout,19,19], w OHWI [Cout,k,k,Cin], aux [B,Cin,19,19] (activation whose >0
     mask gates the result) -> dX*(aux>0) fp32 NCHW [B,Cin,19,19]."""
@@ -67,8 +103,10 @@ def conv_dgrad(dz: torch.Tensor, w: torch.Tensor, aux: torch.Tensor, tiles=None)
 
 
 def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = None,
-               cinp: int | None = None) -> torch.Tensor:
-    """dW[co][kh][kw][ci] = sum_{b,p} dz[b,co,p] * x[b,ci,p+off] (fp32 OHWI)."""
+               cinp: int | None = None, with_bias: bool = False):
+    """dW[co][kh][kw][ci] = sum_{b,p} dz[b,co,p] * x[b,ci,p+off] (fp32 OHWI).
+
+    with_bias=True also returns the fused bias grads (gposb [361][co], gbias [co])."""
     h = hip()
     dev = dz.device
     B, cout = dz.shape[:2]
@@ -83,10 +121,18 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     xf = LY.to_frame(x.to(dev), pad, cinp)
     slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)
     out = torch.empty((cout, k, k, cin), dtype=torch.float32, device=dev)
+    gp = torch.zeros((NPTS, cout), dtype=torch.float32, device=dev)
+    gb = torch.zeros(cout, dtype=torch.float32, device=dev)
+    nch = h.bias_chunks(B)
+    bpart = torch.empty(nch * (NPTS + 19) * cout, dtype=torch.float32, device=dev)
     s = stream_handle()
-    h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, npix, KPw,
+    h.bias_grad_partial(dzf.data_ptr(), B, cout, max(1, pad), bpart.data_ptr(), s)
+    h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B, KPw,
                  splits, slab.data_ptr(), s)
-    h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp, s)
+    h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp,
+                   bpart.data_ptr(), nch, gp.data_ptr(), gb.data_ptr(), s)
+    if with_bias:
+        return out, gp, gb
     return out
 
 
@@ -106,17 +152,24 @@ def head(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: torch.Tenso
     logp = torch.zeros((B, NPTS), dtype=torch.float32, device=dev)
     lab = labels.to(dev, torch.int32).contiguous() if labels is not None else None
     out = {"loss": loss, "pred": pred, "logp": logp}
-    dzf = gw = gb = gp = None
+    dzf = gw = gb = gp = gwp = dzb = None
     if train:
         dzf = LY.alloc_frame(B, C, 1, dev)
         gw = torch.zeros(k * k * C, dtype=torch.float32, device=dev)
         gb = torch.zeros(1, dtype=torch.float32, device=dev)
         gp = torch.zeros(NPTS, dtype=torch.float32, device=dev)
-    h.head(k, xf.data_ptr(), pad, C, B, w.float().contiguous().data_ptr(),
-           bias.float().contiguous().data_ptr(), posb.float().contiguous().data_ptr(), _ptr(lab),
-           loss.data_ptr(), pred.data_ptr(), logp.data_ptr(), _ptr(dzf), 1, _ptr(gw), _ptr(gb),
-           _ptr(gp), int(head_relu), float(grad_scale if grad_scale is not None else 1.0 / B),
-           stream_handle())
+        gwp = torch.zeros((B, k * k * C), dtype=torch.float32, device=dev)
+        dzb = torch.zeros((B, NPTS), dtype=torch.float32, device=dev)
+    s = stream_handle()
+    wc = w.float().contiguous()
+    bc = bias.float().contiguous()
+    pc = posb.float().contiguous()
+    h.head(k, xf.data_ptr(), pad, C, B, wc.data_ptr(), bc.data_ptr(), pc.data_ptr(), _ptr(lab),
+           loss.data_ptr(), pred.data_ptr(), logp.data_ptr(), _ptr(dzf), 1, _ptr(gwp), 0,
+           _ptr(dzb), int(head_relu), float(grad_scale if grad_scale is not None else 1.0 / B), s)
+    if train:
+        h.head_reduce(dzb.data_ptr(), gwp.data_ptr(), B, k * k * C, gw.data_ptr(), gb.data_ptr(),
+                      gp.data_ptr(), s)
     if train:
         out.update(dz=LY.from_frame(dzf, 1, C), gw=gw.view(1, k, k, C), gbias=gb, gposb=gp)
     return out
@@ -138,12 +191,15 @@ def expand_features(planes: torch.Tensor, player: torch.Tensor, rank: torch.Tens
 
 
 def bias_grad(dz: torch.Tensor):
+    """Pass 1 of the bias grads on the GPU, pass 2 summed here: (gposb [361][C], gbias [C])."""
     h = hip()
     B, C = dz.shape[:2]
     dzf = LY.to_frame(dz, 1)
-    gp = torch.zeros((NPTS, C), dtype=torch.float32, device=dz.device)
-    gb = torch.zeros(C, dtype=torch.float32, device=dz.device)
-    h.bias_grad(dzf.data_ptr(), B, C, 1, gp.data_ptr(), gb.data_ptr(), stream_handle())
+    nch = h.bias_chunks(B)
+    part = torch.empty(nch * (NPTS + 19) * C, dtype=torch.float32, device=dz.device)
+    h.bias_grad_partial(dzf.data_ptr(), B, C, 1, part.data_ptr(), stream_handle())
+    gp = part[:nch * NPTS * C].view(nch, NPTS, C).sum(0)
+    gb = part[nch * NPTS * C:].view(nch * 19, C).sum(0)
     return gp, gb
 
 

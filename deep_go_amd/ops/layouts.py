@@ -101,3 +101,13 @@ def pick_wgrad_splits(npix: int, KPw: int, Mpad: int, num_cus: int = 256) -> int
     target = max(1, (2 * num_cus) // tiles)
     max_split = max(1, npix // 256)
     return max(1, min(target, max_split))
+
+
+def board_ok(k: int, cin_frame: int) -> bool:
+    """The board-tiled kernel (conv_board.hip) handles 1x1/3x3 layers whose input frame
+    has a multiple of 64 channels; everything else uses the pixel-tiled conv_nt kernel."""
+    return k in (1, 3) and cin_frame % 64 == 0
+
+
+def board_bm(cout: int) -> int:
+    return 64 if cout <= 64 else 128

@@ -69,6 +69,37 @@ def test_conv_dgrad(B, cin, cout, k):
     assert rel_err(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (5, 128, 128, 3), (2, 256, 256, 3),
+                                          (3, 128, 64, 3), (2, 64, 128, 1), (1, 192, 128, 3)])
+def test_conv_board_forward(B, cin, cout, k):
+    torch.manual_seed(5)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5))
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y = Fn.conv_board(x, w, epi="linear")
+    assert rel_err(y, conv_ref(x, w, k)) < 1e-2
+    y = Fn.conv_board(x, w, b, pb, epi="fwd")
+    ref = F.relu(conv_ref(x, w, k) + b.view(1, -1, 1, 1) + pb.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (4, 128, 128, 3), (2, 256, 256, 3),
+                                          (2, 64, 128, 3)])
+def test_conv_board_dgrad(B, cin, cout, k):
+    torch.manual_seed(6)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5))
+    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+    aux = bf(torch.relu(torch.randn(B, cin, 19, 19, device=DEV)))
+    got = Fn.conv_board(dz, w, epi="dgrad", aux=aux)
+    xr = x.clone().requires_grad_(True)
+    (gx,) = torch.autograd.grad(conv_ref(xr, w, k), xr, dz)
+    assert rel_err(got, gx * (aux > 0)) < 1e-2
+
+
 @pytest.mark.parametrize("B,cin,cout,k,splits", [(3, 64, 64, 3, None), (7, 128, 128, 3, None),
                                                  (2, 40, 128, 5, 3), (5, 256, 256, 3, None),
                                                  (1, 16, 16, 3, 1), (2, 128, 128, 1, 2)])
@@ -77,11 +108,14 @@ def test_conv_wgrad(B, cin, cout, k, splits):
     from deep_go_amd.ops import functional as Fn
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    got = Fn.conv_wgrad(dz, x, k, splits=splits)
+    got, gp, gb = Fn.conv_wgrad(dz, x, k, splits=splits, with_bias=True)
     w0 = torch.zeros(cout, k, k, cin, device=DEV, requires_grad=True)
     y = conv_ref(x, w0, k)
     (gw,) = torch.autograd.grad(y, w0, dz)
     assert rel_err(got, gw) < 1e-3
+    # fused bias grads (column sums of dZ)
+    assert rel_err(gp, dz.sum(0).reshape(cout, 361).t()) < 1e-4
+    assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
 
 
 @pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True), (2, 32, 1, False),
@@ -90,7 +124,7 @@ def test_head(B, C, k, relu):
     torch.manual_seed(4)
     from deep_go_amd.ops import functional as Fn
     x = bf(torch.relu(torch.randn(B, C, 19, 19, device=DEV)))
-    w = torch.randn(1, k, k, C, device=DEV) * 0.05
+    w = bf(torch.randn(1, k, k, C, device=DEV) * 0.05)  # fwd dots use bf16 weights
     b = torch.randn(1, device=DEV) * 0.1
     pb = torch.randn(361, device=DEV) * 0.1
     labels = torch.randint(0, 361, (B,), device=DEV)
