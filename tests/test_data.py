@@ -1,0 +1,95 @@
+"""Dataset index, packed dataset and threaded loader."""
+import numpy as np
+import pytest
+
+from deep_go_amd.data.dataset import (GameIndex, PackedDataset, load_index, sample_reference,
+                                      write_counts)
+from deep_go_amd.data.loader import BatchLoader
+
+
+@pytest.fixture(scope="module")
+def train_index(ref_data):
+    return load_index(ref_data, "train", build_missing=False)
+
+
+def test_index_parsing(ref_data, train_index):
+    # 21 listed games, one with count 0 and no directory -> 20 usable, 4139 positions
+    assert len(train_index) == 20
+    assert train_index.num_positions == 4139
+    assert load_index(ref_data, "validation").num_positions == 134
+    assert load_index(ref_data, "test").num_positions == 125
+
+
+def test_write_counts_matches_reference_index(ref_data, tmp_path):
+    import shutil
+    root = tmp_path / "data"
+    shutil.copytree(f"{ref_data}/test", root / "test")
+    write_counts(str(root), "test")
+    idx = load_index(str(root), "test")
+    assert [n for _, n in idx.games] == [125]
+
+
+def test_packed_matches_files(train_index):
+    pk = PackedDataset.from_index(train_index)
+    assert len(pk) == 4139 and pk.num_games == 20
+    lf = BatchLoader(train_index, 16, threads=3, prefetch=3, seed=7, pin=False)
+    lp = BatchLoader(pk, 16, threads=2, prefetch=2, seed=7, pin=False)
+    for _ in range(5):
+        a, b = lf.next_numpy(), lp.next_numpy()
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    assert lf.errors() == 0
+    lf.close()
+    lp.close()
+
+
+def test_loader_deterministic_across_thread_counts(train_index):
+    pk = PackedDataset.from_index(train_index)
+    runs = []
+    for threads in (1, 5):
+        ld = BatchLoader(pk, 32, threads=threads, prefetch=4, seed=123, pin=False)
+        runs.append([ld.next_numpy()[3] for _ in range(6)])
+        ld.close()
+    assert all(np.array_equal(a, b) for a, b in zip(*runs))
+
+
+def test_game_uniform_sampling_bias():
+    """The reference samples a game uniformly then a move uniformly (data.lua:29-37): a
+    game with 10 positions is drawn as often as one with 1000."""
+    counts = [10, 1000]
+    pk = PackedDataset.from_arrays(np.zeros((1010, 9, 19, 19), np.uint8), np.ones(1010),
+                                   np.ones(1010), np.arange(1010) % 361, game_size=10)
+    pk.game_start = np.array([0, 10])
+    pk.game_count = np.array(counts, np.int32)
+    ld = BatchLoader(pk, 256, threads=2, prefetch=2, seed=1, pin=False)
+    small = 0
+    n = 0
+    impl = ld._impl
+    for k in range(40):
+        s = impl.sample_batch(k)
+        small += sum(1 for g, _ in s if g == 0)
+        n += len(s)
+    ld.close()
+    assert 0.4 < small / n < 0.6
+    g, m = sample_reference(counts, 20000, np.random.default_rng(0))
+    assert 0.45 < (g == 0).mean() < 0.55 and m.min() >= 1
+
+
+def test_position_uniform_sampling():
+    pk = PackedDataset.from_arrays(np.zeros((1010, 9, 19, 19), np.uint8), np.ones(1010),
+                                   np.ones(1010), np.arange(1010) % 361)
+    pk.game_start = np.array([0, 10])
+    pk.game_count = np.array([10, 1000], np.int32)
+    ld = BatchLoader(pk, 256, threads=1, prefetch=2, seed=1, sampling="position", pin=False)
+    s = [g for k in range(20) for g, _ in ld._impl.sample_batch(k)]
+    ld.close()
+    assert np.mean(np.array(s) == 0) < 0.03
+
+
+def test_packed_save_load(tmp_path, train_index):
+    pk = PackedDataset.from_index(train_index)
+    p = str(tmp_path / "t.npz")
+    pk.save(p)
+    q = PackedDataset.load(p)
+    assert np.array_equal(pk.planes, q.planes) and np.array_equal(pk.label, q.label)
+    assert np.array_equal(pk.game_count, q.game_count)
