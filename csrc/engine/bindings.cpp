@@ -239,7 +239,7 @@ class PyLoader {
            int threads, const std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t>>&
                slots,
            uint64_t seed, bool position_uniform, uintptr_t pk_planes, uintptr_t pk_player,
-           uintptr_t pk_rank, uintptr_t pk_label) {
+           uintptr_t pk_rank, uintptr_t pk_label, int64_t start_seq) {
     std::vector<GameRef> g;
     for (auto& t : games) g.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t)});
     std::vector<SlotBuffers> sb;
@@ -249,7 +249,7 @@ class PyLoader {
     impl_ = std::make_unique<Loader>(std::move(g), batch, threads, std::move(sb), seed,
                                      position_uniform, (const uint8_t*)pk_planes,
                                      (const uint8_t*)pk_player, (const uint8_t*)pk_rank,
-                                     (const int32_t*)pk_label);
+                                     (const int32_t*)pk_label, start_seq);
   }
   py::tuple next() {
     int64_t seq = -1;
@@ -478,7 +478,11 @@ PYBIND11_MODULE(_dgcpu, m) {
   py::class_<PyLoader>(m, "Loader")
       .def(py::init<const std::vector<std::tuple<std::string, int64_t, int>>&, int, int,
                     const std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t>>&,
-                    uint64_t, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t>())
+                    uint64_t, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t>(),
+           py::arg("games"), py::arg("batch"), py::arg("threads"), py::arg("slots"),
+           py::arg("seed"), py::arg("position_uniform"), py::arg("pk_planes") = 0,
+           py::arg("pk_player") = 0, py::arg("pk_rank") = 0, py::arg("pk_label") = 0,
+           py::arg("start_seq") = 0)
       .def("next", &PyLoader::next)
       .def("release", &PyLoader::release)
       .def("stop", &PyLoader::stop)

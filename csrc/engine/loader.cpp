@@ -20,7 +20,7 @@ inline uint64_t splitmix64(uint64_t x) {
 Loader::Loader(std::vector<GameRef> games, int batch, int threads, std::vector<SlotBuffers> slots,
                uint64_t seed, bool position_uniform, const uint8_t* packed_planes,
                const uint8_t* packed_player, const uint8_t* packed_rank,
-               const int32_t* packed_label)
+               const int32_t* packed_label, int64_t start_seq)
     : games_(std::move(games)),
       batch_(batch),
       slots_(std::move(slots)),
@@ -40,6 +40,8 @@ Loader::Loader(std::vector<GameRef> games, int batch, int threads, std::vector<S
   for (size_t i = 0; i < games_.size(); ++i) cum_[i + 1] = cum_[i] + games_[i].count;
   slot_seq_.assign(slots_.size(), -1);
   slot_state_.assign(slots_.size(), 0);
+  // resume: batch numbers continue from start_seq (slot = seq % nslots)
+  produce_next_ = consume_next_ = start_seq;
   threads = std::max(1, threads);
   for (int t = 0; t < threads; ++t) threads_.emplace_back([this] { worker(); });
 }

@@ -40,7 +40,8 @@ class Loader {
   // Packed source arrays must outlive the loader (the Python wrapper keeps them alive).
   Loader(std::vector<GameRef> games, int batch, int threads, std::vector<SlotBuffers> slots,
          uint64_t seed, bool position_uniform, const uint8_t* packed_planes,
-         const uint8_t* packed_player, const uint8_t* packed_rank, const int32_t* packed_label);
+         const uint8_t* packed_player, const uint8_t* packed_rank, const int32_t* packed_label,
+         int64_t start_seq = 0);
   ~Loader();
   Loader(const Loader&) = delete;
 

@@ -43,9 +43,10 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
                                 hipStream_t s);
 int dg_bias_chunks(int B);
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
-                  hipStream_t s);
+                  const float* gate, hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
-                      float decay, float gscale, hipStream_t s);
+                      float decay, float gscale, const float* gate, hipStream_t s);
+hipError_t dg_finite_gate(const float* loss, int n, float* gate, int* bad_count, hipStream_t s);
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, hipStream_t s);
 }
@@ -132,14 +133,20 @@ PYBIND11_MODULE(_dghip, m) {
   });
   m.def("bias_chunks", [](int B) { return dg_bias_chunks(B); });
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
-                  uintptr_t stream) {
-    check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, S(stream)), "sgd");
+                  uintptr_t gate, uintptr_t stream) {
+    check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, P<float>(gate), S(stream)),
+          "sgd");
   });
   m.def("rmsprop", [](uintptr_t p, uintptr_t g, uintptr_t ms, size_t n, uintptr_t lr,
-                      float decay, float gscale, uintptr_t stream) {
+                      float decay, float gscale, uintptr_t gate, uintptr_t stream) {
     check(dg_rmsprop(P<float>(p), P<float>(g), P<float>(ms), n, P<double>(lr), decay, gscale,
-                     S(stream)),
+                     P<float>(gate), S(stream)),
           "rmsprop");
+  });
+  m.def("finite_gate", [](uintptr_t loss, int n, uintptr_t gate, uintptr_t bad,
+                          uintptr_t stream) {
+    check(dg_finite_gate(P<float>(loss), n, P<float>(gate), P<int>(bad), S(stream)),
+          "finite_gate");
   });
   m.def("lr_decay", [](uintptr_t lr, double decay, uintptr_t step, uintptr_t stream) {
     check(dg_lr_decay(P<double>(lr), decay, P<long long>(step), S(stream)), "lr_decay");

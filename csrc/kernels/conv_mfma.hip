@@ -259,9 +259,9 @@ conv_wgrad_kernel(WgradArgs a) {
   // one XCD and hit its L2, instead of re-streaming from the Infinity Cache.
   const int nwg = a.ktiles * a.mtiles * a.splits;
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, slot = bid >> 3;
+  const int xcd = bid & 7, xslot = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
   const int kt = lid % a.ktiles;
   const int rest = lid / a.ktiles;
   const int mt = rest % a.mtiles;

@@ -130,8 +130,10 @@ bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
 // SGD (optimizer.lua:24-27): theta -= lr * g over the flat fp32 master buffer.  lr lives
 // on the device (double) so the step can be replayed inside a hipGraph.
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n,
-                           const double* __restrict__ lr, float gscale) {
-  const float l = (float)(*lr) * gscale;
+                           const double* __restrict__ lr, float gscale,
+                           const float* __restrict__ gate) {
+  // gate (optional, device): 0 skips the update (non-finite loss policy, graph-friendly)
+  const float l = (float)(*lr) * gscale * (gate ? *gate : 1.f);
   const size_t n4 = n / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -149,14 +151,31 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, s
 // ms = decay*ms + (1-decay)*g^2 ; theta -= lr * g / sqrt(ms); ms initialised to 1.
 __global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
                                float* __restrict__ ms, size_t n, const double* __restrict__ lr,
-                               float decay, float gscale) {
-  const float l = (float)(*lr);
+                               float decay, float gscale, const float* __restrict__ gate) {
+  const float l = (float)(*lr) * (gate ? *gate : 1.f);
+  if (gate && *gate == 0.f) return;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
     const float m = decay * ms[i] + (1.f - decay) * gi * gi;
     ms[i] = m;
     p[i] -= l * gi * rsqrtf(m);
+  }
+}
+
+// gate = isfinite(sum(loss[0..n))) ? 1 : 0 — one workgroup; feeds the optimizer gate.
+__global__ void finite_gate_kernel(const float* __restrict__ loss, int n, float* __restrict__ gate,
+                                   int* __restrict__ bad_count) {
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  int bad = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) bad |= !isfinite(loss[i]);
+  if (bad) atomicOr(&s_bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *gate = s_bad ? 0.f : 1.f;
+    if (s_bad && bad_count) *bad_count += 1;
   }
 }
 
@@ -224,20 +243,26 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
 
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
-                  hipStream_t s) {
+                  const float* gate, hipStream_t s) {
   int blocks = (int)((n / 4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sgd_kernel, dim3(blocks), dim3(256), 0, s, p, g, n, lr, gscale);
+  hipLaunchKernelGGL(sgd_kernel, dim3(blocks), dim3(256), 0, s, p, g, n, lr, gscale, gate);
   return hipGetLastError();
 }
 
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
-                      float decay, float gscale, hipStream_t s) {
+                      float decay, float gscale, const float* gate, hipStream_t s) {
   int blocks = (int)((n + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, s, p, g, ms, n, lr, decay,
-                     gscale);
+                     gscale, gate);
+  return hipGetLastError();
+}
+
+hipError_t dg_finite_gate(const float* loss, int n, float* gate, int* bad_count,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(finite_gate_kernel, dim3(1), dim3(256), 0, s, loss, n, gate, bad_count);
   return hipGetLastError();
 }
 

@@ -19,7 +19,7 @@ from .dataset import GameIndex, PackedDataset
 
 class BatchLoader:
     def __init__(self, source, batch: int, threads: int = 8, prefetch: int = 4, seed: int = 0,
-                 sampling: str = "game", pin: Optional[bool] = None):
+                 sampling: str = "game", pin: Optional[bool] = None, start_seq: int = 0):
         if prefetch < 2:
             raise ValueError("prefetch must be >= 2")
         self.batch = batch
@@ -44,7 +44,8 @@ class BatchLoader:
         else:
             raise TypeError("source must be a GameIndex or PackedDataset")
         self._impl = cpu().Loader(games, B, threads, slots, int(seed) & (2 ** 64 - 1),
-                                  sampling == "position", *pk)
+                                  sampling == "position", *pk, int(start_seq))
+        self.consumed = int(start_seq)
         self._pending = []  # (slot, event) awaiting release
 
     def next_host(self):
@@ -52,6 +53,7 @@ class BatchLoader:
         slot, seq = self._impl.next()
         if slot < 0:
             raise RuntimeError("loader stopped")
+        self.consumed = seq + 1
         return slot, seq
 
     def release(self, slot: int):

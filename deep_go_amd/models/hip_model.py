@@ -88,6 +88,9 @@ class HipGoNet:
         self.ms = None
         if cfg.optimizer == "rmsprop":
             self.ms = torch.ones_like(self.params)
+        # non-finite loss guard (cfg.nan_policy == "skip"): device gate read by the optimizer
+        self.gate = torch.ones(1, dtype=torch.float32, device=dev)
+        self.bad_steps = torch.zeros(1, dtype=torch.int32, device=dev)
 
         # ---- per-layer plans + bf16 operand weights ----
         self.plans: List[ConvPlan] = []
@@ -140,6 +143,10 @@ class HipGoNet:
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.loss = torch.zeros(B, dtype=torch.float32, device=dev)
         self.pred = torch.zeros(B, dtype=torch.int32, device=dev)
+        # evaluation writes its own outputs so it never clobbers the training step's loss
+        # (read by the optimizer's finite gate)
+        self.eval_loss = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.eval_pred = torch.zeros(B, dtype=torch.int32, device=dev)
         hdl = L[-1]
         self.head_gw_part = torch.zeros((B, hdl.k * hdl.k * hdl.cin), dtype=torch.float32,
                                         device=dev)
@@ -202,8 +209,8 @@ class HipGoNet:
                                           G + hd.b_off * f4, G + hd.pos_off * f4))
         self._head_eval = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
                                     P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
-                                    self.labels.data_ptr(), self.loss.data_ptr(),
-                                    self.pred.data_ptr(), 0, 0, 0, 0, 0, 0,
+                                    self.labels.data_ptr(), self.eval_loss.data_ptr(),
+                                    self.eval_pred.data_ptr(), 0, 0, 0, 0, 0, 0,
                                     int(self.cfg.head_relu), 1.0 / self.global_batch))
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -290,12 +297,18 @@ class HipGoNet:
     def optimizer_step(self, grad_scale: float = 1.0):
         s = stream_handle()
         n = self.layout.numel
+        gate = 0
+        if self.cfg.nan_policy == "skip":
+            self.h.finite_gate(self.loss.data_ptr(), self.B, self.gate.data_ptr(),
+                               self.bad_steps.data_ptr(), s)
+            gate = self.gate.data_ptr()
         if self.ms is not None:
             self.h.rmsprop(self.params.data_ptr(), self.grads.data_ptr(), self.ms.data_ptr(), n,
-                           self.lr.data_ptr(), float(self.cfg.rmsprop_decay), grad_scale, s)
+                           self.lr.data_ptr(), float(self.cfg.rmsprop_decay), grad_scale, gate,
+                           s)
         else:
             self.h.sgd(self.params.data_ptr(), self.grads.data_ptr(), n, self.lr.data_ptr(),
-                       grad_scale, s)
+                       grad_scale, gate, s)
         self.h.lr_decay(self.lr.data_ptr(), float(self.cfg.rateDecay),
                         self.step_count.data_ptr(), s)
         self.refresh_weights()
@@ -424,7 +437,8 @@ class SegmentedStep:
         self.opt_graph = g
         torch.cuda.synchronize()
 
-    def __call__(self):
+    def forward_backward(self):
+        """Gradients (all-reduced across ranks when DP) of the batch in the input buffers."""
         for si, (fns, fire) in enumerate(self.segments):
             if self.use_graphs:
                 self.graphs[si].replay()
@@ -435,7 +449,13 @@ class SegmentedStep:
                     self.bucketer.fire(b)
         if self.bucketer is not None:
             self.bucketer.wait()
+
+    def optimizer(self):
         if self.use_graphs:
             self.opt_graph.replay()
         else:
             self.net.optimizer_step()
+
+    def __call__(self):
+        self.forward_backward()
+        self.optimizer()

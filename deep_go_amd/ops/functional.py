@@ -208,7 +208,7 @@ def sgd_(p: torch.Tensor, g: torch.Tensor, lr: float, decay: float, steps: int =
     lrt = torch.tensor([lr], dtype=torch.float64, device=p.device)
     s = stream_handle()
     for _ in range(steps):
-        h.sgd(p.data_ptr(), g.data_ptr(), p.numel(), lrt.data_ptr(), 1.0, s)
+        h.sgd(p.data_ptr(), g.data_ptr(), p.numel(), lrt.data_ptr(), 1.0, 0, s)
         h.lr_decay(lrt.data_ptr(), decay, 0, s)
     return lrt
 

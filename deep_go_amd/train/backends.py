@@ -1,0 +1,211 @@
+"""Compute backends behind the Experiment (one per device type).
+
+Both expose the same small surface used by the training loop:
+  set_batch(planes uint8 [B,9,19,19], player, rank, labels)   (host numpy or tensors)
+  forward_backward()         loss/argmax of the batch + gradients (global-batch mean)
+  optimizer_step()           SGD/RMSProp + per-step LR decay
+  evaluate(n)                forward only on the first n boards of the current batch
+  loss_sum() / correct()     of the last forward (host floats; synchronising)
+  params / rate / state_dict / load_state_dict
+
+* ``CPUBackend`` — fp32 PyTorch on the CPU (the reference's useCuda=false path,
+  experiments.lua:97; also the numerical oracle).  DP over gloo.
+* ``HIPBackend`` — the MI355X executor (models/hip_model.py) with hipGraph replay and, for
+  world > 1, RCCL gradient buckets overlapped with backward.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..config import ExperimentConfig
+from ..models.gocnn import ParamLayout, init_params, reference_forward
+from ..ops.native import cpu
+from ..parallel import dp
+from .optim import SGD, RMSProp
+
+
+def _np(x, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy().astype(dtype, copy=False)
+    return np.asarray(x, dtype=dtype)
+
+
+class CPUBackend:
+    def __init__(self, cfg: ExperimentConfig, batch: int, flat: Optional[torch.Tensor] = None,
+                 world: int = 1, bucket_mb: float = 4.0):
+        self.cfg = cfg
+        self.layout = ParamLayout(cfg)
+        self.B = batch
+        self.world = world
+        self.params = (flat.clone().float() if flat is not None
+                       else init_params(self.layout, cfg.seed)).contiguous()
+        self.params.requires_grad_(True)
+        if cfg.optimizer == "rmsprop":
+            self.opt = RMSProp(cfg.rate, cfg.rmsprop_decay, self.layout.numel)
+        else:
+            self.opt = SGD(cfg.rate, cfg.rateDecay)
+        self._x = None
+        self._y = None
+        self._loss_sum = 0.0
+        self._correct = 0
+        self.bucketer = None
+        if world > 1:
+            ranges = [self.layout.layer_range(i) for i in range(len(self.layout.layers))]
+            self.buckets = dp.make_buckets(ranges, int(bucket_mb * 2 ** 20))
+        self.nan_skipped = 0
+        self._last = "train"
+        self._eval = (0.0, 0)
+
+    @property
+    def rate(self) -> float:
+        return self.opt.rate
+
+    def set_batch(self, planes, player, rank, labels):
+        pl = _np(planes, np.uint8).reshape(-1, 9, 19, 19)
+        self._x = torch.from_numpy(cpu().expand(pl, _np(player, np.uint8), _np(rank, np.uint8)))
+        self._y = torch.from_numpy(_np(labels, np.int64))
+
+    def _forward(self, x):
+        return reference_forward(self.layout, self.params, x, head_relu=self.cfg.head_relu)
+
+    def forward_backward(self):
+        if self.params.grad is not None:
+            self.params.grad.zero_()
+        logp = self._forward(self._x)
+        # mean over the GLOBAL batch: local mean / world, then SUM all-reduce
+        loss = F.nll_loss(logp, self._y, reduction="sum") / (self.B * self.world)
+        loss.backward()
+        with torch.no_grad():
+            self._loss_sum = float(F.nll_loss(logp, self._y, reduction="sum"))
+            self._correct = int((logp.argmax(1) == self._y).sum())
+        self._last = "train"
+        if self.world > 1:
+            g = self.params.grad
+            works = [torch.distributed.all_reduce(g[s:e], async_op=True)
+                     for s, e, _ in self.buckets]
+            for w in works:
+                w.wait()
+
+    def optimizer_step(self):
+        if self.cfg.nan_policy == "skip" and not np.isfinite(self._loss_sum):
+            self.nan_skipped += 1
+            self.opt.rate = self.opt.rate * (1.0 - getattr(self.opt, "rate_decay", 0.0))
+            return
+        with torch.no_grad():
+            self.opt.step(self.params, self.params.grad)
+
+    @torch.no_grad()
+    def evaluate(self, n: Optional[int] = None):
+        x, y = self._x, self._y
+        if n is not None:
+            x, y = x[:n], y[:n]
+        logp = self._forward(x)
+        self._eval = (float(F.nll_loss(logp, y, reduction="sum")),
+                      int((logp.argmax(1) == y).sum()))
+        self._last = "eval"
+        return logp
+
+    def loss_sum(self) -> float:
+        return self._eval[0] if self._last == "eval" else self._loss_sum
+
+    def correct(self) -> int:
+        return self._eval[1] if self._last == "eval" else self._correct
+
+    def flat_params(self) -> torch.Tensor:
+        return self.params.detach()
+
+    def load_params(self, flat: torch.Tensor):
+        with torch.no_grad():
+            self.params.copy_(flat.float())
+
+    def state_dict(self):
+        return {"optimizer": self.opt.state_dict()}
+
+    def load_state_dict(self, d):
+        self.opt.load_state_dict(d["optimizer"])
+
+
+class HIPBackend:
+    def __init__(self, cfg: ExperimentConfig, batch: int, flat: Optional[torch.Tensor] = None,
+                 world: int = 1, device=None, use_graphs: bool = True, bucket_mb: float = 4.0,
+                 grad_dtype: str = "fp32"):
+        from ..models.hip_model import HipGoNet, SegmentedStep
+        self.cfg = cfg
+        self.B = batch
+        self.world = world
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.net = HipGoNet(cfg, batch, device=self.device, flat_params=flat,
+                            global_batch=batch * world)
+        self.layout = self.net.layout
+        if world > 1 and flat is None:
+            dp.broadcast_(self.net.params, 0)
+            self.net.refresh_weights()
+        self.bucketer = None
+        if world > 1:
+            ranges = [self.layout.layer_range(i) for i in range(len(self.layout.layers))]
+            self.bucketer = dp.GradBucketer(self.net.grads,
+                                            dp.make_buckets(ranges, int(bucket_mb * 2 ** 20)),
+                                            grad_dtype=grad_dtype)
+        self._step = SegmentedStep(self.net, self.bucketer, use_graphs=use_graphs)
+        self._eval_n = batch
+        self._last = "train"
+
+    @property
+    def rate(self) -> float:
+        return float(self.net.lr.item())
+
+    @property
+    def params(self):
+        return self.net.params
+
+    def set_batch(self, planes, player, rank, labels):
+        dev = self.device
+        t = lambda a, dt: (a if isinstance(a, torch.Tensor) else torch.from_numpy(np.asarray(a)))
+        self.net.set_batch(t(planes, None).to(dev), t(player, None).to(dev),
+                           t(rank, None).to(dev), t(labels, None).to(dev, torch.int32))
+
+    def forward_backward(self):
+        self._step.forward_backward()
+        self._last = "train"
+
+    def optimizer_step(self):
+        self._step.optimizer()
+
+    def evaluate(self, n: Optional[int] = None):
+        self._eval_n = n or self.B
+        self.net.evaluate()
+        self._last = "eval"
+
+    def loss_sum(self) -> float:
+        if self._last == "eval":
+            return float(self.net.eval_loss[:self._eval_n].sum().item())
+        return float(self.net.loss.sum().item())
+
+    def correct(self) -> int:
+        if self._last == "eval":
+            n = self._eval_n
+            return int((self.net.eval_pred[:n] == self.net.labels[:n]).sum().item())
+        return int((self.net.pred == self.net.labels).sum().item())
+
+    def flat_params(self) -> torch.Tensor:
+        return self.net.params.detach().cpu()
+
+    def load_params(self, flat: torch.Tensor):
+        self.net.load_params(flat)
+
+    def state_dict(self):
+        d = {"optimizer": {"kind": self.cfg.optimizer, "rate": self.rate,
+                           "rate_decay": self.cfg.rateDecay}}
+        if self.net.ms is not None:
+            d["optimizer"]["ms"] = self.net.ms.detach().cpu()
+        return d
+
+    def load_state_dict(self, d):
+        o = d["optimizer"]
+        self.net.lr.fill_(float(o["rate"]))
+        if "ms" in o and self.net.ms is not None:
+            self.net.ms.copy_(o["ms"].to(self.net.ms.device))

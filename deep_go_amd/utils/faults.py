@@ -1,0 +1,87 @@
+"""Failure detection and fault injection.
+
+Reference: a ``pcall`` around the first of its two fwd/bwd passes stashes a failing batch in
+globals (``train.lua:106-109``); nothing else (no watchdog, no NaN handling).
+
+Here:
+* ``check_finite`` — NaN/Inf guard on the loss (policy ``raise`` dumps the offending batch
+  to ``<dir>/bad_batch_<step>.npz`` then raises; policy ``skip`` leaves the update to the
+  optimizer gate so the step is skipped but the LR still decays).
+* ``StepWatchdog`` — a thread that aborts the process (``os._exit``) when a training step
+  does not finish within a timeout, so a hung collective cannot wedge a node forever;
+  torch.distributed's own collective timeout also applies.
+* ``DG_FAULT=rank:step:kind`` fault injection for tests: kinds ``nan`` (poison the loss),
+  ``raise`` (exception), ``hang`` (sleep past the watchdog), ``exit`` (hard exit code 17).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Optional
+
+import numpy as np
+
+
+class NonFiniteLoss(RuntimeError):
+    pass
+
+
+def parse_fault(spec: Optional[str] = None):
+    spec = spec if spec is not None else os.environ.get("DG_FAULT", "")
+    if not spec:
+        return None
+    rank, step, kind = spec.split(":")
+    return int(rank), int(step), kind
+
+
+def maybe_inject(rank: int, step: int, spec=None):
+    """Returns 'nan' when the loss of this step must be poisoned; raises / hangs / exits for
+    the other kinds."""
+    f = parse_fault(spec) if spec is None or isinstance(spec, str) else spec
+    if not f or f[0] != rank or f[1] != step:
+        return None
+    kind = f[2]
+    if kind == "raise":
+        raise RuntimeError(f"DG_FAULT injected exception at rank {rank} step {step}")
+    if kind == "hang":
+        time.sleep(3600)
+    if kind == "exit":
+        os._exit(17)
+    return kind
+
+
+def check_finite(loss_sum: float, step: int, policy: str, batch=None, dump_dir: str = "."):
+    if np.isfinite(loss_sum):
+        return True
+    if policy == "skip":
+        return False
+    if batch is not None:
+        path = os.path.join(dump_dir, f"bad_batch_{step}.npz")
+        np.savez(path, *[np.asarray(b) for b in batch])
+    raise NonFiniteLoss(f"non-finite loss {loss_sum} at step {step}")
+
+
+class StepWatchdog:
+    def __init__(self, timeout_s: float, on_timeout=None):
+        self.timeout = timeout_s
+        self.on_timeout = on_timeout
+        self._beat = time.monotonic()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def beat(self):
+        self._beat = time.monotonic()
+
+    def _run(self):
+        while not self._stop.wait(min(1.0, self.timeout / 4)):
+            if time.monotonic() - self._beat > self.timeout:
+                if self.on_timeout:
+                    self.on_timeout()
+                else:
+                    print(f"[watchdog] no step progress for {self.timeout}s: aborting", flush=True)
+                    os._exit(42)
+
+    def stop(self):
+        self._stop.set()

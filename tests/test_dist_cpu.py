@@ -1,0 +1,104 @@
+"""Data parallelism without a cluster (SURVEY.md §4.3 'Distributed tests'):
+
+(a) DP=k with per-rank batch B/k gives the same update as DP=1 with batch B;
+(b) a CPU gloo world exercises the bucketing / async all-reduce logic;
+(c) the bucket scheduler is unit-tested without any communicator."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deep_go_amd.config import ExperimentConfig
+from deep_go_amd.parallel.dp import GradBucketer, make_buckets
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_make_buckets_reverse_order_and_sizes():
+    ranges = [(0, 100), (100, 300), (300, 350), (350, 1000)]
+    b = make_buckets(ranges, bucket_bytes=4 * 250)
+    # walk from the last layer: [350,1000) fills a bucket; then [100,350) (2 layers) ...
+    assert b[0] == (350, 1000, 3)
+    assert b[1] == (100, 350, 1)
+    assert b[-1][0] == 0 and b[-1][2] == 0
+    covered = sorted((s, e) for s, e, _ in b)
+    assert covered[0][0] == 0 and covered[-1][1] == 1000
+    assert all(covered[i][1] == covered[i + 1][0] for i in range(len(covered) - 1))
+
+
+def _data(B, seed=0):
+    from deep_go_amd.data.synthetic import random_planes
+    return random_planes(B, seed=seed)
+
+
+def _dp_worker(rank, world, port, B, out_path, grad_dtype):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deep_go_amd.models.gocnn import ParamLayout
+    from deep_go_amd.train.backends import CPUBackend
+    cfg = ExperimentConfig(numLayers=3, channelSize=16, rate=0.1, seed=5, bucket_mb=0.01)
+    be = CPUBackend(cfg, B // world, world=world, bucket_mb=0.01)
+    planes, player, rank_, labels = _data(B)
+    sl = slice(rank * (B // world), (rank + 1) * (B // world))
+    for step in range(3):
+        be.set_batch(planes[sl], player[sl], rank_[sl], labels[sl])
+        be.forward_backward()
+        be.optimizer_step()
+    # GradBucketer (async buckets + optional bf16 wire format) on the same world
+    g = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+    bk = GradBucketer(g, make_buckets([(0, 400), (400, 1000)], 4 * 300), grad_dtype=grad_dtype)
+    for i in range(len(bk.buckets)):
+        bk.fire(i)
+    bk.wait()
+    if rank == 0:
+        torch.save({"params": be.flat_params().clone(), "g": g.clone()}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_dp2_equals_dp1(tmp_path, grad_dtype):
+    B = 8
+    out2 = str(tmp_path / "dp2.pt")
+    mp.spawn(_dp_worker, args=(2, _free_port(), B, out2, grad_dtype), nprocs=2, join=True)
+    out1 = str(tmp_path / "dp1.pt")
+    mp.spawn(_dp_worker, args=(1, _free_port(), B, out1, grad_dtype), nprocs=1, join=True)
+    a = torch.load(out2, weights_only=True)
+    b = torch.load(out1, weights_only=True)
+    assert torch.allclose(a["params"], b["params"], atol=1e-6, rtol=1e-5)
+    ref = torch.arange(1000, dtype=torch.float32) * 3  # sum over ranks of (rank+1)*i
+    if grad_dtype == "fp32":
+        assert torch.equal(a["g"], ref)
+    else:
+        assert torch.allclose(a["g"], ref, rtol=1e-2)
+
+
+def _exp_worker(rank, world, port, ref_data, ckdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from deep_go_amd.train.experiment import Experiment
+    cfg = ExperimentConfig(numLayers=2, channelSize=16, batchSize=4, validationSize=12,
+                           validation_interval=3, log_interval=3, useCuda=False,
+                           data_root=ref_data, checkpoint_dir=ckdir, loader_threads=1,
+                           prefetch=2, seed=1)
+    e = Experiment(cfg, id="dist")
+    res = e.run(6)
+    assert e.iterations == 6 and len(e.validation_costs) == 2
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_experiment_runs_under_gloo_world2(tmp_path, ref_data):
+    mp.spawn(_exp_worker, args=(2, _free_port(), ref_data, str(tmp_path)), nprocs=2, join=True)
+    assert os.path.exists(tmp_path / "dist.model")  # rank 0 checkpoint only

@@ -101,8 +101,8 @@ def test_eval_matches_train_forward():
     cfg, net, data = _setup(3, 64, 7)
     net.evaluate()
     torch.cuda.synchronize()
-    l1 = net.loss.clone()
-    p1 = net.pred.clone()
+    l1 = net.eval_loss.clone()
+    p1 = net.eval_pred.clone()
     net.forward_backward()
     torch.cuda.synchronize()
     assert torch.allclose(l1, net.loss)

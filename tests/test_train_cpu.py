@@ -1,0 +1,208 @@
+"""Training loop, optimizer, validation, checkpoint/resume on the CPU path
+(§5.3-5.4)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deep_go_amd.config import ExperimentConfig, get_preset
+from deep_go_amd.models.gocnn import ParamLayout, init_params, reference_forward
+
+
+def test_param_counts_match_reference_sizing():
+    # BASELINE.md derived sizing table
+    assert ExperimentConfig(numLayers=3, channelSize=64).num_params() == 143338
+    assert ExperimentConfig(numLayers=6, channelSize=64).num_params() == 323434
+    assert ExperimentConfig(numLayers=12, channelSize=128).num_params() == 2104170
+    assert ExperimentConfig(numLayers=12, channelSize=256).num_params() == 7157098
+    lay = ParamLayout(ExperimentConfig(numLayers=3, channelSize=64))
+    assert lay.num_params == 143338
+
+
+def test_config_rejects_unknown_keys_and_presets():
+    with pytest.raises(KeyError):
+        get_preset("localtest", validation_size=100)  # the reference's silent typo
+    c = get_preset("default-experiment")
+    assert (c.numLayers, c.channelSize, c.batchSize, c.rate) == (6, 64, 64, 0.512)
+    assert c.kernels == [5, 3, 3, 3, 3, 3] and c.channels == [37, 64, 64, 64, 64, 64, 1]
+    # deep copy semantics: derived lists never alias / mutate the prototype
+    c.kernels.append(9)
+    assert get_preset("default-experiment").kernels == [5, 3, 3, 3, 3, 3]
+
+
+def test_head_relu_and_mean_nll():
+    cfg = ExperimentConfig(numLayers=2, channelSize=16)
+    lay = ParamLayout(cfg)
+    flat = init_params(lay, 0)
+    x = torch.rand(3, 37, 19, 19)
+    lp = reference_forward(lay, flat, x, head_relu=True)
+    assert torch.allclose(lp.exp().sum(1), torch.ones(3), atol=1e-5)
+    # with the head ReLU every logit is >= 0: log-probs bounded by -log(361) from above only
+    # when logits are equal; check relu actually applied by forcing negative bias
+    hd = lay.layers[-1]
+    flat2 = flat.clone()
+    flat2[hd.b_off] = -1e3
+    lp2 = reference_forward(lay, flat2, x, head_relu=True)
+    assert torch.allclose(lp2, torch.full_like(lp2, -math.log(361)), atol=1e-5)
+
+
+def test_sgd_rate_decay_matches_reference():
+    from deep_go_amd.train.optim import SGD
+    opt = SGD(0.01, 1e-7)
+    p = torch.zeros(4)
+    g = torch.ones(4)
+    for _ in range(1000):
+        opt.step(p, g)
+    assert opt.rate == pytest.approx(0.01 * (1 - 1e-7) ** 1000, rel=1e-14)
+
+
+def _cfg(tmp_path, ref_data, **kw):
+    base = dict(numLayers=3, channelSize=16, batchSize=4, validationSize=10,
+                validation_interval=5, log_interval=5, useCuda=False, data_root=ref_data,
+                checkpoint_dir=str(tmp_path), seed=3, loader_threads=2, prefetch=2)
+    base.update(kw)
+    return ExperimentConfig(**base)
+
+
+def test_localtest_end_to_end(tmp_path, ref_data, capsys):
+    from deep_go_amd.train.experiment import Experiment
+    cfg = get_preset("localtest", data_root=ref_data, checkpoint_dir=str(tmp_path),
+                     validationSize=50, loader_threads=2)
+    e = Experiment(cfg, id="lt")
+    res = e.run(20)
+    out = capsys.readouterr().out
+    assert "initializing model..." in out
+    assert "training " in out and "(samples per second" in out
+    assert "validation at iteration 20: cost=" in out
+    assert "total samples per second" in out
+    assert np.isfinite(res["train_cost"]) and len(e.validation_costs) == 1
+    assert os.path.exists(tmp_path / "lt.model")
+
+
+def test_resume_is_exact(tmp_path, ref_data):
+    from deep_go_amd.train.experiment import Experiment
+    cfg = _cfg(tmp_path, ref_data)
+    a = Experiment(cfg, id="a")
+    a.run(10)
+    path = a.save()
+    a2 = Experiment.load(path)
+    a2.id = "a2"
+    a2.run(10)
+    b = Experiment(cfg, id="b")
+    b.run(20)
+    assert torch.equal(a2.backend.flat_params(), b.backend.flat_params())
+    assert a2.backend.rate == b.backend.rate
+    assert a2.iterations == 20 and a2.loader_seq == b.loader_seq
+    assert a2.validation_costs[:2] == b.validation_costs[:2]
+
+
+def test_reset_optimizer_like_repeated_lua(tmp_path, ref_data):
+    from deep_go_amd.train.experiment import Experiment
+    cfg = _cfg(tmp_path, ref_data, rateDecay=1e-2)
+    a = Experiment(cfg, id="r")
+    a.run(5)
+    p = a.save()
+    assert Experiment.load(p)._restore_opt["rate"] == pytest.approx(cfg.rate * 0.99 ** 5)
+    r = Experiment.load(p, reset_optimizer=True)
+    r.init()
+    assert r.backend.rate == cfg.rate
+
+
+def test_checkpoint_roundtrip_and_t7_export(tmp_path, ref_data):
+    from deep_go_amd.train.experiment import Experiment
+    from deep_go_amd.utils import checkpoint as ck
+    cfg = _cfg(tmp_path, ref_data)
+    e = Experiment(cfg, id="c")
+    e.run(5)
+    p = e.save()
+    cfg2, flat, state, opt = ck.load_checkpoint(p)
+    assert cfg2 == cfg and state["iterations"] == 5
+    assert torch.equal(flat, e.backend.flat_params())
+    t7 = e.export_t7(str(tmp_path / "c.t7"))
+    cfg3, flat3, state3, rate3 = ck.import_t7(t7, cfg)
+    assert torch.equal(flat3, flat)
+    assert rate3 == pytest.approx(e.backend.rate)
+    from deep_go_amd.ops.native import cpu
+    tbl = cpu().t7_load(t7)
+    mods = tbl["model"]["modules"]
+    assert tbl["model"]["__torch_class__"] == "nn.Sequential"
+    assert mods[2]["__torch_class__"] == "nn.SpatialConvolutionMM"
+    assert mods[2]["weight"].shape == (16, 37 * 25)  # reference layout [c_out, c_in*k*k]
+    assert mods[len(mods)]["__torch_class__"] == "nn.LogSoftMax"
+
+
+class _FakeBackend:
+    """Every board costs 1 nat; board i is correct iff i is even."""
+    def __init__(self):
+        self.n = 0
+        self.lab = None
+
+    def set_batch(self, planes, player, rank, labels):
+        self.lab = np.asarray(labels)
+
+    def evaluate(self, n):
+        self.n = n
+
+    def loss_sum(self):
+        return float(self.n)
+
+    def correct(self):
+        return int(sum(1 for v in self.lab[:self.n] if v % 2 == 0))
+
+
+def test_validation_exact_and_reference_quirks():
+    from deep_go_amd.train.experiment import Experiment
+    e = Experiment(ExperimentConfig(batchSize=4), id="v")
+    e.backend = _FakeBackend()
+    e.local_batch = 4
+    N = 10
+    data = (np.zeros((N, 9, 19, 19), np.uint8), np.ones(N, np.uint8), np.ones(N, np.uint8),
+            np.arange(N, dtype=np.int32))
+    cost, acc = e.eval_batch_set(data, quirks=False)
+    assert cost == pytest.approx(1.0) and acc == pytest.approx(0.5)
+    # train.lua:23-44: floor(10/4)=2 chunks, weight bs-1=3, denominator 10; tail unevaluated
+    cost_q, acc_q = e.eval_batch_set(data, quirks=True)
+    assert cost_q == pytest.approx(2 * 3 / 10)
+    assert acc_q == pytest.approx(1 - 4 / 10)
+
+
+def test_nan_policy_and_fault_injection(tmp_path, ref_data, monkeypatch):
+    from deep_go_amd.train.experiment import Experiment
+    from deep_go_amd.utils.faults import NonFiniteLoss
+    monkeypatch.setenv("DG_FAULT", "0:3:nan")
+    e = Experiment(_cfg(tmp_path, ref_data, nan_policy="raise"), id="n")
+    with pytest.raises(NonFiniteLoss):
+        e.run(6)
+    assert any(f.startswith("bad_batch_3") for f in os.listdir(tmp_path))
+    s = Experiment(_cfg(tmp_path, ref_data, nan_policy="skip"), id="s")
+    res = s.run(6)
+    assert np.isfinite(res["train_cost"])
+    monkeypatch.setenv("DG_FAULT", "0:2:raise")
+    with pytest.raises(RuntimeError, match="DG_FAULT"):
+        Experiment(_cfg(tmp_path, ref_data), id="f").run(4)
+
+
+def test_cli_train_resume_eval(tmp_path, ref_data):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=os.getcwd())
+    base = [sys.executable, "-m", "deep_go_amd"]
+    ov = [f"data_root={ref_data}", f"checkpoint_dir={tmp_path}", "numLayers=2",
+          "channelSize=16", "batchSize=4", "validationSize=8", "validation_interval=4",
+          "loader_threads=2", "id=cli"]
+    r = subprocess.run(base + ["train", "--iters", "4", "--device", "cpu"] + ov,
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ck = json.loads(r.stdout.strip().splitlines()[-1])["checkpoint"]
+    r = subprocess.run(base + ["resume", ck, "--iters", "4", "--device", "cpu", "--id", "cli2"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip().splitlines()[-1])["iterations"] == 8
+    r = subprocess.run(base + ["eval", ck, "--split", "test", "--n", "16", "--device", "cpu"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert 0.0 <= json.loads(r.stdout.strip().splitlines()[-1])["accuracy"] <= 1.0
