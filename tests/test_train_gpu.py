@@ -1,0 +1,72 @@
+"""Experiment on the HIP backend (graphs, checkpoint/resume, CPU-vs-GPU parity, real data)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from deep_go_amd.config import ExperimentConfig
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "data_cache", "fixture")
+
+
+def _cfg(tmp_path, **kw):
+    base = dict(numLayers=4, channelSize=64, batchSize=32, validationSize=64,
+                validation_interval=10, log_interval=5, useCuda=True, synthetic=True,
+                checkpoint_dir=str(tmp_path), seed=2, loader_threads=4, prefetch=3)
+    base.update(kw)
+    return ExperimentConfig(**base)
+
+
+def test_gpu_experiment_run_and_resume(tmp_path):
+    from deep_go_amd.train.experiment import Experiment
+    e = Experiment(_cfg(tmp_path), id="g")
+    res = e.run(20)
+    assert np.isfinite(res["train_cost"]) and len(e.validation_costs) == 2
+    p = e.save()
+    r = Experiment.load(p)
+    r.id = "g2"
+    r.run(10)
+    assert r.iterations == 30
+    assert torch.isfinite(r.backend.net.params).all()
+
+
+def test_gpu_step_matches_cpu_step(tmp_path):
+    """One SGD step through the HIP kernels vs the fp32 PyTorch oracle from the same init."""
+    from deep_go_amd.data.synthetic import random_planes
+    from deep_go_amd.train.backends import CPUBackend, HIPBackend
+    cfg = _cfg(tmp_path, rate=0.05, head_relu=False)
+    cpu_be = CPUBackend(cfg, 16)
+    gpu_be = HIPBackend(cfg, 16, flat=cpu_be.flat_params().clone())
+    batch = random_planes(16, seed=4)
+    for be in (cpu_be, gpu_be):
+        be.set_batch(*batch)
+        be.forward_backward()
+        be.optimizer_step()
+    a = cpu_be.flat_params()
+    b = gpu_be.flat_params()
+    p0 = CPUBackend(cfg, 16).flat_params()
+    da, db = a - p0, b - p0
+    rel = (da - db).norm() / da.norm()
+    assert rel < 0.05, rel.item()
+    assert gpu_be.rate == pytest.approx(cpu_be.rate, rel=1e-12)
+
+
+@pytest.mark.skipif(not os.path.isdir(FIXTURE), reason="packed fixture not built")
+def test_real_data_training_reduces_loss(tmp_path):
+    from deep_go_amd.train.experiment import Experiment
+    cfg = _cfg(tmp_path, synthetic=False, data_root=FIXTURE, numLayers=6, channelSize=64,
+               batchSize=64, rate=0.05, head_relu=False, validation_interval=150,
+               validationSize=256, log_interval=20)
+    # default-experiment.lua shape (6 layers, d=64, B=64). Without the head ReLU the reference
+    # rate .512 diverges on this tiny fixture; the tools/real_data_run.py sweep (profiles/
+    # README.md) puts 0.05 at val cost ~4.2 after 300 steps.
+    e = Experiment(cfg, id="real")
+    e.run(300)
+    assert e.train_costs[-1] < e.train_costs[0] - 0.5, e.train_costs
+    assert e.validation_costs[-1] < 5.0, e.validation_costs
+    cost, acc = e.evaluate_split("test", 125)
+    assert np.isfinite(cost) and acc > 0.0
