@@ -24,6 +24,10 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_wgrad_set_ablate(int mode);
+void dg_conv_wgrad3_set_ablate(int mode);
+int dg_wgrad3_tiles(int Mpad, int x_C);
+hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad, const void* X, int x_pad,
+                          int x_C, int B, int KP, int splits, float* slab, hipStream_t stream);
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
@@ -97,6 +101,13 @@ PYBIND11_MODULE(_dghip, m) {
                         splits, P<float>(slab), S(stream)),
           "conv_wgrad");
   });
+  m.def("conv_wgrad3", [](uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X, int x_pad,
+                          int x_C, int B, int KP, int splits, uintptr_t slab, uintptr_t stream) {
+    check(dg_conv_wgrad3(P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, B, KP, splits,
+                         P<float>(slab), S(stream)),
+          "conv_wgrad3");
+  });
+  m.def("wgrad3_tiles", [](int Mpad, int x_C) { return dg_wgrad3_tiles(Mpad, x_C); });
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
                            uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {
@@ -157,6 +168,7 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
+  m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
 }

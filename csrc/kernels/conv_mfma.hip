@@ -325,7 +325,6 @@ conv_wgrad_kernel(WgradArgs a) {
   const int q = li >> 2, pp = li & 3;
   for (int st = 0; st < nsteps; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nsteps) stage(buf ^ 1, st + 1);
     const char* sA = smem + buf * STAGE;
     const char* sB = sA + T_BYTES;
     // all 32 transposed fragment reads of the step first (distinct registers), then the
@@ -359,6 +358,9 @@ conv_wgrad_kernel(WgradArgs a) {
         }
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // next step's DMA after the tr-reads (else the compiler waits vmcnt(0) before them)
+    if (st + 1 < nsteps) stage(buf ^ 1, st + 1);
     __builtin_amdgcn_sched_barrier(0);
     if (a.ablate & 1) {
 #pragma unroll

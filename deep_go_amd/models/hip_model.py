@@ -18,6 +18,7 @@ batch 256 needs < 1 GB of HBM, so nothing is ever re-allocated in the step.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -53,6 +54,7 @@ class ConvPlan:
     bn_d: int = 128
     board: bool = False    # fwd uses the board-tiled kernel
     board_d: bool = False  # dgrad uses the board-tiled kernel
+    wgrad3: bool = False   # wgrad uses the row-stripe kernel (conv_wgrad3.hip)
 
 
 class HipGoNet:
@@ -104,9 +106,13 @@ class HipGoNet:
                 bm = LY.board_bm(spec.cout)
             KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
             Mpad_w = LY.round_up(spec.cout, 128)
-            splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
+            w3 = LY.wgrad3_ok(spec.k, cinp, spec.pad) and os.environ.get("DG_WGRAD3", "1") != "0"
+            if w3:
+                splits = LY.pick_wgrad3_splits(batch, Mpad_w, cinp, num_cus)
+            else:
+                splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
-                         Mpad, KPw, Mpad_w, splits, board=board)
+                         Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
             if spec.index > 0:
                 bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
@@ -222,9 +228,14 @@ class HipGoNet:
             # reduce launch, which also finalises the weight grad
             ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
                                               self.bpart.data_ptr())))
-            ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                       xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                       p.splits, self.slab.data_ptr())))
+            if p.wgrad3:
+                ops.append((h.conv_wgrad3, (self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                            xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
+                                            p.splits, self.slab.data_ptr())))
+            else:
+                ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                           xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
+                                           p.splits, self.slab.data_ptr())))
             ops.append((h.wgrad_reduce, (self.slab.data_ptr(), G + spec.w_off * f4, p.splits,
                                          p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp,
                                          self.bpart.data_ptr(), self.bchunks,

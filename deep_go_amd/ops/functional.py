@@ -103,7 +103,7 @@ def conv_dgrad(dz: torch.Tensor, w: torch.Tensor, aux: torch.Tensor, tiles=None)
 
 
 def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = None,
-               cinp: int | None = None, with_bias: bool = False):
+               cinp: int | None = None, with_bias: bool = False, algo: str = "auto"):
     """dW[co][kh][kw][ci] = sum_{b,p} dz[b,co,p] * x[b,ci,p+off] (fp32 OHWI).
 
     with_bias=True also returns the fused bias grads (gposb [361][co], gbias [co])."""
@@ -116,7 +116,11 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     npix = B * NPTS
     _, KPw, _ = LY.conv_dims(k, cinp, cout, 128)
     Mpad = LY.round_up(cout, 128)
-    splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad)
+    w3 = algo == "rows" or (algo == "auto" and LY.wgrad3_ok(k, cinp, pad))
+    if w3:
+        splits = splits or LY.pick_wgrad3_splits(B, Mpad, cinp)
+    else:
+        splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad)
     dzf = LY.to_frame(dz, max(1, pad))
     xf = LY.to_frame(x.to(dev), pad, cinp)
     slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)
@@ -127,8 +131,12 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     bpart = torch.empty(nch * (NPTS + 19) * cout, dtype=torch.float32, device=dev)
     s = stream_handle()
     h.bias_grad_partial(dzf.data_ptr(), B, cout, max(1, pad), bpart.data_ptr(), s)
-    h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B, KPw,
-                 splits, slab.data_ptr(), s)
+    if w3:
+        h.conv_wgrad3(dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B, KPw,
+                      splits, slab.data_ptr(), s)
+    else:
+        h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B,
+                     KPw, splits, slab.data_ptr(), s)
     h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp,
                    bpart.data_ptr(), nch, gp.data_ptr(), gb.data_ptr(), s)
     if with_bias:

@@ -103,6 +103,23 @@ def pick_wgrad_splits(npix: int, KPw: int, Mpad: int, num_cus: int = 256) -> int
     return max(1, min(target, max_split))
 
 
+def wgrad3_ok(k: int, cin_frame: int, pad: int) -> bool:
+    """Row-stripe wgrad (conv_wgrad3.hip): 3x3 layers on frames of 64k channels, pad 1-2."""
+    return k == 3 and cin_frame % 64 == 0 and 1 <= pad <= 2
+
+
+def wgrad3_tiles(Mpad: int, cin_frame: int) -> int:
+    ck = 128 if cin_frame % 128 == 0 else 64
+    return (Mpad // 128) * 3 * (cin_frame // ck)
+
+
+def pick_wgrad3_splits(batch: int, Mpad: int, cin_frame: int, num_cus: int = 256) -> int:
+    """One workgroup per CU: splits x tiles <= num_cus (single dispatch round), and every
+    split gets at least one 64-pixel step (6 per board)."""
+    tiles = wgrad3_tiles(Mpad, cin_frame)
+    return max(1, min(num_cus // tiles, batch * 6))
+
+
 def board_ok(k: int, cin_frame: int) -> bool:
     """The board-tiled kernel (conv_board.hip) handles 1x1/3x3 layers whose input frame
     has a multiple of 64 channels; everything else uses the pixel-tiled conv_nt kernel."""

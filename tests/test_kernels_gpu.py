@@ -118,6 +118,22 @@ def test_conv_wgrad(B, cin, cout, k, splits):
     assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
 
 
+@pytest.mark.parametrize("B,cin,cout,splits,algo", [
+    (3, 128, 128, None, "rows"), (3, 128, 128, None, "im2col"), (9, 128, 128, 5, "rows"),
+    (2, 64, 128, 1, "rows"), (4, 192, 64, None, "rows"), (2, 256, 256, 3, "rows"),
+    (1, 128, 128, 6, "rows")])
+def test_conv_wgrad_algos(B, cin, cout, splits, algo):
+    """Row-stripe 3x3 wgrad (conv_wgrad3.hip) vs the im2col kernel vs the fp32 reference."""
+    torch.manual_seed(5)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+    got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo=algo)
+    w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
+    (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
+    assert rel_err(got, gw) < 1e-3
+
+
 @pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True), (2, 32, 1, False),
                                         (4, 256, 3, True)])
 def test_head(B, C, k, relu):
