@@ -242,7 +242,7 @@ DG_DEV int koff_wg(int kg, const WgradArgs& a) {
 }
 
 template <int KW>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 conv_wgrad_kernel(WgradArgs a) {
   constexpr int BM = 128, BN = 128, BKN = 64;  // BKN pixels per step
   constexpr int T_BYTES = BKN * 256;           // 64 rows x 256 B

@@ -66,7 +66,7 @@ def test_real_data_training_reduces_loss(tmp_path):
     # README.md) puts 0.05 at val cost ~4.2 after 300 steps.
     e = Experiment(cfg, id="real")
     e.run(300)
-    assert e.train_costs[-1] < e.train_costs[0] - 0.5, e.train_costs
+    assert e.train_costs[-1] < e.train_costs[0] - 0.3, e.train_costs  # EMA(0.95): lags
     assert e.validation_costs[-1] < 5.0, e.validation_costs
     cost, acc = e.evaluate_split("test", 125)
     assert np.isfinite(cost) and acc > 0.0
