@@ -44,8 +44,11 @@ struct BoardArgs {
               // 8 no epilogue, 16 no per-step barrier (timing only)
 };
 
-template <int KW, int WM, int EPI>
-__global__ void __launch_bounds__(512)
+// HB = halo buffers: 2 double-buffers the per-chunk halo (one workgroup per CU, BM = 128);
+// 1 keeps a single halo image (73 KB of LDS at BM = 64), so TWO workgroups share a CU and
+// one's prologue / chunk-switch / epilogue runs under the other's MFMAs.
+template <int KW, int WM, int EPI, int HB>
+__global__ void __launch_bounds__(512, (WM == 1 ? 2 : 1))
 conv_board_kernel(BoardArgs a) {
   constexpr int WN = 8 / WM;
   constexpr int MF = 4;                   // 64 rows per wave
@@ -129,7 +132,7 @@ conv_board_kernel(BoardArgs a) {
     // spread the next chunk's halo DMA over this chunk's tap steps: wave-local instruction
     // k (0 .. h_per_wave-1) at step t = k; whatever is left (and the 8-wave remainder) at
     // the chunk's last step, so the whole halo has landed by the barrier ending the chunk.
-    if (c + 1 < nchunk) {
+    if (HB == 2 && c + 1 < nchunk) {
       if (t < T - 1) {
         if (t < h_per_wave) stage_H_instr((c + 1) & 1, c + 1, wave * h_per_wave + t);
       } else {
@@ -140,7 +143,7 @@ conv_board_kernel(BoardArgs a) {
       }
     }
     const char* sA = sA0 + (s & 1) * A_BYTES;
-    const char* sH = sH0 + (c & 1) * H_BYTES;
+    const char* sH = sH0 + (HB == 2 ? (c & 1) * H_BYTES : 0);
     const int toff = (t / KW - R) * F + (t % KW - R);
     // all 20 fragment reads of the step are issued before the first MFMA (distinct
     // registers), so the k-half 0 MFMAs only wait for their own operands and the k-half 1
@@ -187,6 +190,11 @@ conv_board_kernel(BoardArgs a) {
     // keep the DMA wait + barrier BELOW the MFMAs so they hide the next tile's DMA latency
     __builtin_amdgcn_sched_barrier(0);
     if (!(a.ablate & 16)) __syncthreads();
+    if (HB == 1 && t == T - 1 && c + 1 < nchunk) {
+      // single halo image: every wave is past its reads of chunk c (barrier above)
+      for (int j = wave; j < h_instr_total; j += 8) stage_H_instr(0, c + 1, j);
+      __syncthreads();
+    }
   }
 
   if (a.ablate & 8) {
@@ -285,13 +293,16 @@ void allow_lds(K kernel, size_t bytes) {
 
 template <int KW, int WM, int EPI>
 hipError_t launch(const BoardArgs& a, int B, int Mpad, hipStream_t s) {
+  constexpr int HB = WM == 1 ? 1 : 2;
   const int F = 19 + 2 * a.x_pad;
   const int hrows = (F * F + 63) / 64 * 64;
-  const size_t lds = 2 * (size_t)(64 * WM * 128) + 2 * (size_t)hrows * 128;
+  size_t lds = 2 * (size_t)(64 * WM * 128) + HB * (size_t)hrows * 128;
+  const size_t epi = (size_t)NPTS * 64 * WM * 2;  // epilogue tile reuses the staging area
+  if (epi > lds) lds = epi;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  allow_lds(conv_board_kernel<KW, WM, EPI>, lds);
-  hipLaunchKernelGGL((conv_board_kernel<KW, WM, EPI>), dim3(B, Mpad / (64 * WM)), dim3(512), lds,
-                     s, a);
+  allow_lds(conv_board_kernel<KW, WM, EPI, HB>, lds);
+  hipLaunchKernelGGL((conv_board_kernel<KW, WM, EPI, HB>), dim3(B, Mpad / (64 * WM)), dim3(512),
+                     lds, s, a);
   return hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -127,4 +129,10 @@ def board_ok(k: int, cin_frame: int) -> bool:
 
 
 def board_bm(cout: int) -> int:
-    return 64 if cout <= 64 else 128
+    """M tile of the board kernel: 64 -> single halo image, two workgroups per CU (the
+    epilogue of one overlaps the other's MFMAs); 128 -> one workgroup per CU.  DG_BOARD_BM
+    overrides (A/B benchmarking)."""
+    env = os.environ.get("DG_BOARD_BM")
+    if env:
+        return int(env)
+    return 64

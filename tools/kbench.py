@@ -48,9 +48,11 @@ def main():
     flops = 2.0 * C * C * 9 * 361 * B
     res = {}
 
-    def board():
-        h.conv_board(h.EPI_FWD, 3, 128, A.data_ptr(), KP, C, Mpad, x.data_ptr(), 1, C, B,
-                     y.data_ptr(), 1, bias.data_ptr(), posb.data_ptr(), 0, 0, s)
+    def board(bm=128, epi=None):
+        e = h.EPI_FWD if epi is None else epi
+        h.conv_board(e, 3, bm, A.data_ptr(), KP, C, Mpad, x.data_ptr(), 1, C, B,
+                     y.data_ptr(), 1, bias.data_ptr(), posb.data_ptr(),
+                     x.data_ptr() if e == h.EPI_DGRAD else 0, 1, s)
 
     def nt(bm, bn):
         def f():
@@ -63,6 +65,13 @@ def main():
             h.conv_board_set_ablate(mode)
             t = timeit(board)
             res.setdefault(f"board_ablate{mode}", []).append(round(t, 2))
+        h.conv_board_set_ablate(0)
+        for bm in (64, 128):
+            for en, e in (("fwd", h.EPI_FWD), ("dgrad", h.EPI_DGRAD)):
+                res.setdefault(f"board{bm}_{en}", []).append(
+                    round(timeit(lambda: board(bm, e)), 2))
+        h.conv_board_set_ablate(8)
+        res.setdefault("board64_fwd_noepi", []).append(round(timeit(lambda: board(64)), 2))
         h.conv_board_set_ablate(0)
         for bm, bn in ((128, 128), (128, 192)):
             res.setdefault(f"nt_{bm}x{bn}", []).append(round(timeit(nt(bm, bn)), 2))
