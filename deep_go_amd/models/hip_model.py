@@ -158,6 +158,9 @@ class HipGoNet:
                                         device=dev)
         self.head_dzb = torch.zeros((B, NUM_POINTS), dtype=torch.float32, device=dev)
 
+        # weight-gradient chain of the backward runs on its own stream (backward_layer)
+        self.side = (torch.cuda.Stream(device=dev)
+                     if os.environ.get("DG_SIDE_STREAM", "0") == "1" else None)
         self._refresh_table = self._build_refresh_table()
         self._build_plans()
         self.refresh_weights()
@@ -292,11 +295,32 @@ class HipGoNet:
         for fn in hooks.get(self.L - 1, []):
             fn()
         for i in range(self.L - 2, -1, -1):
-            ops = self._bwd[i]
-            self._run(ops[:3], s)          # bias grads + wgrad + reduce: layer i grads final
-            for fn in hooks.get(i, []):
+            self.backward_layer(i, hooks.get(i, ()))
+        self.join_side()
+
+    def backward_layer(self, i: int, hooks=()):
+        """Layer i's backward: bias grads + wgrad + slab reduce (final grads of layer i, then
+        ``hooks``) and the dgrad into layer i-1.  The two halves only share dZ_i (read-only),
+        so with a side stream the weight-gradient chain runs beside the dgrad chain — the
+        critical path is the dgrad sequence, and each kernel's ramp/tail is filled by the
+        other stream's work.  Callers end the backward with ``join_side()``."""
+        ops = self._bwd[i]
+        main = torch.cuda.current_stream()
+        if self.side is None:
+            self._run(ops[:3], main.cuda_stream)
+            for fn in hooks:
                 fn()
-            self._run(ops[3:], s)          # dgrad into layer i-1
+        else:
+            self.side.wait_stream(main)          # dZ_i (dgrad of layer i+1 / head) ready
+            with torch.cuda.stream(self.side):
+                self._run(ops[:3], self.side.cuda_stream)
+                for fn in hooks:
+                    fn()
+        self._run(ops[3:], main.cuda_stream)
+
+    def join_side(self):
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
 
     def evaluate(self):
         s = stream_handle()
@@ -407,14 +431,13 @@ class SegmentedStep:
             segs.append((cur, fire_after[net.L - 1]))
             cur = []
         for i in range(net.L - 2, -1, -1):
-            ops = net._bwd[i]
-            emit(lambda ops=ops: net._run(ops[:3], stream_handle()))
+            emit(lambda i=i: net.backward_layer(i))
             if i in fire_after:
+                emit(net.join_side)           # bucket grads final on the main stream
                 segs.append((cur, fire_after[i]))
                 cur = []
-            if len(ops) > 3:
-                emit(lambda ops=ops: net._run(ops[3:], stream_handle()))
         if cur:
+            emit(net.join_side)
             segs.append((cur, []))
         self.segments = segs
         self.use_graphs = use_graphs

@@ -76,6 +76,39 @@ def test_graph_replay_matches_eager():
     assert abs(net.lr.item() - lr_eager) < 1e-15
 
 
+@pytest.mark.parametrize("layers,ch,B", [(4, 128, 6)])
+def test_side_stream_backward_matches_single_stream(layers, ch, B, monkeypatch):
+    """The weight-gradient chain on a side stream (HipGoNet.backward_layer) must give the
+    same gradients as the single-stream order, eager and inside a segmented graph with a
+    DP-style bucket boundary."""
+    from deep_go_amd.models.hip_model import SegmentedStep
+    monkeypatch.setenv("DG_SIDE_STREAM", "0")
+    _, net0, _ = _setup(layers, ch, B)
+    net0.forward_backward()
+    torch.cuda.synchronize()
+    g0 = net0.grads.clone()
+    monkeypatch.setenv("DG_SIDE_STREAM", "1")
+    _, net1, _ = _setup(layers, ch, B)
+    assert net1.side is not None
+    net1.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(net1.grads, g0, rtol=1e-5, atol=1e-7)
+
+    class _Buckets:  # fake bucketer: two buckets, no communication
+        buckets = [(0, 0, 2), (0, 0, 0)]
+
+        def fire(self, b):
+            pass
+
+        def wait(self):
+            pass
+    step = SegmentedStep(net1, _Buckets(), use_graphs=True)
+    assert len(step.graphs) >= 2
+    step.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(net1.grads, g0, rtol=1e-5, atol=1e-7)
+
+
 def test_loss_decreases():
     # head_relu=False: with the reference's head ReLU a large LR kills every logit (the
     # loss then pins at ln(361) exactly, see test_head_relu_dead_logits_quirk)
