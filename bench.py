@@ -64,16 +64,14 @@ def main():
 
     # synthetic data pool on device (different per rank)
     planes, player, rank, labels = random_planes(B * args.pool, seed=1000 + info.rank)
-    pool = {
-        "planes": torch.from_numpy(planes).to(dev).view(args.pool, B, 9, 361),
-        "player": torch.from_numpy(player).to(dev).view(args.pool, B),
-        "rank": torch.from_numpy(rank).to(dev).view(args.pool, B),
-        "labels": torch.from_numpy(labels).to(dev).view(args.pool, B),
-    }
+    # packed [planes | player | rank | labels] batches: one device copy per step
+    from deep_go_amd.models.hip_model import pack_batch
+    pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
+                                   rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
+                        for j in range(args.pool)]).to(dev)
 
     def load(i):
-        j = i % args.pool
-        net.set_batch(pool["planes"][j], pool["player"][j], pool["rank"][j], pool["labels"][j])
+        net.set_batch_packed(pool[i % args.pool])
 
     bucketer = None
     if world > 1:

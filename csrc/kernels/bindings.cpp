@@ -52,7 +52,8 @@ hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const doubl
                       float decay, float gscale, const float* gate, hipStream_t s);
 hipError_t dg_finite_gate(const float* loss, int n, float* gate, int* bad_count, hipStream_t s);
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
-hipError_t dg_weight_refresh(const long long* table, int n, hipStream_t s);
+hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
+                             long long* step, hipStream_t s);
 }
 
 namespace {
@@ -163,7 +164,14 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_lr_decay(P<double>(lr), decay, P<long long>(step), S(stream)), "lr_decay");
   });
   m.def("weight_refresh", [](uintptr_t table, int n, uintptr_t stream) {
-    check(dg_weight_refresh(P<long long>(table), n, S(stream)), "weight_refresh");
+    check(dg_weight_refresh(P<long long>(table), n, nullptr, 0.0, nullptr, S(stream)),
+          "weight_refresh");
+  });
+  m.def("weight_refresh_decay", [](uintptr_t table, int n, uintptr_t lr, double decay,
+                                   uintptr_t step, uintptr_t stream) {
+    check(dg_weight_refresh(P<long long>(table), n, P<double>(lr), decay, P<long long>(step),
+                            S(stream)),
+          "weight_refresh_decay");
   });
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");

@@ -143,10 +143,13 @@ class HipGoNet:
                                  device=dev)
 
         # ---- step I/O ----
-        self.planes = torch.zeros((B, 9, NUM_POINTS), dtype=torch.uint8, device=dev)
-        self.player = torch.ones(B, dtype=torch.uint8, device=dev)
-        self.rank = torch.ones(B, dtype=torch.uint8, device=dev)
-        self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
+        # one packed uint8 input buffer (planes | player | rank | labels as int32), so a step's
+        # batch lands with ONE copy (set_batch_packed / pack_batch); the named views are what
+        # the kernels read
+        self.inbuf = torch.zeros(packed_batch_bytes(B), dtype=torch.uint8, device=dev)
+        self.planes, self.player, self.rank, self.labels = unpack_views(self.inbuf, B)
+        self.player.fill_(1)
+        self.rank.fill_(1)
         self.loss = torch.zeros(B, dtype=torch.float32, device=dev)
         self.pred = torch.zeros(B, dtype=torch.int32, device=dev)
         # evaluation writes its own outputs so it never clobbers the training step's loss
@@ -273,6 +276,10 @@ class HipGoNet:
         self.rank.copy_(rank, non_blocking=non_blocking)
         self.labels.copy_(labels, non_blocking=non_blocking)
 
+    def set_batch_packed(self, packed: torch.Tensor, non_blocking: bool = True):
+        """One copy of a ``pack_batch`` buffer (device or pinned host) into the inputs."""
+        self.inbuf.copy_(packed, non_blocking=non_blocking)
+
     def forward(self):
         s = stream_handle()
         self._run(self._pre, s)
@@ -344,9 +351,10 @@ class HipGoNet:
         else:
             self.h.sgd(self.params.data_ptr(), self.grads.data_ptr(), n, self.lr.data_ptr(),
                        grad_scale, gate, s)
-        self.h.lr_decay(self.lr.data_ptr(), float(self.cfg.rateDecay),
-                        self.step_count.data_ptr(), s)
-        self.refresh_weights()
+        # bf16 operand copies of the updated weights + lr *= (1 - rateDecay), one launch
+        self.h.weight_refresh_decay(self._refresh_table.ctypes.data, len(self._refresh_table),
+                                    self.lr.data_ptr(), float(self.cfg.rateDecay),
+                                    self.step_count.data_ptr(), s)
 
     def refresh_weights(self):
         self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table),
@@ -374,6 +382,40 @@ class HipGoNet:
         ts = [self.params, self.grads, self.slab, self.x0, *self.act, *self.dz, *self.wf,
               *[w for w in self.wd if w is not None]]
         return sum(t.numel() * t.element_size() for t in ts)
+
+
+def packed_batch_bytes(B: int) -> int:
+    n = B * 9 * NUM_POINTS + 2 * B
+    return n + (-n % 4) + 4 * B
+
+
+def unpack_views(buf: torch.Tensor, B: int):
+    """(planes [B,9,361] u8, player [B] u8, rank [B] u8, labels [B] i32) views of a packed
+    batch buffer (labels 4-byte aligned)."""
+    n = B * 9 * NUM_POINTS
+    planes = buf[:n].view(B, 9, NUM_POINTS)
+    player = buf[n:n + B]
+    rank = buf[n + B:n + 2 * B]
+    lo = n + 2 * B
+    lo += -lo % 4
+    labels = buf[lo:lo + 4 * B].view(torch.int32)
+    return planes, player, rank, labels
+
+
+def pack_batch(planes, player, rank, labels, device=None) -> torch.Tensor:
+    """Pack one batch (numpy arrays or tensors) into the HipGoNet input layout."""
+    def t(x, dt):
+        x = torch.as_tensor(x)
+        return x.to(dt)
+    planes = t(planes, torch.uint8)
+    B = planes.shape[0]
+    buf = torch.zeros(packed_batch_bytes(B), dtype=torch.uint8, device=device or planes.device)
+    p, pl, rk, lb = unpack_views(buf, B)
+    p.copy_(planes.reshape(B, 9, NUM_POINTS))
+    pl.copy_(t(player, torch.uint8))
+    rk.copy_(t(rank, torch.uint8))
+    lb.copy_(t(labels, torch.int32))
+    return buf
 
 
 class GraphedStep:

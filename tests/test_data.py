@@ -93,3 +93,16 @@ def test_packed_save_load(tmp_path, train_index):
     q = PackedDataset.load(p)
     assert np.array_equal(pk.planes, q.planes) and np.array_equal(pk.label, q.label)
     assert np.array_equal(pk.game_count, q.game_count)
+
+
+@pytest.mark.parametrize("B", [1, 5, 8])
+def test_pack_batch_roundtrip(B):
+    """HipGoNet's single-copy input layout (planes | player | rank | int32 labels)."""
+    from deep_go_amd.data.synthetic import random_planes
+    from deep_go_amd.models.hip_model import pack_batch, packed_batch_bytes, unpack_views
+    pl, py, rk, lb = random_planes(B, seed=2)
+    buf = pack_batch(pl, py, rk, lb)
+    assert buf.numel() == packed_batch_bytes(B)
+    a, b, c, d = unpack_views(buf, B)
+    assert (a.numpy() == pl.reshape(B, 9, 361)).all() and (b.numpy() == py).all()
+    assert (c.numpy() == rk).all() and (d.numpy() == lb).all()

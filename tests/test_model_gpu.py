@@ -109,6 +109,20 @@ def test_side_stream_backward_matches_single_stream(layers, ch, B, monkeypatch):
     assert torch.allclose(net1.grads, g0, rtol=1e-5, atol=1e-7)
 
 
+def test_lr_decay_fused_into_weight_refresh():
+    """lr_t = lr0 * (1 - decay)^t (optimizer.lua:25-26), applied by the refresh launch."""
+    cfg, net, data = _setup(3, 64, 4, rateDecay=1e-3)
+    for _ in range(3):
+        net.train_step()
+    torch.cuda.synchronize()
+    assert abs(net.lr.item() - cfg.rate * (1 - 1e-3) ** 3) < 1e-15
+    assert int(net.step_count.item()) == 3
+    # refresh_weights() alone (init / load) must not decay
+    net.refresh_weights()
+    torch.cuda.synchronize()
+    assert abs(net.lr.item() - cfg.rate * (1 - 1e-3) ** 3) < 1e-15
+
+
 def test_loss_decreases():
     # head_relu=False: with the reference's head ReLU a large LR kills every logit (the
     # loss then pins at ln(361) exactly, see test_head_relu_dead_logits_quirk)
