@@ -26,6 +26,8 @@ void dg_conv_board_set_ablate(int mode);
 void dg_conv_wgrad_set_ablate(int mode);
 void dg_conv_wgrad3_set_ablate(int mode);
 int dg_wgrad3_tiles(int Mpad, int x_C);
+int dg_wgrad3_wgs_per_cu(int x_C);
+void dg_wgrad3_set_variant(int v);
 hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad, const void* X, int x_pad,
                           int x_C, int B, int KP, int splits, float* slab, hipStream_t stream);
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
@@ -109,6 +111,9 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_wgrad3");
   });
   m.def("wgrad3_tiles", [](int Mpad, int x_C) { return dg_wgrad3_tiles(Mpad, x_C); });
+  m.def("wgrad3_wgs_per_cu", [](int x_C) { return dg_wgrad3_wgs_per_cu(x_C); });
+  m.def("wgrad3_set_variant", [](int v) { dg_wgrad3_set_variant(v); },
+        "0: 128-ch chunks / 8 waves; 1: 64-ch / 4 waves (2 WGs per CU); 2: 64-ch / 8 waves");
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
                            uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {

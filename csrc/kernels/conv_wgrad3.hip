@@ -26,6 +26,8 @@
 //
 // Reference op: nn.SpatialConvolutionMM accGradParameters (SURVEY.md N4;
 // /root/reference/experiments.lua:138).
+#include <stdlib.h>
+
 #include "dg_common.h"
 
 using namespace dg;
@@ -36,6 +38,22 @@ constexpr int PSTEP = 64;
 constexpr int NSUB = (NPTS + PSTEP - 1) / PSTEP;  // 6
 
 DG_DEV int div19(int p) { return (p * 3450) >> 16; }  // exact for 0 <= p < 400
+
+// LDS-DMA issued from inline asm: the compiler's waitcnt pass does not see it, so it
+// neither waits for it in front of later LDS reads nor before barriers.  The kernel
+// accounts for it by hand: every wave issues exactly DMA_PER_STEP per K-step and waits
+// with s_waitcnt vmcnt(DMA_PER_STEP) — the newest stage stays in flight.
+DG_DEV void dma16(const void* gsrc, uint32_t lds_wave_base) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :
+               : "s"(lds_wave_base), "v"(gsrc)
+               : "memory", "m0");
+}
+template <int N>
+DG_DEV void wait_vmcnt() {
+  static_assert(N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
 
 struct W3Args {
   const char* dZ;  // gradient frame [B][Fz][Fz][M] bf16
@@ -57,27 +75,36 @@ constexpr int RS_A = 288;                         // dZ rows: 128 co = 256 B + p
 constexpr int A_BYTES = PSTEP * RS_A;             // 18 KiB = 18 DMA instructions
 template <int CK> struct XGeo {
   static constexpr int RS = CK * 2 + 32;          // stripe row stride
-  static constexpr int BYTES = 24 * 1024;         // >= 84 rows * 288 (F <= 23)
+  static constexpr int BYTES = CK == 128 ? 24 * 1024 : 14 * 1024;  // >= 84 rows (F <= 23)
 };
 
-template <int CK>
-__global__ void __launch_bounds__(512)
+// NW waves per workgroup: 8 (one workgroup per CU, 3-stage ring) or 4 (two independent
+// workgroups per CU — one's reads / barrier / slab store run under the other's MFMAs —
+// with a 2-stage ring in 64 KB of LDS).
+template <int CK, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1)
 conv_wgrad3_kernel(W3Args a) {
+  constexpr int NSTAGE = NW == 8 ? 3 : 2;
+  constexpr int LOOK = NSTAGE - 1;           // stages in flight ahead of the one read
+  constexpr int WN = NW / 2;
   constexpr int RS_X = XGeo<CK>::RS;
   constexpr int X_BYTES = XGeo<CK>::BYTES;
   constexpr int STAGE = A_BYTES + X_BYTES;
   constexpr int NKT = 3 * CK;                // k width of the tile
-  constexpr int WK = NKT / 4;                // k per wave
-  constexpr int NF = WK / 16;                // 6 (CK 128) or 3 (CK 64)
+  constexpr int WK = NKT / WN;               // k per wave
+  constexpr int NF = WK / 16;                // 6 (CK 128 / NW 8, CK 64 / NW 4) or 3
   constexpr int MF = 4;
   constexpr int A_INSTR = A_BYTES / 1024;    // 18
   constexpr int X_INSTR_MAX = X_BYTES / 1024;
+  constexpr int A_PW = (A_INSTR + NW - 1) / NW;      // dZ DMA instructions per wave
+  constexpr int X_PW = (X_INSTR_MAX + NW - 1) / NW;  // stripe DMA instructions per wave
+  constexpr int DMA_PER_STEP = A_PW + X_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware remap (cdna guide T1): consecutive logical ids (the tiles of one split, which
   // share every dZ row and most X rows) land on one XCD and hit its L2.
@@ -123,50 +150,66 @@ conv_wgrad3_kernel(W3Args a) {
   // DMA lane geometry (loop invariant): instruction j of a stage covers LDS bytes
   // [j*1024, j*1024+1024); lane -> (row, col) of the padded image.  Pad lanes re-read
   // column 0 of their row (any valid address).
-  int a_row[3], a_col[3], x_row[3], x_col[3];
+  int a_row[A_PW], a_col[A_PW], x_row[X_PW], x_col[X_PW];
 #pragma unroll
-  for (int m = 0; m < 3; ++m) {
-    const int d = (wave + 8 * m) * 1024 + lane * 16;
+  for (int m = 0; m < A_PW; ++m) {
+    const int d = (wave + NW * m) * 1024 + lane * 16;
     a_row[m] = d / RS_A;
     const int ca = d - a_row[m] * RS_A;
     a_col[m] = ca < 256 ? ca : 0;
+  }
+#pragma unroll
+  for (int m = 0; m < X_PW; ++m) {
+    const int d = (wave + NW * m) * 1024 + lane * 16;
     x_row[m] = d / RS_X;
     const int cx = d - x_row[m] * RS_X;
     x_col[m] = cx < CK * 2 ? cx : 0;
   }
 
   const bool no_dma = a.ablate & 4;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
+  // Exactly A_PW dZ + X_PW X instructions per wave and step (DMA_PER_STEP): instructions past
+  // the real count repeat one of the step's real ones (same source, same destination,
+  // identical bytes), so vmcnt arithmetic is static.
   auto stage = [&](int buf, const Geo& g) {
     if (no_dma) return;
-    char* sA = smem + buf * STAGE;
-    char* sX = sA + A_BYTES;
+    const uint32_t sA = lds0 + buf * STAGE;
+    const uint32_t sX = sA + A_BYTES;
     const char* zb = a.dZ + (size_t)g.b * Fz * Fz * zrow;
 #pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int j = wave + 8 * m;
-      if (j < A_INSTR) {
-        const int r = a_row[m];
-        const char* src;
-        if (r < g.pc) {
-          const int p = g.p0 + r;
-          const int h = div19(p), w = p - 19 * h;
-          src = zb + ((h + a.dz_pad) * Fz + w + a.dz_pad) * zrow + mt * 256 + a_col[m];
-        } else {
-          src = zb + (a_col[m] & 255);  // zero border row 0 of the frame
-        }
-        glds16(src, (LDS_AS void*)(sA + j * 1024));
+    for (int m = 0; m < A_PW; ++m) {
+      // (no runtime-indexed register arrays here: they would go to scratch, and a scratch
+      // load's vmcnt wait would also wait for the in-flight DMA)
+      const bool real = wave + NW * m < A_INSTR;  // past the 18 pieces: repeat piece m = 0
+      const int j = real ? wave + NW * m : wave;
+      const int r = real ? a_row[m] : a_row[0];
+      const int acol = real ? a_col[m] : a_col[0];
+      const char* src;
+      if (r < g.pc) {
+        const int p = g.p0 + r;
+        const int h = div19(p), w = p - 19 * h;
+        src = zb + ((h + a.dz_pad) * Fz + w + a.dz_pad) * zrow + mt * 256 + acol;
+      } else {
+        src = zb + (acol & 255);  // zero border row 0 of the frame
       }
+      dma16(src, __builtin_amdgcn_readfirstlane(sA + j * 1024));
     }
-    const int ninstr = (g.nr * RS_X + 1023) / 1024;
+    const int ninstr = min((g.nr * RS_X + 1023) / 1024, X_INSTR_MAX);
     const char* xb = a.X + (size_t)g.b * FF * xrow + cc * (CK * 2);
 #pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int j = wave + 8 * m;
-      if (j < ninstr && j < X_INSTR_MAX) {
-        int fr = g.fr0 + x_row[m];
-        fr = fr < FF ? fr : FF - 1;
-        glds16(xb + (size_t)fr * xrow + x_col[m], (LDS_AS void*)(sX + j * 1024));
+    for (int m = 0; m < X_PW; ++m) {
+      int j = wave + NW * m;
+      int rr = x_row[m], col = x_col[m];
+      if (j >= ninstr) {  // repeat a real instruction of this step (identical bytes)
+        j = wave % ninstr;
+        const int d = j * 1024 + lane * 16;
+        rr = d / RS_X;
+        col = d - rr * RS_X;
+        col = col < CK * 2 ? col : 0;
       }
+      int fr = g.fr0 + rr;
+      fr = fr < FF ? fr : FF - 1;
+      dma16(xb + (size_t)fr * xrow + col, __builtin_amdgcn_readfirstlane(sX + j * 1024));
     }
   };
 
@@ -187,15 +230,17 @@ conv_wgrad3_kernel(W3Args a) {
   const int lane_col = (pp >> 1) * 16 + (pp & 1) * 8;
   const int a_base = prow0 * RS_A + wm * 128 + lane_col;
 
+  const int nst = st_end - st_begin;
   Geo cur = geo(st_begin);
-  if (st_begin < st_end) {
-    stage(0, cur);
-    __syncthreads();
-  }
+  if (nst > 0) stage(0, cur);
+  if (LOOK == 2 && nst > 1) stage(1, geo(st_begin + 1));
+  if (LOOK == 2 && nst > 1) wait_vmcnt<DMA_PER_STEP>(); else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
   for (int st = st_begin; st < st_end; ++st) {
-    const int buf = (st - st_begin) & 1;
-    Geo nxt = cur;
-    if (st + 1 < st_end) nxt = geo(st + 1);
+    const int ls = st - st_begin;
+    const int buf = ls % NSTAGE;
+    const bool more = ls + LOOK < nst;
+    if (more) stage((ls + LOOK) % NSTAGE, geo(st + LOOK));  // into the stage read at ls - 1
     const LDS_AS char* sA = (const LDS_AS char*)(smem + buf * STAGE) + a_base;
     const LDS_AS char* sX = (const LDS_AS char*)(smem + buf * STAGE + A_BYTES) + lane_col;
     // stripe row of each pixel row this lane reads: rel = frame(p) - frame(p0)
@@ -237,11 +282,6 @@ conv_wgrad3_kernel(W3Args a) {
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    // Next step's DMA goes out AFTER this step's fragment reads: the compiler cannot tell
-    // the tr-reads from the DMA destination apart and would otherwise put a vmcnt(0) in
-    // front of the reads, i.e. wait for the prefetch it was meant to hide.
-    if (st + 1 < st_end) stage(buf ^ 1, nxt);
-    __builtin_amdgcn_sched_barrier(0);
     if (a.ablate & 1) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -275,8 +315,11 @@ conv_wgrad3_kernel(W3Args a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // DMA wait + barrier stay below the MFMAs
-    __syncthreads();
-    cur = nxt;
+    // stage ls+1 must have landed (every wave's part) before anyone reads it; stage ls+2
+    // (issued this step) stays in flight
+    if (LOOK == 2 && more) wait_vmcnt<DMA_PER_STEP>(); else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (ls + 1 < nst) cur = geo(st + 1);
   }
 
   if (a.ablate & 8) {
@@ -304,17 +347,30 @@ conv_wgrad3_kernel(W3Args a) {
   }
 }
 
-template <int CK>
+template <int CK, int NW>
 hipError_t launch3(const W3Args& a, hipStream_t s) {
-  constexpr size_t lds = 2 * (size_t)(A_BYTES + XGeo<CK>::BYTES);
+  constexpr size_t lds = (NW == 8 ? 3 : 2) * (size_t)(A_BYTES + XGeo<CK>::BYTES);
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad3_kernel<CK>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad3_kernel<CK, NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL(conv_wgrad3_kernel<CK>, dim3(a.splits * a.tiles), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((conv_wgrad3_kernel<CK, NW>), dim3(a.splits * a.tiles), dim3(NW * 64), lds,
+                     s, a);
   return hipGetLastError();
+}
+
+// variant: 0 = CK 128 / 8 waves (x_C % 128 == 0), 1 = CK 64 / 4 waves, 2 = CK 64 / 8 waves
+int g_variant = -1;
+int variant_for(int x_C) {
+  int& v = g_variant;
+  if (v < 0) {
+    const char* e = getenv("DG_WGRAD3_VARIANT");
+    v = e ? atoi(e) : 1;
+  }
+  if (v == 0 && x_C % 128 != 0) return 2;
+  return v;
 }
 
 }  // namespace
@@ -324,9 +380,12 @@ extern "C" void dg_conv_wgrad3_set_ablate(int m) { g_wgrad3_ablate = m; }
 
 // Tiles per split for a layer (host helper shared with the Python split picker).
 extern "C" int dg_wgrad3_tiles(int Mpad, int x_C) {
-  const int ck = x_C % 128 == 0 ? 128 : 64;
+  const int ck = variant_for(x_C) == 0 ? 128 : 64;
   return (Mpad / 128) * 3 * (x_C / ck);
 }
+// workgroups that fit on one CU (LDS / registers): splits = num_cus * this / tiles
+extern "C" void dg_wgrad3_set_variant(int v) { g_variant = v; }
+extern "C" int dg_wgrad3_wgs_per_cu(int x_C) { return variant_for(x_C) == 1 ? 2 : 1; }
 
 extern "C" hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                                      int x_pad, int x_C, int B, int KP, int splits, float* slab,
@@ -350,5 +409,9 @@ extern "C" hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad
   a.tiles = dg_wgrad3_tiles(Mpad, x_C);
   a.ablate = g_wgrad3_ablate;
   if (splits != a.splits) return hipErrorInvalidValue;  // caller sized the slab for `splits`
-  return x_C % 128 == 0 ? launch3<128>(a, stream) : launch3<64>(a, stream);
+  switch (variant_for(x_C)) {
+    case 0: return launch3<128, 8>(a, stream);
+    case 1: return launch3<64, 4>(a, stream);
+    default: return launch3<64, 8>(a, stream);
+  }
 }

@@ -106,9 +106,10 @@ class HipGoNet:
                 bm = LY.board_bm(spec.cout)
             KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
             Mpad_w = LY.round_up(spec.cout, 128)
-            w3 = LY.wgrad3_ok(spec.k, cinp, spec.pad) and os.environ.get("DG_WGRAD3", "1") != "0"
+            w3 = LY.wgrad3_ok(spec.k, cinp, spec.pad) and os.environ.get("DG_WGRAD3", "0") == "1"
             if w3:
-                splits = LY.pick_wgrad3_splits(batch, Mpad_w, cinp, num_cus)
+                splits = LY.pick_wgrad3_splits(batch, self.h.wgrad3_tiles(Mpad_w, cinp),
+                                                self.h.wgrad3_wgs_per_cu(cinp), num_cus)
             else:
                 splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,

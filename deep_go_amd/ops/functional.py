@@ -118,7 +118,8 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     Mpad = LY.round_up(cout, 128)
     w3 = algo == "rows" or (algo == "auto" and LY.wgrad3_ok(k, cinp, pad))
     if w3:
-        splits = splits or LY.pick_wgrad3_splits(B, Mpad, cinp)
+        splits = splits or LY.pick_wgrad3_splits(B, h.wgrad3_tiles(Mpad, cinp),
+                                                  h.wgrad3_wgs_per_cu(cinp))
     else:
         splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad)
     dzf = LY.to_frame(dz, max(1, pad))

@@ -110,16 +110,11 @@ def wgrad3_ok(k: int, cin_frame: int, pad: int) -> bool:
     return k == 3 and cin_frame % 64 == 0 and 1 <= pad <= 2
 
 
-def wgrad3_tiles(Mpad: int, cin_frame: int) -> int:
-    ck = 128 if cin_frame % 128 == 0 else 64
-    return (Mpad // 128) * 3 * (cin_frame // ck)
-
-
-def pick_wgrad3_splits(batch: int, Mpad: int, cin_frame: int, num_cus: int = 256) -> int:
-    """One workgroup per CU: splits x tiles <= num_cus (single dispatch round), and every
-    split gets at least one 64-pixel step (6 per board)."""
-    tiles = wgrad3_tiles(Mpad, cin_frame)
-    return max(1, min(num_cus // tiles, batch * 6))
+def pick_wgrad3_splits(batch: int, tiles: int, wgs_per_cu: int = 1, num_cus: int = 256) -> int:
+    """One dispatch round: splits x tiles <= num_cus x workgroups-per-CU, and every split
+    gets at least one 64-pixel step (6 per board).  ``tiles``/``wgs_per_cu`` come from the
+    kernel (hip().wgrad3_tiles / wgrad3_wgs_per_cu: they depend on the kernel variant)."""
+    return max(1, min(num_cus * wgs_per_cu // tiles, batch * 6))
 
 
 def board_ok(k: int, cin_frame: int) -> bool:

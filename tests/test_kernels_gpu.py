@@ -126,16 +126,25 @@ def test_conv_wgrad(B, cin, cout, k, splits):
     (3, 128, 128, None, "rows"), (3, 128, 128, None, "im2col"), (9, 128, 128, 5, "rows"),
     (2, 64, 128, 1, "rows"), (4, 192, 64, None, "rows"), (2, 256, 256, 3, "rows"),
     (1, 128, 128, 6, "rows")])
-def test_conv_wgrad_algos(B, cin, cout, splits, algo):
-    """Row-stripe 3x3 wgrad (conv_wgrad3.hip) vs the im2col kernel vs the fp32 reference."""
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
+    """Row-stripe 3x3 wgrad (conv_wgrad3.hip, each variant) vs the im2col kernel vs the fp32
+    reference."""
+    if algo != "rows" and variant != 1:
+        pytest.skip("variant only applies to the row-stripe kernel")
     torch.manual_seed(5)
     from deep_go_amd.ops import functional as Fn
-    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
-    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo=algo)
-    w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
-    (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
-    assert rel_err(got, gw) < 1e-3
+    from deep_go_amd.ops.native import hip
+    hip().wgrad3_set_variant(variant)
+    try:
+        x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+        dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+        got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo=algo)
+        w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
+        (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
+        assert rel_err(got, gw) < 1e-3
+    finally:
+        hip().wgrad3_set_variant(1)
 
 
 @pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True), (2, 32, 1, False),

@@ -95,18 +95,21 @@ def main():
                 h.wgrad_reduce(slab3.data_ptr() if sp != splits else slab.data_ptr(),
                                gw.data_ptr(), sp, C, 128, KPw, 9, C, C, 0, 0, 0, 0, s)
             return f
-        # row-stripe wgrad (conv_wgrad3.hip)
-        sp3 = LY.pick_wgrad3_splits(B, 128, C)
-        slab3 = torch.empty(sp3 * 128 * KPw, device=dev)
+        # row-stripe wgrad (conv_wgrad3.hip), each kernel variant
+        for var in (0, 1, 2):
+            h.wgrad3_set_variant(var)
+            sp3 = LY.pick_wgrad3_splits(B, h.wgrad3_tiles(128, C), h.wgrad3_wgs_per_cu(C))
+            slab3 = torch.empty(sp3 * 128 * KPw, device=dev)
 
-        def wg3():
-            h.conv_wgrad3(dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, sp3,
-                          slab3.data_ptr(), s)
-        for mode in (0, 1, 2, 4, 8, 7, 15, 3):
-            h.conv_wgrad3_set_ablate(mode)
-            res.setdefault(f"wgrad3_ablate{mode}", []).append(round(timeit(wg3), 2))
-        h.conv_wgrad3_set_ablate(0)
-        res.setdefault("splits3", []).append(sp3)
+            def wg3():
+                h.conv_wgrad3(dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, sp3,
+                              slab3.data_ptr(), s)
+            for mode in ((0, 1, 2, 4, 8, 7, 15) if var == 1 else (0, 4)):
+                h.conv_wgrad3_set_ablate(mode)
+                res.setdefault(f"wgrad3v{var}_ablate{mode}", []).append(round(timeit(wg3), 2))
+            h.conv_wgrad3_set_ablate(0)
+            res.setdefault(f"splits3v{var}", []).append(sp3)
+        h.wgrad3_set_variant(1)
         res.setdefault("reduce_im2col_splits", []).append(round(timeit(red(splits)), 2))
         res.setdefault("reduce_rows_splits", []).append(round(timeit(red(sp3)), 2))
     out = {k: {"us": v, "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
