@@ -24,6 +24,17 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_wgrad_set_ablate(int mode);
+hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
+                             const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
+                             int y_pad, const float* bias, const float* posb, const float* s_x,
+                             const float* s_w, const float* s_y, unsigned* amax_y,
+                             hipStream_t stream);
+hipError_t dg_fp8_scales(const long long* table, int n, float* scales, unsigned* amax,
+                         float margin, hipStream_t s);
+hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
+                         const float* s_w, hipStream_t s);
+hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
+                           unsigned* amax, hipStream_t s);
 void dg_conv_wgrad3_set_ablate(int mode);
 int dg_wgrad3_tiles(int Mpad, int x_C);
 int dg_wgrad3_wgs_per_cu(int x_C);
@@ -114,6 +125,34 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("wgrad3_wgs_per_cu", [](int x_C) { return dg_wgrad3_wgs_per_cu(x_C); });
   m.def("wgrad3_set_variant", [](int v) { dg_wgrad3_set_variant(v); },
         "0: 128-ch chunks / 8 waves; 1: 64-ch / 4 waves (2 WGs per CU); 2: 64-ch / 8 waves");
+  m.def("conv_board_fp8", [](int kw, int bm, uintptr_t A8, int KP, int M, int Mpad, uintptr_t X8,
+                             int x_pad, int x_C, int B, uintptr_t Y, uintptr_t Y8, int y_pad,
+                             uintptr_t bias, uintptr_t posb, uintptr_t s_x, uintptr_t s_w,
+                             uintptr_t s_y, uintptr_t amax_y, uintptr_t stream) {
+    check(dg_conv_board_fp8(kw, bm, P<void>(A8), KP, M, Mpad, P<void>(X8), x_pad, x_C, B,
+                            P<void>(Y), P<void>(Y8), y_pad, P<float>(bias), P<float>(posb),
+                            P<float>(s_x), P<float>(s_w), P<float>(s_y), P<unsigned>(amax_y),
+                            S(stream)),
+          "conv_board_fp8");
+  });
+  m.def("fp8_scales", [](uintptr_t table, int n, uintptr_t scales, uintptr_t amax, float margin,
+                         uintptr_t stream) {
+    check(dg_fp8_scales(P<long long>(table), n, P<float>(scales), P<unsigned>(amax), margin,
+                        S(stream)),
+          "fp8_scales");
+  });
+  m.def("weight_fp8", [](uintptr_t w, uintptr_t wf8, int cout, int cin, int taps, int cinp,
+                         int kp, uintptr_t s_w, uintptr_t stream) {
+    check(dg_weight_fp8(P<float>(w), P<void>(wf8), cout, cin, taps, cinp, kp, P<float>(s_w),
+                        S(stream)),
+          "weight_fp8");
+  });
+  m.def("frame_to_fp8", [](uintptr_t src, uintptr_t dst, size_t n, uintptr_t scale,
+                           uintptr_t amax, uintptr_t stream) {
+    check(dg_frame_to_fp8(P<void>(src), P<void>(dst), n, P<float>(scale), P<unsigned>(amax),
+                          S(stream)),
+          "frame_to_fp8");
+  });
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
                            uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {

@@ -1,0 +1,374 @@
+// FP8 forward path (BASELINE config 5, "fp8 MFMA path"): the hidden 3x3 / 1x1 forward
+// convolutions run on the block-scaled MX MFMA v_mfma_scale_f32_16x16x128_f8f6f4 with
+// OCP e4m3 operands (2x the bf16 MFMA rate on gfx950), fp32 accumulation, per-tensor
+// delayed scaling (unit MX block scales).  The backward stays bf16.
+//
+//   y = relu( (s_x * s_w) * sum_k X8[p + off][c] W8[co][t][c] + bias[co] + posb[p][co] )
+//
+// Layout facts (tools/fp8_mfma_probe.hip, exact integer data): A / B rows are lane & 15,
+// the 128-deep k of one instruction is split over the 4 lane groups; any k assignment
+// works if both operands use the same one, so lane group g holds the 32 contiguous bytes
+// k = 32g .. 32g+31 — i.e. a 128-channel fp8 chunk is a 128-byte LDS row, exactly the
+// geometry of the bf16 board kernel's 64-channel rows (same XOR swizzle, same DMA).
+//
+// Outputs: the bf16 activation frame (read by the bf16 backward and the head) AND an
+// fp8 shadow frame for the next layer's forward, quantized with that layer's delayed
+// scale s_y = amax_prev / 448; the kernel folds its own output amax into amax_y (bit-wise
+// atomicMax: post-ReLU values are >= 0).  fp8_scales_kernel turns amax into scales once
+// per step.
+//
+// Reference op: nn.SpatialConvolutionMM forward + nn.Add + nn.ReLU (experiments.lua:138-147).
+#include "dg_common.h"
+
+using namespace dg;
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+namespace {
+
+constexpr int NCOL = 384;
+constexpr float FP8_MAX = 448.f;
+
+DG_DEV uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  // v_cvt_pk_fp8_f32: two floats -> two e4m3 bytes in the low / high word half
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+struct Fp8Args {
+  const uint8_t* A;    // [Mpad][KP] e4m3 weights, k = tap*x_C + ci
+  const uint8_t* X;    // fp8 input frame [B][F][F][x_C]
+  char* Y;             // bf16 output frame [B][Fy][Fy][M]
+  uint8_t* Y8;         // fp8 output frame (same geometry) or null
+  const float* bias;   // [M]
+  const float* posb;   // [361][M]
+  const float* s_x;    // input activation scale (device scalar)
+  const float* s_w;    // weight scale
+  const float* s_y;    // output fp8 scale
+  unsigned* amax_y;    // output amax (float bits)
+  int KP, M, x_pad, x_C, y_pad;
+};
+
+// One workgroup = one board x BM (64 * WM) output channels, 8 waves; see conv_board.hip
+// for the staging scheme (single halo image -> 2 workgroups per CU at BM = 64).
+template <int KW, int WM>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WM == 1 ? 4 : 2)))
+conv_board_fp8_kernel(Fp8Args a) {
+  constexpr int WN = 8 / WM;
+  constexpr int MF = 4;
+  constexpr int NF = NCOL / (16 * WN);
+  constexpr int BM = 64 * WM;
+  constexpr int R = (KW - 1) / 2;
+  constexpr int T = KW * KW;
+  constexpr int A_BYTES = BM * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int b = blockIdx.x;
+  const int m_tile = blockIdx.y * BM;
+  const int F = BOARD + 2 * a.x_pad;
+  const int FF = F * F;
+  const int HROWS = (FF + 63) / 64 * 64;
+  char* sA0 = smem;
+  char* sH = smem + 2 * A_BYTES;
+  const int nchunk = a.x_C / 128;
+  const int nsteps = nchunk * T;
+  const uint8_t* Xb = a.X + (size_t)b * FF * a.x_C;
+
+  const int g_src = (lane & 7) ^ (lane >> 3);
+  auto stage_A = [&](int buf, int step) {
+    const int c = step / T, t = step - (step / T) * T;
+    const int kcol = t * a.x_C + c * 128;
+    char* dst = sA0 + buf * A_BYTES;
+    constexpr int INSTR = BM / 64;
+#pragma unroll
+    for (int i = 0; i < INSTR; ++i) {
+      const int r = (wave * INSTR + i) * 8 + (lane >> 3);
+      glds16(a.A + (size_t)(m_tile + r) * a.KP + kcol + g_src * 16,
+             (LDS_AS void*)(dst + (wave * INSTR + i) * 1024));
+    }
+  };
+  auto stage_H = [&](int c) {
+    for (int j = wave; j < HROWS / 8; j += 8) {
+      const int r = j * 8 + (lane >> 3);
+      const int rs = r < FF ? r : FF - 1;
+      glds16(Xb + (size_t)rs * a.x_C + c * 128 + g_src * 16, (LDS_AS void*)(sH + j * 1024));
+    }
+  };
+
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  int fp[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    fp[j] = (h + a.x_pad) * F + (w + a.x_pad);
+  }
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_H(0);
+  stage_A(0, 0);
+  __syncthreads();
+  // lane group lq holds k bytes [32 lq, 32 lq + 32) = 16-B slots 2lq, 2lq+1 of the row
+  const int s0 = 2 * lq, s1 = 2 * lq + 1;
+  for (int s = 0; s < nsteps; ++s) {
+    const int c = s / T, t = s - (s / T) * T;
+    if (s + 1 < nsteps) stage_A((s + 1) & 1, s + 1);
+    const char* sA = sA0 + (s & 1) * A_BYTES;
+    const int toff = (t / KW - R) * F + (t % KW - R);
+    // 32 fragment bytes per lane = two 16-B slots of the row (XOR-swizzled like the bf16 rows)
+    auto frag = [&](const char* base, int row) {
+      const LDS_AS char* rp = (const LDS_AS char*)(base + row * 128);
+      const i32x4 lo = *(const LDS_AS i32x4*)(rp + ((s0 ^ (row & 7)) * 16));
+      const i32x4 hi = *(const LDS_AS i32x4*)(rp + ((s1 ^ (row & 7)) * 16));
+      return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    };
+    i32x8 af[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) af[i] = frag(sA, wm * 64 + i * 16 + lr);
+    // one B fragment live at a time (register budget of 2 workgroups per CU); the compiler
+    // overlaps fragment j+1's reads with fragment j's MFMAs
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const i32x8 bj = frag(sH, fp[j] + toff);
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bj, acc[i][j], 0, 0,
+                                                                      0, 127, 0, 127);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (t == T - 1 && c + 1 < nchunk) {  // single halo image: next chunk after the barrier
+      stage_H(c + 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: dequantize, bias + pos-bias + ReLU -> bf16 tile in LDS -> bf16 + fp8 ----
+  constexpr int NCH = BM / 8;
+  constexpr int CMASK = NCH - 1;
+  constexpr int ROWB = BM * 2;
+  const float deq = *a.s_x * *a.s_w;
+  const float inv_y = a.Y8 ? 1.f / *a.s_y : 0.f;
+  f32x4 bb[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int co = m_tile + wm * 64 + i * 16 + lq * 4;
+    bb[i] = *(const f32x4*)(a.bias + (co < a.M ? co : 0));
+  }
+  char* sT = smem;
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) continue;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int col = wm * 64 + i * 16 + lq * 4;
+      const int co = m_tile + col;
+      const f32x4 pb = *(const f32x4*)(a.posb + p * a.M + (co < a.M ? co : 0));
+      f32x4 v = acc[i][j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = fmaxf(v[r] * deq + bb[i][r] + pb[r], 0.f);
+        vmax = fmaxf(vmax, co + r < a.M ? v[r] : 0.f);
+      }
+      uint2 o;
+      o.x = pack_bf16x2(v[0], v[1]);
+      o.y = pack_bf16x2(v[2], v[3]);
+      const int chunk = (col >> 3) ^ (p & CMASK);
+      *(uint2*)(sT + p * ROWB + chunk * 16 + (col & 4) * 2) = o;
+    }
+  }
+  vmax = wave_max(vmax);
+  if (lane == 0 && a.amax_y) atomicMax(a.amax_y, __float_as_uint(vmax));
+  __syncthreads();
+  const int Fy = BOARD + 2 * a.y_pad;
+  char* Yb = a.Y + (size_t)b * Fy * Fy * a.M * 2;
+  uint8_t* Y8b = a.Y8 ? a.Y8 + (size_t)b * Fy * Fy * a.M : nullptr;
+  for (int idx = tid; idx < NPTS * NCH; idx += 512) {
+    const int p = idx / NCH, c = idx - (idx / NCH) * NCH;
+    const int co = m_tile + c * 8;
+    if (co >= a.M) continue;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    const uint4 v = *(const uint4*)(sT + p * ROWB + ((c ^ (p & CMASK)) * 16));
+    const size_t pix = (size_t)((h + a.y_pad) * Fy + (w + a.y_pad)) * a.M + co;
+    *(uint4*)(Yb + pix * 2) = v;
+    if (Y8b) {
+      auto q = [&](uint32_t u, int hi) {
+        const float f = __uint_as_float(hi ? (u & 0xFFFF0000u) : (u << 16));
+        return fminf(f * inv_y, FP8_MAX);
+      };
+      uint2 o8;
+      o8.x = pack_fp8x4(q(v.x, 0), q(v.x, 1), q(v.y, 0), q(v.y, 1));
+      o8.y = pack_fp8x4(q(v.z, 0), q(v.z, 1), q(v.w, 0), q(v.w, 1));
+      *(uint2*)(Y8b + pix) = o8;
+    }
+  }
+}
+
+// Per step, one block per layer: weight amax -> s_w; observed activation amax -> s_y (for
+// the next step's quantization; delayed scaling), amax reset.  scales[l] = {s_w, s_y} and
+// amax[l] (float bits).  A floor keeps all-zero tensors finite.
+struct ScaleLayer {
+  const float* w;
+  long long n;
+};
+constexpr int MAX_SCALE_LAYERS = 48;
+struct ScaleArgs {
+  int n;
+  ScaleLayer L[MAX_SCALE_LAYERS];
+};
+
+__global__ void __launch_bounds__(256)
+fp8_scales_kernel(ScaleArgs a, float* scales, unsigned* amax, float margin) {
+  const int l = blockIdx.x;
+  const ScaleLayer L = a.L[l];
+  float m = 0.f;
+  for (long long i = threadIdx.x; i < L.n; i += 256) m = fmaxf(m, fabsf(L.w[i]));
+  m = wave_max(m);
+  __shared__ float s_m[4];
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float mw = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    scales[2 * l] = fmaxf(mw, 1e-12f) / FP8_MAX;
+    const float my = __uint_as_float(amax[l]);
+    if (my > 0.f) scales[2 * l + 1] = my * margin / FP8_MAX;
+    amax[l] = 0u;
+  }
+}
+
+// fp32 OHWI master -> e4m3 operand layout Wf8[co][t * cinp + ci] (quantized with s_w).
+__global__ void __launch_bounds__(256)
+weight_fp8_kernel(const float* w, uint8_t* wf8, int cout, int cin, int taps, int cinp, int kp,
+                  const float* s_w) {
+  const float inv = 1.f / *s_w;
+  const int total = cout * taps * cin;
+  for (int idx = (blockIdx.x * 256 + threadIdx.x) * 4; idx < total; idx += gridDim.x * 1024) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = idx + e;
+      if (k >= total) break;
+      const int co = k / (taps * cin);
+      const int rem = k - co * taps * cin;
+      const int t = rem / cin, ci = rem - t * cin;
+      const float v = fmaxf(fminf(w[k] * inv, FP8_MAX), -FP8_MAX);
+      const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false);
+      wf8[(size_t)co * kp + t * cinp + ci] = (uint8_t)(pk & 0xFF);
+    }
+  }
+}
+
+// bf16 frame -> fp8 frame (whole frame incl. zero border), scale s.  Used to seed the
+// fp8 shadow of a layer whose producer writes bf16 only.
+__global__ void __launch_bounds__(256)
+frame_to_fp8_kernel(const bf16_t* src, uint8_t* dst, size_t n, const float* s,
+                    unsigned* amax) {
+  const float inv = 1.f / *s;
+  float m = 0.f;
+  for (size_t i = (blockIdx.x * 256ull + threadIdx.x) * 4; i < n; i += gridDim.x * 1024ull) {
+    const uint2 u = *(const uint2*)(src + i);
+    const float f0 = __uint_as_float(u.x << 16), f1 = __uint_as_float(u.x & 0xFFFF0000u);
+    const float f2 = __uint_as_float(u.y << 16), f3 = __uint_as_float(u.y & 0xFFFF0000u);
+    m = fmaxf(m, fmaxf(fmaxf(f0, f1), fmaxf(f2, f3)));
+    *(uint32_t*)(dst + i) = pack_fp8x4(fminf(f0 * inv, FP8_MAX), fminf(f1 * inv, FP8_MAX),
+                                       fminf(f2 * inv, FP8_MAX), fminf(f3 * inv, FP8_MAX));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && amax) atomicMax(amax, __float_as_uint(m));
+}
+
+template <typename K>
+void allow_lds(K kernel, size_t bytes) {
+  static size_t done = 0;
+  if (bytes > done) {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = bytes;
+  }
+}
+
+template <int KW, int WM>
+hipError_t launch_fp8(const Fp8Args& a, int B, int Mpad, hipStream_t s) {
+  const int F = 19 + 2 * a.x_pad;
+  const int hrows = (F * F + 63) / 64 * 64;
+  size_t lds = 2 * (size_t)(64 * WM * 128) + (size_t)hrows * 128;
+  const size_t epi = (size_t)NPTS * 64 * WM * 2;
+  if (epi > lds) lds = epi;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  allow_lds(conv_board_fp8_kernel<KW, WM>, lds);
+  hipLaunchKernelGGL((conv_board_fp8_kernel<KW, WM>), dim3(B, Mpad / (64 * WM)), dim3(512), lds,
+                     s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
+                             const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
+                             int y_pad, const float* bias, const float* posb, const float* s_x,
+                             const float* s_w, const float* s_y, unsigned* amax_y,
+                             hipStream_t stream) {
+  if (x_C % 128 != 0 || M % 8 != 0 || (bm != 64 && bm != 128) || Mpad % bm != 0 || B <= 0)
+    return hipErrorInvalidValue;
+  if (KP < kw * kw * x_C || KP % 16 != 0 || x_pad < (kw - 1) / 2) return hipErrorInvalidValue;
+  Fp8Args a{(const uint8_t*)A8, (const uint8_t*)X8, (char*)Y, (uint8_t*)Y8, bias, posb, s_x,
+            s_w, s_y, amax_y, KP, M, x_pad, x_C, y_pad};
+  const bool w2 = bm == 128;
+  switch (kw) {
+    case 1: return w2 ? launch_fp8<1, 2>(a, B, Mpad, stream) : launch_fp8<1, 1>(a, B, Mpad, stream);
+    case 3: return w2 ? launch_fp8<3, 2>(a, B, Mpad, stream) : launch_fp8<3, 1>(a, B, Mpad, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// table: n rows of {w ptr, numel}
+hipError_t dg_fp8_scales(const long long* table, int n, float* scales, unsigned* amax,
+                         float margin, hipStream_t s) {
+  if (n <= 0 || n > MAX_SCALE_LAYERS) return hipErrorInvalidValue;
+  ScaleArgs a;
+  a.n = n;
+  for (int i = 0; i < n; ++i) {
+    a.L[i].w = (const float*)table[2 * i];
+    a.L[i].n = table[2 * i + 1];
+  }
+  hipLaunchKernelGGL(fp8_scales_kernel, dim3(n), dim3(256), 0, s, a, scales, amax, margin);
+  return hipGetLastError();
+}
+
+hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
+                         const float* s_w, hipStream_t s) {
+  const int total = cout * taps * cin;
+  int blocks = (total / 4 + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(weight_fp8_kernel, dim3(blocks), dim3(256), 0, s, w, (uint8_t*)wf8, cout,
+                     cin, taps, cinp, kp, s_w);
+  return hipGetLastError();
+}
+
+hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
+                           unsigned* amax, hipStream_t s) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  int blocks = (int)((n / 4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(frame_to_fp8_kernel, dim3(blocks), dim3(256), 0, s, (const bf16_t*)src,
+                     (uint8_t*)dst, n, scale, amax);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -82,6 +82,45 @@ def conv_board(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: str 
     return LY.from_frame(out, 1, M)
 
 
+def conv_board_fp8(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: torch.Tensor,
+                   bm: int | None = None):
+    """FP8 forward (conv_fp8.hip): x [B,Cin,19,19] (Cin % 128 == 0), OHWI w, fp32 bias/posb.
+    Quantizes x / w with per-tensor scales (amax / 448) through the same device kernels the
+    model uses; returns (y bf16-frame interior as fp32 NCHW, y8 dequantized, s_y, amax_y)."""
+    h = hip()
+    dev = w.device
+    B = x.shape[0]
+    cout, k, _, cin = w.shape
+    pad = (k - 1) // 2
+    bm = bm or LY.board_bm(cout)
+    KP, _, Mpad = LY.conv_dims(k, cin, cout, bm)
+    s = stream_handle()
+    wflat = w.float().contiguous().to(dev)
+    # scales[0] = s_w, scales[1] = (unused) ; s_x / s_y separate device scalars
+    scales = torch.ones(2, device=dev)
+    amax = torch.zeros(1, dtype=torch.int32, device=dev)
+    import numpy as np
+    tbl = np.array([[wflat.data_ptr(), wflat.numel()]], dtype=np.int64)
+    h.fp8_scales(tbl.ctypes.data, 1, scales.data_ptr(), amax.data_ptr(), 1.0, s)
+    A8 = torch.zeros((Mpad, KP), dtype=torch.uint8, device=dev)
+    h.weight_fp8(wflat.data_ptr(), A8.data_ptr(), cout, cin, k * k, cin, KP, scales.data_ptr(), s)
+    xf = LY.to_frame(x.to(dev), pad, cin)
+    s_x = (xf.float().abs().max() / 448.0).clamp_min(1e-12).reshape(1)
+    x8 = torch.zeros(xf.numel(), dtype=torch.uint8, device=dev)
+    h.frame_to_fp8(xf.data_ptr(), x8.data_ptr(), xf.numel(), s_x.data_ptr(), 0, s)
+    y = LY.alloc_frame(B, cout, 1, dev)
+    y8 = torch.zeros(y.numel(), dtype=torch.uint8, device=dev)
+    s_y = torch.full((1,), 1.0 / 64, device=dev)
+    amax_y = torch.zeros(1, dtype=torch.int32, device=dev)
+    h.conv_board_fp8(k, bm, A8.data_ptr(), KP, cout, Mpad, x8.data_ptr(), pad, cin, B,
+                     y.data_ptr(), y8.data_ptr(), 1, bias.float().contiguous().to(dev).data_ptr(),
+                     posb.float().contiguous().to(dev).data_ptr(), s_x.data_ptr(),
+                     scales.data_ptr(), s_y.data_ptr(), amax_y.data_ptr(), s)
+    y8f = (y8.view(torch.float8_e4m3fn).float() * s_y).reshape(y.shape).to(torch.bfloat16)
+    return (LY.from_frame(y, 1, cout), LY.from_frame(y8f, 1, cout), s_y.item(),
+            amax_y.view(torch.float32).item())
+
+
 def conv_dgrad(dz: torch.Tensor, w: torch.Tensor, aux: torch.Tensor, tiles=None) -> torch.Tensor:
     """dz [B,Cout,19,19], w OHWI [Cout,k,k,Cin], aux [B,Cin,19,19] (activation whose >0
     mask gates the result) -> dX*(aux>0) fp32 NCHW [B,Cin,19,19]."""

@@ -87,6 +87,32 @@ def test_conv_board_forward(B, cin, cout, k, bm, monkeypatch):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,cin,cout,k,bm", [(3, 128, 128, 3, 64), (2, 256, 128, 3, 64),
+                                             (2, 128, 256, 3, 128), (2, 128, 64, 1, 64)])
+def test_conv_board_fp8_forward(B, cin, cout, k, bm):
+    """FP8 (e4m3, MX-scaled MFMA) forward vs the fp32 reference of the same op: error at the
+    e4m3 quantization level (3 mantissa bits), bf16 + fp8 outputs, amax tracking."""
+    torch.manual_seed(8)
+    from deep_go_amd.ops import functional as Fn
+    x = torch.relu(torch.randn(B, cin, 19, 19, device=DEV))
+    w = torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y, y8, s_y, amax = Fn.conv_board_fp8(x, w, b, pb, bm=bm)
+    ref = F.relu(conv_ref(x, w, k) + b.view(1, -1, 1, 1) + pb.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref) < 0.08   # e4m3 operands: ~4-5% expected (CPU simulation)
+    # exact-semantics check: the same op on e4m3-rounded operands (torch's OCP e4m3fn cast)
+    q = lambda t, sc: ((t.cpu() / sc).to(torch.float8_e4m3fn).float() * sc).to(DEV)
+    xb = bf(x)  # the kernel quantizes the bf16 activation frame, with its amax
+    sx = xb.abs().max().item() / 448
+    sw = w.abs().max().item() / 448
+    ref_q = F.relu(conv_ref(q(xb, sx), q(w, sw), k) + b.view(1, -1, 1, 1)
+                   + pb.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref_q) < 1e-2
+    assert abs(amax - y.max().item()) < 1e-2 * y.max().item() + 1e-6
+    assert rel_err(y8, ref) < 0.15  # second quantization (fp8 shadow for the next layer)
+
+
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (4, 128, 128, 3), (2, 256, 256, 3),
                                           (2, 64, 128, 3)])
 @pytest.mark.parametrize("bm", ["64", "128"])
