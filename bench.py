@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
     args = ap.parse_args()
 
     import torch
@@ -55,7 +57,7 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg = get_preset("12x128-bf16", numLayers=args.layers, channelSize=args.channels,
-                     batchSize=args.batch * world, seed=1234)
+                     batchSize=args.batch * world, seed=1234, dtype=args.dtype)
     B = args.batch
     net = HipGoNet(cfg, B, device=dev, global_batch=B * world)
     if world > 1:
@@ -117,7 +119,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic (random 19x19 uint8 feature planes, GPU-expanded to 37 planes; random-init weights)",
             "config": {"model": f"{args.layers}-layer d={args.channels} CNN (5x5 first, 3x3 hidden, 3x3 head, untied biases)",
                        "global_batch": B * world, "seq_len": 361,

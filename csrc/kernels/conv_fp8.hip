@@ -14,7 +14,7 @@
 // Outputs: the bf16 activation frame (read by the bf16 backward and the head) AND an
 // fp8 shadow frame for the next layer's forward, quantized with that layer's delayed
 // scale s_y = amax_prev / 448; the kernel folds its own output amax into amax_y (bit-wise
-// atomicMax: post-ReLU values are >= 0).  fp8_scales_kernel turns amax into scales once
+// atomicMax: post-ReLU values are >= 0).  fp8_update_scales_kernel turns amax into scales once
 // per step.
 //
 // Reference op: nn.SpatialConvolutionMM forward + nn.Add + nn.ReLU (experiments.lua:138-147).
@@ -191,8 +191,8 @@ conv_board_fp8_kernel(Fp8Args a) {
       *(uint2*)(sT + p * ROWB + chunk * 16 + (col & 4) * 2) = o;
     }
   }
-  vmax = wave_max(vmax);
-  if (lane == 0 && a.amax_y) atomicMax(a.amax_y, __float_as_uint(vmax));
+  __shared__ float s_amax[8];
+  if (a.amax_y) block_amax(vmax, a.amax_y, s_amax);  // (uniform branch: contains a barrier)
   __syncthreads();
   const int Fy = BOARD + 2 * a.y_pad;
   char* Yb = a.Y + (size_t)b * Fy * Fy * a.M * 2;
@@ -218,36 +218,20 @@ conv_board_fp8_kernel(Fp8Args a) {
   }
 }
 
-// Per step, one block per layer: weight amax -> s_w; observed activation amax -> s_y (for
-// the next step's quantization; delayed scaling), amax reset.  scales[l] = {s_w, s_y} and
-// amax[l] (float bits).  A floor keeps all-zero tensors finite.
-struct ScaleLayer {
-  const float* w;
-  long long n;
-};
-constexpr int MAX_SCALE_LAYERS = 48;
-struct ScaleArgs {
-  int n;
-  ScaleLayer L[MAX_SCALE_LAYERS];
-};
-
-__global__ void __launch_bounds__(256)
-fp8_scales_kernel(ScaleArgs a, float* scales, unsigned* amax, float margin) {
-  const int l = blockIdx.x;
-  const ScaleLayer L = a.L[l];
-  float m = 0.f;
-  for (long long i = threadIdx.x; i < L.n; i += 256) m = fmaxf(m, fabsf(L.w[i]));
-  m = wave_max(m);
-  __shared__ float s_m[4];
-  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float mw = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-    scales[2 * l] = fmaxf(mw, 1e-12f) / FP8_MAX;
-    const float my = __uint_as_float(amax[l]);
-    if (my > 0.f) scales[2 * l + 1] = my * margin / FP8_MAX;
-    amax[l] = 0u;
-  }
+// Per step, BEFORE the weight refresh: s_w[l] from the weight amax the previous refresh
+// observed (delayed weight scaling, 5% headroom: SGD moves weights slowly; values past it
+// saturate at +-448), s_y[l] from the activation amax of the last forward; both reset.
+// scales[2l] = s_w, scales[2l+1] = s_y; amax_w / amax_y: float bits.
+__global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
+                                         float w_margin) {
+  const int l = threadIdx.x;
+  if (l >= n) return;
+  const float mw = __uint_as_float(amax_w[l]);
+  if (mw > 0.f) scales[2 * l] = mw * w_margin / FP8_MAX;
+  const float my = __uint_as_float(amax_y[l]);
+  if (my > 0.f) scales[2 * l + 1] = my / FP8_MAX;
+  amax_w[l] = 0u;
+  amax_y[l] = 0u;
 }
 
 // fp32 OHWI master -> e4m3 operand layout Wf8[co][t * cinp + ci] (quantized with s_w).
@@ -286,8 +270,8 @@ frame_to_fp8_kernel(const bf16_t* src, uint8_t* dst, size_t n, const float* s,
     *(uint32_t*)(dst + i) = pack_fp8x4(fminf(f0 * inv, FP8_MAX), fminf(f1 * inv, FP8_MAX),
                                        fminf(f2 * inv, FP8_MAX), fminf(f3 * inv, FP8_MAX));
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && amax) atomicMax(amax, __float_as_uint(m));
+  __shared__ float s_amax[4];
+  if (amax) block_amax(m, amax, s_amax);
 }
 
 template <typename K>
@@ -336,17 +320,11 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
   }
 }
 
-// table: n rows of {w ptr, numel}
-hipError_t dg_fp8_scales(const long long* table, int n, float* scales, unsigned* amax,
-                         float margin, hipStream_t s) {
-  if (n <= 0 || n > MAX_SCALE_LAYERS) return hipErrorInvalidValue;
-  ScaleArgs a;
-  a.n = n;
-  for (int i = 0; i < n; ++i) {
-    a.L[i].w = (const float*)table[2 * i];
-    a.L[i].n = table[2 * i + 1];
-  }
-  hipLaunchKernelGGL(fp8_scales_kernel, dim3(n), dim3(256), 0, s, a, scales, amax, margin);
+hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
+                               float w_margin, hipStream_t s) {
+  if (n <= 0 || n > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(1), dim3(n < 64 ? 64 : (n + 63) / 64 * 64), 0,
+                     s, n, scales, amax_w, amax_y, w_margin);
   return hipGetLastError();
 }
 

@@ -59,6 +59,24 @@ DG_DEV float wave_max(float v) {
   return v;
 }
 
+// Block-wide max of non-negative v folded into *amax (float bits) with ONE device atomic per
+// workgroup, skipped when the stored value is already larger (thousands of same-address
+// atomics serialize at the memory side).  s_tmp: >= blockDim/64 floats of LDS.  Every
+// thread of the block must call it (contains a barrier).
+DG_DEV void block_amax(float v, unsigned* amax, float* s_tmp) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) s_tmp[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = s_tmp[0];
+    for (int w = 1; w < nw; ++w) m = fmaxf(m, s_tmp[w]);
+    const unsigned u = __float_as_uint(m);
+    if (u > __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(amax, u);
+  }
+}
+
 // Exact floor(n / d) for 0 <= n < 2^22 and 1 <= d <= 4096 via a 64-bit magic
 // m = floor(2^32 / d) + 1 (host computes it; checked exhaustively in tests/tools).
 DG_DEV uint32_t fastdiv(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }

@@ -193,7 +193,10 @@ __global__ void lr_decay_kernel(double* lr, double decay, long long* step) {
 struct WRefreshLayer {
   const float* w;
   bf16_t* wf;
-  bf16_t* wd;  // may be null (first layer / head)
+  bf16_t* wd;          // may be null (first layer / head)
+  uint8_t* wf8;        // e4m3 forward operand (fp8 layers) or null; same [co][t*cinp+ci], kpf
+  const float* s_w;    // its quantization scale (device)
+  unsigned* amax_w;    // |w| max observed here (float bits) -> next step's s_w
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -218,10 +221,13 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
   const int nct = (L.cout + 63) / 64, nit = (L.cin + 63) / 64;
   const int tiles = L.taps * nct * nit;
   __shared__ float tileS[64][65];
+  __shared__ float s_amax[4];
+  float wmax = 0.f;
   for (int tix = blockIdx.x; tix < tiles; tix += gridDim.x) {
     const int t = tix / (nct * nit);
     const int r = tix - t * nct * nit;
     const int cot = r / nit, cit = r - cot * nit;
+    const float inv8 = L.wf8 ? 1.f / *L.s_w : 0.f;
     for (int e = threadIdx.x; e < 64 * 64; e += 256) {
       const int rr = e >> 6, cc = e & 63;
       const int co = cot * 64 + rr, ci = cit * 64 + cc;
@@ -229,6 +235,12 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       if (co < L.cout && ci < L.cin) {
         v = L.w[((size_t)co * L.taps + t) * L.cin + ci];
         L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = f2bf(v);
+        if (L.wf8) {
+          const float q = fmaxf(fminf(v * inv8, 448.f), -448.f);
+          L.wf8[(size_t)co * L.kpf + t * L.cinp + ci] =
+              (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xFF);
+          wmax = fmaxf(wmax, fabsf(v));
+        }
       }
       tileS[rr][cc] = v;
     }
@@ -243,6 +255,7 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
     }
     __syncthreads();
   }
+  if (L.wf8 && L.amax_w) block_amax(wmax, L.amax_w, s_amax);  // uniform per block
 }
 
 }  // namespace
@@ -299,7 +312,8 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
   return hipGetLastError();
 }
 
-// layers: n entries of 10 int64 words {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused}
+// layers: n entries of 13 int64 words
+//   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused, wf8, s_w, amax_w}
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -308,7 +322,7 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 10 * i;
+    const long long* t = table + 13 * i;
     a.L[i].w = (const float*)t[0];
     a.L[i].wf = (bf16_t*)t[1];
     a.L[i].wd = (bf16_t*)t[2];
@@ -318,6 +332,9 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].cinp = (int)t[6];
     a.L[i].kpf = (int)t[7];
     a.L[i].kpd = (int)t[8];
+    a.L[i].wf8 = (uint8_t*)t[10];
+    a.L[i].s_w = (const float*)t[11];
+    a.L[i].amax_w = (unsigned*)t[12];
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;
   }

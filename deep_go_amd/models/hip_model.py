@@ -55,6 +55,7 @@ class ConvPlan:
     board: bool = False    # fwd uses the board-tiled kernel
     board_d: bool = False  # dgrad uses the board-tiled kernel
     wgrad3: bool = False   # wgrad uses the row-stripe kernel (conv_wgrad3.hip)
+    fp8: bool = False      # forward on the e4m3 MX-MFMA kernel (conv_fp8.hip)
 
 
 class HipGoNet:
@@ -96,6 +97,10 @@ class HipGoNet:
 
         # ---- per-layer plans + bf16 operand weights ----
         self.plans: List[ConvPlan] = []
+        self.fp8 = cfg.dtype == "fp8"
+        if cfg.dtype not in ("bf16", "fp8"):
+            raise ValueError(f"unsupported GPU dtype {cfg.dtype!r} (bf16 | fp8)")
+        self.wf8: List[Optional[torch.Tensor]] = []
         self.wf: List[torch.Tensor] = []
         self.wd: List[Optional[torch.Tensor]] = []
         for spec in L[:-1]:
@@ -125,6 +130,9 @@ class HipGoNet:
                 self.wd.append(torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=dev))
             else:
                 self.wd.append(None)
+            p.fp8 = self.fp8 and board and cinp % 128 == 0
+            self.wf8.append(torch.zeros((Mpad, KP), dtype=torch.uint8, device=dev)
+                            if p.fp8 else None)
             self.plans.append(p)
         self.head = L[-1]
 
@@ -136,6 +144,18 @@ class HipGoNet:
         self.act = [LY.alloc_frame(B, L[i].cout, pads[i + 1], dev) for i in range(self.L - 1)]
         # dz[i]: d loss / d pre-activation of layer i, framed with layer i's pad (>=1)
         self.dz = [LY.alloc_frame(B, L[i].cout, max(1, pads[i]), dev) for i in range(self.L - 1)]
+        # fp8 shadow of the input frame of every fp8 layer (same geometry, 1 byte/elem);
+        # per conv layer l: scales[2l] = s_w, scales[2l+1] = s_y (scale of act[l]'s fp8
+        # shadow), amax[l] = observed max of act[l] (float bits), delayed scaling
+        self.x8: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        for p in self.plans:
+            if p.fp8:
+                src = self.x0 if p.index == 0 else self.act[p.index - 1]
+                self.x8[p.index] = torch.zeros(src.numel(), dtype=torch.uint8, device=dev)
+        self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
+        self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
+        self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
+        self._fp8_calibrated = not self.fp8
         slab = max(p.splits * p.Mpad_w * p.KPw for p in self.plans)
         self.slab = torch.empty(slab, dtype=torch.float32, device=dev)
         self.bchunks = self.h.bias_chunks(batch)
@@ -176,8 +196,12 @@ class HipGoNet:
         for p, wf, wd in zip(self.plans, self.wf, self.wd):
             spec = self.layout.layers[p.index]
             w = self.params[spec.w_off:spec.w_off + spec.w_numel]
+            w8 = self.wf8[p.index]
             rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0,
-                         p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd, 0])
+                         p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd, 0,
+                         w8.data_ptr() if w8 is not None else 0,
+                         self.fp8_scales.data_ptr() + 8 * p.index if w8 is not None else 0,
+                         self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
     def _build_plans(self):
@@ -196,7 +220,18 @@ class HipGoNet:
             xin = self.x0 if p.index == 0 else self.act[p.index - 1]
             x_pad = spec.pad
             y_pad = lay.layers[p.index + 1].pad
-            if p.board:
+            nxt = self.plans[p.index + 1] if p.index + 1 < len(self.plans) else None
+            if p.fp8:
+                i = p.index
+                S = self.fp8_scales.data_ptr()
+                y8 = self.x8[i + 1].data_ptr() if nxt is not None and nxt.fp8 else 0
+                self._fwd.append((h.conv_board_fp8, (
+                    p.k, p.bm, self.wf8[i].data_ptr(), p.KP, p.cout, p.Mpad,
+                    self.x8[i].data_ptr(), x_pad, p.cinp, self.B, self.act[i].data_ptr(), y8,
+                    y_pad, P + spec.b_off * f4, P + spec.pos_off * f4, S + (2 * i - 1) * f4,
+                    S + 2 * i * f4, S + (2 * i + 1) * f4,
+                    self.fp8_amax.data_ptr() + i * 4 if y8 else 0)))
+            elif p.board:
                 self._fwd.append((h.conv_board, (h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(),
                                                  p.KP, p.cout, p.Mpad, xin.data_ptr(), x_pad,
                                                  p.cinp, self.B, self.act[p.index].data_ptr(),
@@ -208,6 +243,13 @@ class HipGoNet:
                                               xin.data_ptr(), x_pad, p.cinp, self.npix,
                                               self.act[p.index].data_ptr(), y_pad,
                                               P + spec.b_off * f4, P + spec.pos_off * f4, 0, 0)))
+            if nxt is not None and nxt.fp8 and not p.fp8:
+                # bf16 producer feeding an fp8 layer: quantize its output frame
+                i = p.index
+                self._fwd.append((h.frame_to_fp8, (
+                    self.act[i].data_ptr(), self.x8[i + 1].data_ptr(), self.act[i].numel(),
+                    self.fp8_scales.data_ptr() + (2 * i + 1) * 4,
+                    self.fp8_amax.data_ptr() + i * 4)))
         hd = self.head
         hx = self.act[-1]
         self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
@@ -276,10 +318,14 @@ class HipGoNet:
         self.player.copy_(player, non_blocking=non_blocking)
         self.rank.copy_(rank, non_blocking=non_blocking)
         self.labels.copy_(labels, non_blocking=non_blocking)
+        if not self._fp8_calibrated:
+            self.calibrate_fp8()
 
     def set_batch_packed(self, packed: torch.Tensor, non_blocking: bool = True):
         """One copy of a ``pack_batch`` buffer (device or pinned host) into the inputs."""
         self.inbuf.copy_(packed, non_blocking=non_blocking)
+        if not self._fp8_calibrated:
+            self.calibrate_fp8()
 
     def forward(self):
         s = stream_handle()
@@ -352,14 +398,38 @@ class HipGoNet:
         else:
             self.h.sgd(self.params.data_ptr(), self.grads.data_ptr(), n, self.lr.data_ptr(),
                        grad_scale, gate, s)
-        # bf16 operand copies of the updated weights + lr *= (1 - rateDecay), one launch
+        self._fp8_update(s)
+        # bf16 (+ e4m3) operand copies of the updated weights + lr *= (1 - rateDecay)
         self.h.weight_refresh_decay(self._refresh_table.ctypes.data, len(self._refresh_table),
                                     self.lr.data_ptr(), float(self.cfg.rateDecay),
                                     self.step_count.data_ptr(), s)
 
     def refresh_weights(self):
-        self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table),
-                              stream_handle())
+        """bf16 (and fp8) operand copies of the fp32 master weights (init / load)."""
+        s = stream_handle()
+        n = len(self._refresh_table)
+        self.h.weight_refresh(self._refresh_table.ctypes.data, n, s)
+        if self.fp8:  # first pass observed |w| max: derive s_w, requantize with it
+            self._fp8_update(s)
+            self.h.weight_refresh(self._refresh_table.ctypes.data, n, s)
+
+    def _fp8_update(self, s):
+        """Delayed scaling: s_w from the last refresh's weight amax (+5%), s_y from the last
+        forward's activation amax; runs BEFORE the refresh that quantizes with s_w."""
+        if self.fp8:
+            self.h.fp8_update_scales(len(self.plans), self.fp8_scales.data_ptr(),
+                                     self.fp8_amax_w.data_ptr(), self.fp8_amax.data_ptr(), 1.05,
+                                     s)
+
+    def calibrate_fp8(self):
+        """Forwards on the current inputs to observe activation ranges, then derive the
+        fp8 scales (called automatically on the first batch of an fp8 model)."""
+        s = stream_handle()
+        for _ in range(2):
+            self.evaluate()
+            self._fp8_update(s)
+            self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table), s)
+        self._fp8_calibrated = True
 
     def train_step(self):
         self.forward_backward()

@@ -96,12 +96,7 @@ def conv_board_fp8(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: t
     KP, _, Mpad = LY.conv_dims(k, cin, cout, bm)
     s = stream_handle()
     wflat = w.float().contiguous().to(dev)
-    # scales[0] = s_w, scales[1] = (unused) ; s_x / s_y separate device scalars
-    scales = torch.ones(2, device=dev)
-    amax = torch.zeros(1, dtype=torch.int32, device=dev)
-    import numpy as np
-    tbl = np.array([[wflat.data_ptr(), wflat.numel()]], dtype=np.int64)
-    h.fp8_scales(tbl.ctypes.data, 1, scales.data_ptr(), amax.data_ptr(), 1.0, s)
+    scales = (wflat.abs().max() / 448.0).clamp_min(1e-12).reshape(1)  # s_w
     A8 = torch.zeros((Mpad, KP), dtype=torch.uint8, device=dev)
     h.weight_fp8(wflat.data_ptr(), A8.data_ptr(), cout, cin, k * k, cin, KP, scales.data_ptr(), s)
     xf = LY.to_frame(x.to(dev), pad, cin)
@@ -266,7 +261,8 @@ def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0,
     cout, k, _, cin = w.shape
     wf = torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=w.device)
     wd = torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=w.device) if KPd else None
-    tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0]],
+    tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0,
+                     0, 0, 0]],
                    dtype=np.int64)
     h.weight_refresh(tbl.ctypes.data, 1, stream_handle())
     torch.cuda.synchronize()

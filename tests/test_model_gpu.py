@@ -123,6 +123,41 @@ def test_lr_decay_fused_into_weight_refresh():
     assert abs(net.lr.item() - cfg.rate * (1 - 1e-3) ** 3) < 1e-15
 
 
+def test_fp8_forward_model_tracks_bf16():
+    """dtype='fp8': hidden-layer forwards on e4m3 MX-MFMA with delayed scaling; loss and
+    gradients stay close to the bf16 model with the same weights and batch."""
+    _, net_b, _ = _setup(4, 128, 6, seed=3)
+    _, net_8, _ = _setup(4, 128, 6, seed=3, dtype="fp8")
+    assert any(p.fp8 for p in net_8.plans) and net_8._fp8_calibrated
+    net_b.forward_backward()
+    net_8.forward_backward()
+    torch.cuda.synchronize()
+    lb, l8 = net_b.mean_loss().item(), net_8.mean_loss().item()
+    assert abs(lb - l8) < 0.03 * abs(lb), (lb, l8)
+    gb, g8 = net_b.grads, net_8.grads
+    assert ((g8 - gb).norm() / gb.norm()).item() < 0.15
+    assert torch.isfinite(net_8.fp8_scales).all() and (net_8.fp8_scales > 0).all()
+
+
+def test_fp8_training_reduces_loss():
+    """Same memorisation run as test_loss_decreases, fp8 forward vs bf16: both converge and
+    the fp8 trajectory stays close to the bf16 one."""
+    from deep_go_amd.models.hip_model import SegmentedStep
+    finals = {}
+    for dt in ("bf16", "fp8"):
+        cfg, net, data = _setup(4, 128, 16, seed=4, dtype=dt, head_relu=False, rate=0.1)
+        step = SegmentedStep(net, None, use_graphs=True)
+        losses = []
+        for _ in range(40):
+            step()
+            losses.append(net.mean_loss().item())
+        torch.cuda.synchronize()
+        assert all(np.isfinite(losses)), (dt, losses)
+        assert losses[-1] < 0.8 * losses[0], (dt, losses[0], losses[-1])
+        finals[dt] = losses[-1]
+    assert abs(finals["fp8"] - finals["bf16"]) < 0.1, finals  # both memorise the batch
+
+
 def test_loss_decreases():
     # head_relu=False: with the reference's head ReLU a large LR kills every logit (the
     # loss then pins at ln(361) exactly, see test_head_relu_dead_logits_quirk)
