@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--profile", type=int, default=0, metavar="N",
+                    help="after the timed run, N extra steps with roctx ranges (load / segments"
+                         " / allreduce / optimizer) and a host phase breakdown; run under "
+                         "rocprofv3 --marker-trace --kernel-trace to see them on the timeline")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
     args = ap.parse_args()
@@ -100,6 +104,19 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
+    phases = None
+    if args.profile > 0:
+        from deep_go_amd.utils import trace
+        trace.enable(True, host_timing=True)
+        torch.cuda.synchronize()
+        for i in range(args.profile):
+            with trace.range("step"):
+                with trace.range("load"):
+                    load(i)
+                step()
+        torch.cuda.synchronize()
+        phases = {k: round(1e3 * v / args.profile, 4) for k, v in trace.totals(True).items()}
+        trace.enable(False)
     # accuracy/loss of the last step (sanity: finite)
     loss = net.mean_loss().item()
     acc = net.correct().item() / B
@@ -128,6 +145,7 @@ def main():
             "last_loss": round(loss, 4),
             "last_batch_top1": round(acc, 4),
             "graphs": not args.no_graph,
+            **({"profile_host_ms_per_step": phases} if phases else {}),
         }), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

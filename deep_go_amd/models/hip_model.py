@@ -28,6 +28,7 @@ import torch
 from ..config import NUM_POINTS, ExperimentConfig
 from ..ops import layouts as LY
 from ..ops.native import hip, stream_handle
+from ..utils import trace
 from .gocnn import ParamLayout, init_params
 
 INPUT_CP = 40  # 37 planes padded to 5 x 8-channel groups
@@ -587,21 +588,25 @@ class SegmentedStep:
     def forward_backward(self):
         """Gradients (all-reduced across ranks when DP) of the batch in the input buffers."""
         for si, (fns, fire) in enumerate(self.segments):
-            if self.use_graphs:
-                self.graphs[si].replay()
-            else:
-                self._call_all(fns)
+            with trace.range(f"segment{si}"):
+                if self.use_graphs:
+                    self.graphs[si].replay()
+                else:
+                    self._call_all(fns)
             if self.bucketer is not None:
-                for b in fire:
-                    self.bucketer.fire(b)
+                with trace.range("allreduce_issue"):
+                    for b in fire:
+                        self.bucketer.fire(b)
         if self.bucketer is not None:
-            self.bucketer.wait()
+            with trace.range("allreduce_wait"):
+                self.bucketer.wait()
 
     def optimizer(self):
-        if self.use_graphs:
-            self.opt_graph.replay()
-        else:
-            self.net.optimizer_step()
+        with trace.range("optimizer"):
+            if self.use_graphs:
+                self.opt_graph.replay()
+            else:
+                self.net.optimizer_step()
 
     def __call__(self):
         self.forward_backward()

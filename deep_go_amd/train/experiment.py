@@ -28,6 +28,7 @@ from ..config import ExperimentConfig
 from ..data.dataset import GameIndex, PackedDataset, load_index
 from ..data.loader import BatchLoader
 from ..parallel import dp
+from ..utils import trace
 from ..utils import checkpoint as ckpt
 from ..utils.faults import StepWatchdog, check_finite, maybe_inject, parse_fault
 from ..utils.metrics import MetricsSink
@@ -163,10 +164,13 @@ class Experiment:
         n_log = 0
         last_val = None
         for _ in range(iters):
-            batch = loader.next_numpy()
+            with trace.range("loader_wait"):
+                batch = loader.next_numpy()
             self.loader_seq = loader.consumed
-            be.set_batch(*batch)
-            be.forward_backward()
+            with trace.range("h2d"):
+                be.set_batch(*batch)
+            with trace.range("fwd_bwd"):
+                be.forward_backward()
             step = self.iterations + 1
             inj = maybe_inject(info.rank, step, fault) if fault else None
             need_cost = (step % cfg.log_interval == 0) or (step % cfg.validation_interval == 0) \
@@ -181,7 +185,8 @@ class Experiment:
             self.iterations = step
             n_log += 1
             if step % cfg.validation_interval == 0:
-                vc, va = self.eval_batch_set(val)
+                with trace.range("validation"):
+                    vc, va = self.eval_batch_set(val)
                 last_val = vc
                 self.validation_costs.append(vc)
                 self.validation_accuracies.append(va)
@@ -189,7 +194,8 @@ class Experiment:
                 self.metrics.record(kind="validation", step=step, val_cost=vc, val_acc=va,
                                     lr=be.rate)
                 if info.is_main:
-                    self.save()
+                    with trace.range("checkpoint"):
+                        self.save()
             if step % cfg.log_interval == 0:
                 now = time.perf_counter()
                 bps = n_log * cfg.batchSize / max(now - t_log, 1e-9)
@@ -199,7 +205,8 @@ class Experiment:
                 self.metrics.record(kind="train", step=step, loss_ema=ema, boards_per_sec=bps,
                                     lr=be.rate)
                 t_log, n_log = now, 0
-            be.optimizer_step()
+            with trace.range("optimizer"):
+                be.optimizer_step()
             if watchdog:
                 watchdog.beat()
         if torch.cuda.is_available() and self._device_kind() == "hip":

@@ -206,3 +206,21 @@ def test_cli_train_resume_eval(tmp_path, ref_data):
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr
     assert 0.0 <= json.loads(r.stdout.strip().splitlines()[-1])["accuracy"] <= 1.0
+
+
+def test_roctx_ranges_and_host_phase_timing():
+    """roctx ranges around step phases (no-op unless enabled)."""
+    from deep_go_amd.utils import trace
+    with trace.range("off"):  # disabled: no-op, nothing recorded
+        pass
+    assert trace.totals() == {}
+    trace.enable(True, host_timing=True)
+    try:
+        with trace.range("phase_a"):
+            with trace.range("phase_b"):
+                pass
+        trace.mark("m")
+        tot = trace.totals(reset=True)
+        assert set(tot) == {"phase_a", "phase_b"} and tot["phase_a"] >= tot["phase_b"] >= 0
+    finally:
+        trace.enable(False)
