@@ -1,6 +1,6 @@
 """Command line: ``python -m deep_go_amd <command> ...``
 
-  train     [--preset NAME] [key=value ...] --iters N [--export-t7 PATH]
+  train     [--preset NAME] [key=value ...] --iters N [--export-t7 PATH] [--auto-resume]
             (localtest.lua / default-experiment.lua / notebook equivalents via presets)
   resume    CKPT --iters N [--reset-optimizer] [--id NAME] [key=value ...]
             (experiments/repeated.lua: -gpu/-num/-iters -> --device/--id/--iters)
@@ -42,7 +42,20 @@ def cmd_train(args):
     elif args.device == "gpu":
         cfg = cfg.replace(useCuda=True)
     e = Experiment(cfg)
-    res = e.run(args.iters)
+    iters = args.iters
+    if args.auto_resume:
+        # restart after a failure: continue <checkpoint_dir>/<id>.model
+        # (exact resume: weights, optimizer, iteration, sampler cursor, RNG) up to --iters
+        if not cfg.id:
+            raise SystemExit("--auto-resume needs a stable experiment id (id=NAME)")
+        path = e.checkpoint_path()
+        if os.path.exists(path):
+            e = Experiment.load(path)
+            if args.device == "cpu":
+                e.cfg = e.cfg.replace(useCuda=False)
+            iters = max(0, args.iters - e.iterations)
+            print(json.dumps({"auto_resume": path, "from_iteration": e.iterations}), flush=True)
+    res = e.run(iters) if iters > 0 else {"iterations": e.iterations}
     if e.info.is_main:
         e.save()
         if args.export_t7:
@@ -138,6 +151,8 @@ def main(argv=None):
     t.add_argument("--iters", type=int, required=True)
     t.add_argument("--device", choices=["auto", "cpu", "gpu"], default="auto")
     t.add_argument("--export-t7")
+    t.add_argument("--auto-resume", action="store_true",
+                   help="continue from <checkpoint_dir>/<id>.model if it exists (--iters = total)")
     t.add_argument("overrides", nargs="*")
     t.set_defaults(fn=cmd_train)
     r = sub.add_parser("resume")

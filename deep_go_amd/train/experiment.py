@@ -163,6 +163,7 @@ class Experiment:
         t_log = t_start
         n_log = 0
         last_val = None
+        save_now = False
         for _ in range(iters):
             with trace.range("loader_wait"):
                 batch = loader.next_numpy()
@@ -193,9 +194,10 @@ class Experiment:
                 self.metrics.line(f"validation at iteration {step}: cost={vc}, accuracy={va}")
                 self.metrics.record(kind="validation", step=step, val_cost=vc, val_acc=va,
                                     lr=be.rate)
-                if info.is_main:
-                    with trace.range("checkpoint"):
-                        self.save()
+                # the reference saves here, BEFORE this iteration's update (train.lua:124):
+                # that checkpoint pairs iteration N with N-1 updates.  We save after the
+                # update below so a resumed run continues bit-exactly (auto-resume).
+                save_now = info.is_main
             if step % cfg.log_interval == 0:
                 now = time.perf_counter()
                 bps = n_log * cfg.batchSize / max(now - t_log, 1e-9)
@@ -207,6 +209,10 @@ class Experiment:
                 t_log, n_log = now, 0
             with trace.range("optimizer"):
                 be.optimizer_step()
+            if save_now:
+                with trace.range("checkpoint"):
+                    self.save()
+                save_now = False
             if watchdog:
                 watchdog.beat()
         if torch.cuda.is_available() and self._device_kind() == "hip":

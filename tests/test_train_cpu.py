@@ -224,3 +224,35 @@ def test_roctx_ranges_and_host_phase_timing():
         assert set(tot) == {"phase_a", "phase_b"} and tot["phase_a"] >= tot["phase_b"] >= 0
     finally:
         trace.enable(False)
+
+
+def test_cli_auto_resume_after_interruption(tmp_path, ref_data):
+    """SURVEY.md §5.3 auto-resume: a run killed by an injected fault restarts from its last
+    checkpoint and ends bit-identical to an uninterrupted run."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=os.getcwd())
+    base = [sys.executable, "-m", "deep_go_amd", "train", "--device", "cpu"]
+    ov = [f"data_root={ref_data}", "numLayers=2", "channelSize=16", "batchSize=4",
+          "validationSize=8", "validation_interval=3", "log_interval=3", "loader_threads=2",
+          "seed=9"]
+    # uninterrupted reference: 9 iterations
+    r = subprocess.run(base + ["--iters", "9", f"checkpoint_dir={tmp_path / 'ref'}", "id=ref"]
+                       + ov, capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    # interrupted: process exits at step 5 (checkpoint of step 3 on disk), then resumes
+    ck = tmp_path / "ar"
+    r = subprocess.run(base + ["--iters", "9", f"checkpoint_dir={ck}", "id=ar"] + ov,
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(env, DG_FAULT="0:5:exit"))
+    assert r.returncode != 0
+    r = subprocess.run(base + ["--iters", "9", "--auto-resume", f"checkpoint_dir={ck}", "id=ar"]
+                       + ov, capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    assert lines[0]["from_iteration"] == 3 and lines[-1]["iterations"] == 9
+    from deep_go_amd.utils import checkpoint as ckm
+    _, a, sa, _ = ckm.load_checkpoint(str(tmp_path / "ref" / "ref.model"))
+    _, b, sb, _ = ckm.load_checkpoint(str(ck / "ar.model"))
+    assert torch.equal(a, b) and sa["iterations"] == sb["iterations"] == 9
