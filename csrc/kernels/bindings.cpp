@@ -23,11 +23,15 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          const float* bias, const float* posb, const void* aux, int aux_pad,
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
+hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
+                            const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
+                            const float* bias, const float* posb, const void* pbias,
+                            const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
-                             const float* s_w, const float* s_y, unsigned* amax_y,
+                             const float* s_w, const float* s_y, unsigned* amax_y, void* mask,
                              hipStream_t stream);
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
                                float w_margin, hipStream_t s);
@@ -108,6 +112,17 @@ PYBIND11_MODULE(_dghip, m) {
                               aux_pad, S(stream)),
                 "conv_board");
         });
+  m.def("conv_board_ex",
+        [](int epi, int kw, int bm, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
+           int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
+           uintptr_t pbias, uintptr_t aux, int aux_pad, uintptr_t mask, uintptr_t stream) {
+          check(dg_conv_board_ex(epi, kw, bm, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C,
+                                 B, P<void>(Y), y_pad, P<float>(bias), P<float>(posb),
+                                 P<void>(pbias), P<void>(aux), aux_pad, P<void>(mask),
+                                 S(stream)),
+                "conv_board_ex");
+        },
+        "conv_board + optional bf16 bias table (fwd) and ReLU bitmask (fwd writes, dgrad reads)");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
                          int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {
@@ -128,11 +143,11 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_board_fp8", [](int kw, int bm, uintptr_t A8, int KP, int M, int Mpad, uintptr_t X8,
                              int x_pad, int x_C, int B, uintptr_t Y, uintptr_t Y8, int y_pad,
                              uintptr_t bias, uintptr_t posb, uintptr_t s_x, uintptr_t s_w,
-                             uintptr_t s_y, uintptr_t amax_y, uintptr_t stream) {
+                             uintptr_t s_y, uintptr_t amax_y, uintptr_t mask, uintptr_t stream) {
     check(dg_conv_board_fp8(kw, bm, P<void>(A8), KP, M, Mpad, P<void>(X8), x_pad, x_C, B,
                             P<void>(Y), P<void>(Y8), y_pad, P<float>(bias), P<float>(posb),
                             P<float>(s_x), P<float>(s_w), P<float>(s_y), P<unsigned>(amax_y),
-                            S(stream)),
+                            P<void>(mask), S(stream)),
           "conv_board_fp8");
   });
   m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, uintptr_t amax_y,

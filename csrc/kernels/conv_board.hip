@@ -40,6 +40,9 @@ struct BoardArgs {
   int x_pad, x_C;
   int y_pad;
   int aux_pad;
+  const bf16_t* pbias;  // [361][M] bf16 bias + pos_bias (EPI_FWD; replaces bias/posb if set)
+  uint8_t* mask;        // [B][361][M/8] ReLU bitmask: written by EPI_FWD, read by EPI_DGRAD
+                        // (replaces the aux frame) — 1 bit instead of a bf16 per element
   int ablate;  // diagnostics (tools/kbench.py): 1 no MFMA, 2 no LDS reads, 4 no DMA,
               // 8 no epilogue, 16 no per-step barrier (timing only)
 };
@@ -217,7 +220,8 @@ conv_board_kernel(BoardArgs a) {
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
     const int co = m_tile + wm * 64 + i * 16 + lq * 4;
-    if constexpr (EPI == EPI_FWD) bb[i] = *(const f32x4*)(a.bias + (co < a.M ? co : 0));
+    if constexpr (EPI == EPI_FWD)
+      bb[i] = a.pbias ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(a.bias + (co < a.M ? co : 0));
   }
   f32x4 pb[NF][MF];
   if constexpr (EPI == EPI_FWD) {
@@ -228,7 +232,14 @@ conv_board_kernel(BoardArgs a) {
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const int co = m_tile + wm * 64 + i * 16 + lq * 4;
-        pb[j][i] = *(const f32x4*)(a.posb + p * a.M + (co < a.M ? co : 0));
+        const int cc = co < a.M ? co : 0;
+        if (a.pbias) {  // combined bf16 table: 8 B per 4 channels instead of 16 B + bias
+          const uint2 u = *(const uint2*)(a.pbias + p * a.M + cc);
+          pb[j][i] = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xFFFF0000u)};
+        } else {
+          pb[j][i] = *(const f32x4*)(a.posb + p * a.M + cc);
+        }
       }
     }
   }
@@ -263,7 +274,26 @@ conv_board_kernel(BoardArgs a) {
     if (co >= a.M) continue;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     uint4 v = *(const uint4*)(sT + p * ROWB + ((c ^ (p & CMASK)) * 16));
+    const size_t mbyte = ((size_t)b * NPTS + p) * (a.M >> 3) + (co >> 3);
+    if constexpr (EPI == EPI_FWD) {
+      if (a.mask) {  // post-ReLU: bit = value != 0 (== value > 0)
+        auto nz = [](uint32_t u) { return ((u & 0xFFFFu) ? 1u : 0u) | ((u >> 16) ? 2u : 0u); };
+        a.mask[mbyte] = (uint8_t)(nz(v.x) | (nz(v.y) << 2) | (nz(v.z) << 4) | (nz(v.w) << 6));
+      }
+    }
     if constexpr (EPI == EPI_DGRAD) {
+      if (a.mask) {
+        const uint32_t mb = a.mask[mbyte];
+        auto keep = [](uint32_t val, uint32_t bits) {
+          return val & (((bits & 1u) ? 0xFFFFu : 0u) | ((bits & 2u) ? 0xFFFF0000u : 0u));
+        };
+        v.x = keep(v.x, mb);
+        v.y = keep(v.y, mb >> 2);
+        v.z = keep(v.z, mb >> 4);
+        v.w = keep(v.w, mb >> 6);
+        *(uint4*)(Yb + (size_t)(((h + a.y_pad) * Fy + (w + a.y_pad)) * a.M + co) * 2) = v;
+        continue;
+      }
       const uint4 m = *(const uint4*)(Ab + (size_t)(((h + a.aux_pad) * Fa + (w + a.aux_pad)) * a.M + co) * 2);
       // keep the gradient where the activation is > 0 (bf16: sign clear and non-zero)
       auto gate = [](uint32_t val, uint32_t msk) {
@@ -320,15 +350,21 @@ hipError_t dispatch_epi(int epi, const BoardArgs& a, int B, int Mpad, hipStream_
 static int g_board_ablate = 0;
 extern "C" void dg_conv_board_set_ablate(int mode) { g_board_ablate = mode; }
 
-extern "C" hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M,
-                                    int Mpad, const void* X, int x_pad, int x_C, int B, void* Y,
-                                    int y_pad, const float* bias, const float* posb,
-                                    const void* aux, int aux_pad, hipStream_t stream) {
+// pbias (EPI_FWD, optional): bf16 [361][M] bias + pos_bias table (replaces bias / posb);
+// mask (optional): ReLU bitmask [B][361][M/8] — EPI_FWD writes it, EPI_DGRAD gates with it
+// instead of reading the aux activation frame.
+extern "C" hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M,
+                                       int Mpad, const void* X, int x_pad, int x_C, int B,
+                                       void* Y, int y_pad, const float* bias, const float* posb,
+                                       const void* pbias, const void* aux, int aux_pad,
+                                       void* mask, hipStream_t stream) {
   if (x_C % 64 != 0 || M % 8 != 0 || (bm != 64 && bm != 128) || Mpad % bm != 0 || B <= 0)
     return hipErrorInvalidValue;
   if (KP < kw * kw * x_C || x_pad < (kw - 1) / 2) return hipErrorInvalidValue;
+  if (epi == EPI_DGRAD && !aux && !mask) return hipErrorInvalidValue;
   BoardArgs a{(const bf16_t*)A, (const char*)X, (char*)Y, bias, posb, (const char*)aux, KP, M,
-              x_pad, x_C, y_pad, aux_pad, g_board_ablate};
+              x_pad, x_C, y_pad, aux_pad, (const bf16_t*)pbias, (uint8_t*)mask,
+              g_board_ablate};
   const int wm = bm / 64;
   switch (kw) {
     case 1: return wm == 2 ? dispatch_epi<1, 2>(epi, a, B, Mpad, stream)
@@ -337,4 +373,12 @@ extern "C" hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int 
                            : dispatch_epi<3, 1>(epi, a, B, Mpad, stream);
     default: return hipErrorInvalidValue;
   }
+}
+
+extern "C" hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M,
+                                    int Mpad, const void* X, int x_pad, int x_C, int B, void* Y,
+                                    int y_pad, const float* bias, const float* posb,
+                                    const void* aux, int aux_pad, hipStream_t stream) {
+  return dg_conv_board_ex(epi, kw, bm, A, KP, M, Mpad, X, x_pad, x_C, B, Y, y_pad, bias, posb,
+                          nullptr, aux, aux_pad, nullptr, stream);
 }

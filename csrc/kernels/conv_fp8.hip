@@ -48,6 +48,7 @@ struct Fp8Args {
   const float* s_w;    // weight scale
   const float* s_y;    // output fp8 scale
   unsigned* amax_y;    // output amax (float bits)
+  uint8_t* mask;       // ReLU bitmask [B][361][M/8] for the bf16 dgrad (or null)
   int KP, M, x_pad, x_C, y_pad;
 };
 
@@ -205,6 +206,11 @@ conv_board_fp8_kernel(Fp8Args a) {
     const uint4 v = *(const uint4*)(sT + p * ROWB + ((c ^ (p & CMASK)) * 16));
     const size_t pix = (size_t)((h + a.y_pad) * Fy + (w + a.y_pad)) * a.M + co;
     *(uint4*)(Yb + pix * 2) = v;
+    if (a.mask) {
+      auto nz = [](uint32_t u) { return ((u & 0xFFFFu) ? 1u : 0u) | ((u >> 16) ? 2u : 0u); };
+      a.mask[((size_t)b * NPTS + p) * (a.M >> 3) + (co >> 3)] =
+          (uint8_t)(nz(v.x) | (nz(v.y) << 2) | (nz(v.z) << 4) | (nz(v.w) << 6));
+    }
     if (Y8b) {
       auto q = [&](uint32_t u, int hi) {
         const float f = __uint_as_float(hi ? (u & 0xFFFF0000u) : (u << 16));
@@ -316,12 +322,12 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
                              const float* s_w, const float* s_y, unsigned* amax_y,
-                             hipStream_t stream) {
+                             void* mask, hipStream_t stream) {
   if (x_C % 128 != 0 || M % 8 != 0 || (bm != 64 && bm != 128) || Mpad % bm != 0 || B <= 0)
     return hipErrorInvalidValue;
   if (KP < kw * kw * x_C || KP % 16 != 0 || x_pad < (kw - 1) / 2) return hipErrorInvalidValue;
   Fp8Args a{(const uint8_t*)A8, (const uint8_t*)X8, (char*)Y, (uint8_t*)Y8, bias, posb, s_x,
-            s_w, s_y, amax_y, KP, M, x_pad, x_C, y_pad};
+            s_w, s_y, amax_y, (uint8_t*)mask, KP, M, x_pad, x_C, y_pad};
   const bool w2 = bm == 128;
   switch (kw) {
     case 1: return w2 ? launch_fp8<1, 2>(a, B, Mpad, stream) : launch_fp8<1, 1>(a, B, Mpad, stream);

@@ -197,6 +197,9 @@ struct WRefreshLayer {
   uint8_t* wf8;        // e4m3 forward operand (fp8 layers) or null; same [co][t*cinp+ci], kpf
   const float* s_w;    // its quantization scale (device)
   unsigned* amax_w;    // |w| max observed here (float bits) -> next step's s_w
+  const float* bias;   // [cout]            } pbias[p][co] = bf16(bias[co] + posb[p][co]):
+  const float* posb;   // [361][cout]       } the forward epilogue's single bias table
+  bf16_t* pbias;       // [361][cout] or null
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -256,6 +259,11 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
     __syncthreads();
   }
   if (L.wf8 && L.amax_w) block_amax(wmax, L.amax_w, s_amax);  // uniform per block
+  if (L.pbias) {
+    const int n = NPTS * L.cout;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256)
+      L.pbias[e] = f2bf(L.bias[e % L.cout] + L.posb[e]);
+  }
 }
 
 }  // namespace
@@ -312,8 +320,8 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
   return hipGetLastError();
 }
 
-// layers: n entries of 13 int64 words
-//   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused, wf8, s_w, amax_w}
+// layers: n entries of 16 int64 words
+//   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused, wf8, s_w, amax_w, bias, posb, pbias}
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -322,7 +330,7 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 13 * i;
+    const long long* t = table + 16 * i;
     a.L[i].w = (const float*)t[0];
     a.L[i].wf = (bf16_t*)t[1];
     a.L[i].wd = (bf16_t*)t[2];
@@ -335,6 +343,9 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].wf8 = (uint8_t*)t[10];
     a.L[i].s_w = (const float*)t[11];
     a.L[i].amax_w = (unsigned*)t[12];
+    a.L[i].bias = (const float*)t[13];
+    a.L[i].posb = (const float*)t[14];
+    a.L[i].pbias = (bf16_t*)t[15];
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;
   }

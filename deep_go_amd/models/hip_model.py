@@ -153,6 +153,16 @@ class HipGoNet:
             if p.fp8:
                 src = self.x0 if p.index == 0 else self.act[p.index - 1]
                 self.x8[p.index] = torch.zeros(src.numel(), dtype=torch.uint8, device=dev)
+        # forward epilogue bias table (bf16 bias + pos_bias, rebuilt by every weight refresh)
+        # and ReLU bitmasks of the board-kernel outputs consumed by a board dgrad
+        self.pbias = [torch.zeros((NUM_POINTS, p.cout), dtype=torch.bfloat16, device=dev)
+                      if p.board and not p.fp8 else None for p in self.plans]
+        self.relu_mask = [None] * len(self.plans)
+        for p in self.plans[:-1]:
+            nxt = self.plans[p.index + 1]
+            if p.board and nxt.board_d and os.environ.get("DG_RELU_MASK", "1") == "1":
+                self.relu_mask[p.index] = torch.zeros((B, NUM_POINTS, p.cout // 8),
+                                                      dtype=torch.uint8, device=dev)
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
@@ -202,7 +212,10 @@ class HipGoNet:
                          p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd, 0,
                          w8.data_ptr() if w8 is not None else 0,
                          self.fp8_scales.data_ptr() + 8 * p.index if w8 is not None else 0,
-                         self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0])
+                         self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0,
+                         self.params.data_ptr() + 4 * spec.b_off,
+                         self.params.data_ptr() + 4 * spec.pos_off,
+                         self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
     def _build_plans(self):
@@ -231,13 +244,15 @@ class HipGoNet:
                     self.x8[i].data_ptr(), x_pad, p.cinp, self.B, self.act[i].data_ptr(), y8,
                     y_pad, P + spec.b_off * f4, P + spec.pos_off * f4, S + (2 * i - 1) * f4,
                     S + 2 * i * f4, S + (2 * i + 1) * f4,
-                    self.fp8_amax.data_ptr() + i * 4 if y8 else 0)))
+                    self.fp8_amax.data_ptr() + i * 4 if y8 else 0,
+                    self.relu_mask[i].data_ptr() if self.relu_mask[i] is not None else 0)))
             elif p.board:
-                self._fwd.append((h.conv_board, (h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(),
-                                                 p.KP, p.cout, p.Mpad, xin.data_ptr(), x_pad,
-                                                 p.cinp, self.B, self.act[p.index].data_ptr(),
-                                                 y_pad, P + spec.b_off * f4,
-                                                 P + spec.pos_off * f4, 0, 0)))
+                msk = self.relu_mask[p.index]
+                self._fwd.append((h.conv_board_ex, (
+                    h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
+                    xin.data_ptr(), x_pad, p.cinp, self.B, self.act[p.index].data_ptr(), y_pad,
+                    0, 0, self.pbias[p.index].data_ptr(), 0, 0,
+                    msk.data_ptr() if msk is not None else 0)))
             else:
                 self._fwd.append((h.conv_nt, (h.EPI_FWD, p.k, p.bm, p.bn,
                                               self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
@@ -293,11 +308,13 @@ class HipGoNet:
             if i > 0:
                 prev = lay.layers[i - 1]
                 if p.board_d:
-                    ops.append((h.conv_board, (h.EPI_DGRAD, p.k, p.bm_d, self.wd[i].data_ptr(),
-                                               p.KPd, p.cin, p.Mpad_d, self.dz[i].data_ptr(),
-                                               dzp, p.cout, self.B, self.dz[i - 1].data_ptr(),
-                                               max(1, prev.pad), 0, 0,
-                                               self.act[i - 1].data_ptr(), spec.pad)))
+                    msk = self.relu_mask[i - 1]
+                    ops.append((h.conv_board_ex, (
+                        h.EPI_DGRAD, p.k, p.bm_d, self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
+                        self.dz[i].data_ptr(), dzp, p.cout, self.B, self.dz[i - 1].data_ptr(),
+                        max(1, prev.pad), 0, 0, 0,
+                        0 if msk is not None else self.act[i - 1].data_ptr(), spec.pad,
+                        msk.data_ptr() if msk is not None else 0)))
                 else:
                     ops.append((h.conv_nt, (h.EPI_DGRAD, p.k, p.bm_d, p.bn_d,
                                             self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,

@@ -110,7 +110,7 @@ def conv_board_fp8(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: t
     h.conv_board_fp8(k, bm, A8.data_ptr(), KP, cout, Mpad, x8.data_ptr(), pad, cin, B,
                      y.data_ptr(), y8.data_ptr(), 1, bias.float().contiguous().to(dev).data_ptr(),
                      posb.float().contiguous().to(dev).data_ptr(), s_x.data_ptr(),
-                     scales.data_ptr(), s_y.data_ptr(), amax_y.data_ptr(), s)
+                     scales.data_ptr(), s_y.data_ptr(), amax_y.data_ptr(), 0, s)
     y8f = (y8.view(torch.float8_e4m3fn).float() * s_y).reshape(y.shape).to(torch.bfloat16)
     return (LY.from_frame(y, 1, cout), LY.from_frame(y8f, 1, cout), s_y.item(),
             amax_y.view(torch.float32).item())
@@ -262,7 +262,7 @@ def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0,
     wf = torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=w.device)
     wd = torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=w.device) if KPd else None
     tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0,
-                     0, 0, 0]],
+                     0, 0, 0, 0, 0, 0]],
                    dtype=np.int64)
     h.weight_refresh(tbl.ctypes.data, 1, stream_handle())
     torch.cuda.synchronize()

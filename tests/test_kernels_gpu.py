@@ -87,6 +87,47 @@ def test_conv_board_forward(B, cin, cout, k, bm, monkeypatch):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("bm", [64, 128])
+def test_conv_board_pbias_and_relu_mask(bm):
+    """Forward with the combined bf16 bias table writes the ReLU bitmask; dgrad gated by the
+    bitmask equals dgrad gated by the activation frame."""
+    torch.manual_seed(9)
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    B, C, k = 3, 128, 3
+    x = bf(torch.relu(torch.randn(B, C, 19, 19, device=DEV)))
+    w = bf(torch.randn(C, k, k, C, device=DEV) / (k * C ** 0.5))
+    b = torch.randn(C, device=DEV) * 0.1
+    pb = torch.randn(361, C, device=DEV) * 0.1
+    KP, _, Mpad = LY.conv_dims(k, C, C, bm)
+    A = LY.fwd_weight(w.float(), C, KP, Mpad)
+    xf = LY.to_frame(x, 1, C)
+    y = LY.alloc_frame(B, C, 1, DEV)
+    pbias = (b.view(1, C) + pb).to(torch.bfloat16).contiguous()
+    mask = torch.zeros(B, 361, C // 8, dtype=torch.uint8, device=DEV)
+    s = stream_handle()
+    h.conv_board_ex(h.EPI_FWD, k, bm, A.data_ptr(), KP, C, Mpad, xf.data_ptr(), 1, C, B,
+                    y.data_ptr(), 1, 0, 0, pbias.data_ptr(), 0, 0, mask.data_ptr(), s)
+    yv = LY.from_frame(y, 1, C)
+    ref = F.relu(conv_ref(x, w, k) + pbias.float().t().reshape(1, C, 19, 19))
+    assert rel_err(yv, ref) < 1e-2
+    bits = torch.stack([(mask >> e) & 1 for e in range(8)], -1).reshape(B, 361, C)
+    assert torch.equal(bits.bool(), (yv > 0).reshape(B, C, 361).transpose(1, 2))
+    # dgrad: mask vs aux frame
+    dz = bf(torch.randn(B, C, 19, 19, device=DEV))
+    Ad = LY.dgrad_weight(w.float(), KP, Mpad)
+    dzf = LY.to_frame(dz, 1)
+    o1 = LY.alloc_frame(B, C, 1, DEV)
+    o2 = LY.alloc_frame(B, C, 1, DEV)
+    h.conv_board_ex(h.EPI_DGRAD, k, bm, Ad.data_ptr(), KP, C, Mpad, dzf.data_ptr(), 1, C, B,
+                    o1.data_ptr(), 1, 0, 0, 0, y.data_ptr(), 1, 0, s)
+    h.conv_board_ex(h.EPI_DGRAD, k, bm, Ad.data_ptr(), KP, C, Mpad, dzf.data_ptr(), 1, C, B,
+                    o2.data_ptr(), 1, 0, 0, 0, 0, 1, mask.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+
+
 @pytest.mark.parametrize("B,cin,cout,k,bm", [(3, 128, 128, 3, 64), (2, 256, 128, 3, 64),
                                              (2, 128, 256, 3, 128), (2, 128, 64, 1, 64)])
 def test_conv_board_fp8_forward(B, cin, cout, k, bm):

@@ -4,10 +4,10 @@
 # (GPU ASan / XNACK are not available on the MI355X pool).
 set -e -o pipefail
 cd "$(dirname "$0")/.."
-mkdir -p build/sanitize
+OUTDIR=${TMPDIR:-/tmp}/dg_sanitize; mkdir -p $OUTDIR
 SRC="csrc/engine/tests/stress_main.cpp csrc/engine/loader.cpp csrc/engine/go_engine.cpp csrc/engine/features.cpp csrc/engine/t7.cpp csrc/engine/sgf.cpp"
 for SAN in thread address,undefined; do
-  OUT=build/sanitize/stress_${SAN//,/_}
+  OUT=$OUTDIR/stress_${SAN//,/_}
   g++ -std=c++17 -O1 -g -pthread -fno-omit-frame-pointer -fsanitize=$SAN $SRC -o $OUT
   echo "== -fsanitize=$SAN"
   TSAN_OPTIONS="halt_on_error=1" ASAN_OPTIONS="detect_leaks=1:halt_on_error=1" \
