@@ -23,6 +23,8 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          const float* bias, const float* posb, const void* aux, int aux_pad,
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
+hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
+                             hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
                             const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
                             const float* bias, const float* posb, const void* pbias,
@@ -123,6 +125,11 @@ PYBIND11_MODULE(_dghip, m) {
                 "conv_board_ex");
         },
         "conv_board + optional bf16 bias table (fwd) and ReLU bitmask (fwd writes, dgrad reads)");
+  m.def("conv_stack_fwd", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                             uintptr_t stream) {
+    check(dg_conv_stack_fwd(P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
+          "conv_stack_fwd");
+  }, "fused forward of a run of 128->128 3x3 layers, board resident in LDS");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
                          int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {

@@ -266,6 +266,7 @@ class HipGoNet:
                     self.act[i].data_ptr(), self.x8[i + 1].data_ptr(), self.act[i].numel(),
                     self.fp8_scales.data_ptr() + (2 * i + 1) * 4,
                     self.fp8_amax.data_ptr() + i * 4)))
+        self._fuse_forward_stack()
         hd = self.head
         hx = self.act[-1]
         self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
@@ -322,6 +323,42 @@ class HipGoNet:
                                             self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
                                             self.act[i - 1].data_ptr(), spec.pad)))
             self._bwd.append(ops)
+
+    def _fuse_forward_stack(self):
+        """Replace the per-layer forward launches of the longest run of hidden 128->128 3x3
+        bf16 layers by ONE conv_stack_fwd launch (board-resident activations, overlapped
+        stores; csrc/kernels/conv_stack.hip).  DG_STACK=0 keeps per-layer kernels."""
+        self.stack = []
+        if os.environ.get("DG_STACK", "1") == "0":
+            return
+        L = self.layout.layers
+
+        def ok(p):
+            return (p.index > 0 and p.board and not p.fp8 and p.k == 3 and p.cinp == 128
+                    and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1)
+        best, cur = [], []
+        for p in self.plans:
+            cur = cur + [p.index] if ok(p) else []
+            if len(cur) > len(best):
+                best = list(cur)
+        if len(best) < 2:
+            return
+        self.stack = best
+        rows = []
+        for i in best:
+            m = self.relu_mask[i]
+            rows.append([self.wf[i].data_ptr(), self.pbias[i].data_ptr(), self.act[i].data_ptr(),
+                         m.data_ptr() if m is not None else 0])
+        self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+        first = best[0]
+        op = (self.h.conv_stack_fwd, (self._stack_table.ctypes.data, len(best),
+                                      self.act[first - 1].data_ptr(), self.plans[first].KP,
+                                      self.B))
+        if len(self._fwd) != len(self.plans):  # fp8 quantize ops interleaved: keep per-layer
+            self.stack = []
+            return
+        # self._fwd holds exactly one launch per plan here
+        self._fwd = self._fwd[:first] + [op] + self._fwd[best[-1] + 1:]
 
     # ------------------------------------------------------------------ execution
     @staticmethod

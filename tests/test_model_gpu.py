@@ -109,6 +109,28 @@ def test_side_stream_backward_matches_single_stream(layers, ch, B, monkeypatch):
     assert torch.allclose(net1.grads, g0, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("layers", [4, 6])
+def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
+    """conv_stack_fwd (board-resident multi-layer forward) computes the per-layer board
+    kernels' exact MFMA sequence: activations, masks and loss are bit-identical."""
+    monkeypatch.setenv("DG_STACK", "0")
+    _, n0, _ = _setup(layers, 128, 5, seed=6)
+    monkeypatch.setenv("DG_STACK", "1")
+    _, n1, _ = _setup(layers, 128, 5, seed=6)
+    assert len(n1.stack) == layers - 2 and not n0.stack
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    for a0, a1 in zip(n0.act, n1.act):
+        assert torch.equal(a0, a1)
+    for m0, m1 in zip(n0.relu_mask, n1.relu_mask):
+        if m0 is not None:
+            assert torch.equal(m0, m1)
+    assert torch.equal(n0.loss, n1.loss)
+    # (head_reduce folds board partials with atomics: last-bit order effects only)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
+
+
 def test_lr_decay_fused_into_weight_refresh():
     """lr_t = lr0 * (1 - decay)^t (optimizer.lua:25-26), applied by the refresh launch."""
     cfg, net, data = _setup(3, 64, 4, rateDecay=1e-3)

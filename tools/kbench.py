@@ -70,8 +70,9 @@ def main():
             for en, e in (("fwd", h.EPI_FWD), ("dgrad", h.EPI_DGRAD)):
                 res.setdefault(f"board{bm}_{en}", []).append(
                     round(timeit(lambda: board(bm, e)), 2))
-        h.conv_board_set_ablate(8)
-        res.setdefault("board64_fwd_noepi", []).append(round(timeit(lambda: board(64)), 2))
+        for mode in (1, 2, 4, 8, 14, 16, 6, 12):
+            h.conv_board_set_ablate(mode)
+            res.setdefault(f"board64_fwd_ablate{mode}", []).append(round(timeit(lambda: board(64)), 2))
         h.conv_board_set_ablate(0)
         for bm, bn in ((128, 128), (128, 192)):
             res.setdefault(f"nt_{bm}x{bn}", []).append(round(timeit(nt(bm, bn)), 2))
