@@ -61,7 +61,8 @@ hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* 
                    float* unused, float* dzb, int head_relu, float grad_scale,
                    hipStream_t stream);
 hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, const uint8_t* rank,
-                              void* out, int B, int pad, int CP, hipStream_t s);
+                              void* out, int B, int pad, int CP, void* out2, int CP2,
+                              hipStream_t s);
 hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* part,
                                 hipStream_t s);
 int dg_bias_chunks(int B);
@@ -201,9 +202,15 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("expand_features", [](uintptr_t planes, uintptr_t player, uintptr_t rank, uintptr_t out,
                               int B, int pad, int CP, uintptr_t stream) {
     check(dg_expand_features(P<uint8_t>(planes), P<uint8_t>(player), P<uint8_t>(rank),
-                             P<void>(out), B, pad, CP, S(stream)),
+                             P<void>(out), B, pad, CP, nullptr, 0, S(stream)),
           "expand_features");
   });
+  m.def("expand_features2", [](uintptr_t planes, uintptr_t player, uintptr_t rank, uintptr_t out,
+                               int B, int pad, int CP, uintptr_t out2, int CP2, uintptr_t stream) {
+    check(dg_expand_features(P<uint8_t>(planes), P<uint8_t>(player), P<uint8_t>(rank),
+                             P<void>(out), B, pad, CP, P<void>(out2), CP2, S(stream)),
+          "expand_features2");
+  }, "expand into the CP-channel frame and a second CP2-channel copy (board-tiled layer 1)");
   m.def("bias_grad_partial", [](uintptr_t dZ, int B, int C, int pad, uintptr_t part,
                                 uintptr_t stream) {
     check(dg_bias_grad_partial(P<void>(dZ), B, C, pad, P<float>(part), S(stream)),

@@ -321,9 +321,8 @@ void allow_lds(K kernel, size_t bytes) {
   }
 }
 
-template <int KW, int WM, int EPI>
-hipError_t launch(const BoardArgs& a, int B, int Mpad, hipStream_t s) {
-  constexpr int HB = WM == 1 ? 1 : 2;
+template <int KW, int WM, int EPI, int HB>
+hipError_t launch_hb(const BoardArgs& a, int B, int Mpad, hipStream_t s) {
   const int F = 19 + 2 * a.x_pad;
   const int hrows = (F * F + 63) / 64 * 64;
   size_t lds = 2 * (size_t)(64 * WM * 128) + HB * (size_t)hrows * 128;
@@ -334,6 +333,14 @@ hipError_t launch(const BoardArgs& a, int B, int Mpad, hipStream_t s) {
   hipLaunchKernelGGL((conv_board_kernel<KW, WM, EPI, HB>), dim3(B, Mpad / (64 * WM)), dim3(512),
                      lds, s, a);
   return hipGetLastError();
+}
+
+// HB = 1 (single halo image) at BM = 64 (two workgroups per CU) and whenever the input has a
+// single 64-channel chunk (nothing to double-buffer); else HB = 2.
+template <int KW, int WM, int EPI>
+hipError_t launch(const BoardArgs& a, int B, int Mpad, hipStream_t s) {
+  if (WM == 1 || a.x_C == 64) return launch_hb<KW, WM, EPI, 1>(a, B, Mpad, s);
+  return launch_hb<KW, WM, EPI, 2>(a, B, Mpad, s);
 }
 
 template <int KW, int WM>
@@ -371,6 +378,8 @@ extern "C" hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, i
                            : dispatch_epi<1, 1>(epi, a, B, Mpad, stream);
     case 3: return wm == 2 ? dispatch_epi<3, 2>(epi, a, B, Mpad, stream)
                            : dispatch_epi<3, 1>(epi, a, B, Mpad, stream);
+    case 5: return wm == 2 ? dispatch_epi<5, 2>(epi, a, B, Mpad, stream)
+                           : dispatch_epi<5, 1>(epi, a, B, Mpad, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -16,7 +16,8 @@ namespace {
 __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
                                        const uint8_t* __restrict__ player,
                                        const uint8_t* __restrict__ rank, char* __restrict__ out,
-                                       int B, int pad, int CP) {
+                                       int B, int pad, int CP, char* __restrict__ out2,
+                                       int CP2) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * NPTS) return;
   const int b = idx / NPTS;
@@ -55,6 +56,9 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
   for (int r = 1; r <= 9; ++r) v[27 + r] = (rk == r);
   const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
   char* dst = out + frame_off(b, h, w, pad, CP);
+  // optional second frame with CP2 (64) channels for the board-tiled first layer; its
+  // channels >= CP are never written (zero from allocation)
+  char* dst2 = out2 ? out2 + frame_off(b, h, w, pad, CP2) : nullptr;
 #pragma unroll
   for (int c = 0; c < 48; c += 8) {
     if (c >= CP) break;
@@ -64,6 +68,7 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
     o.z = pack_bf16x2(v[c + 4], v[c + 5]);
     o.w = pack_bf16x2(v[c + 6], v[c + 7]);
     *(uint4*)(dst + c * 2) = o;
+    if (dst2) *(uint4*)(dst2 + c * 2) = o;
   }
 }
 
@@ -271,11 +276,13 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
 extern "C" {
 
 hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, const uint8_t* rank,
-                              void* out, int B, int pad, int CP, hipStream_t s) {
+                              void* out, int B, int pad, int CP, void* out2, int CP2,
+                              hipStream_t s) {
   if (CP % 8 != 0 || CP < 40 || CP > 48) return hipErrorInvalidValue;
+  if (out2 && (CP2 % 8 != 0 || CP2 < CP)) return hipErrorInvalidValue;
   const int n = B * NPTS;
   hipLaunchKernelGGL(expand_features_kernel, dim3((n + 255) / 256), dim3(256), 0, s, planes,
-                     player, rank, (char*)out, B, pad, CP);
+                     player, rank, (char*)out, B, pad, CP, (char*)out2, CP2);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ class ConvPlan:
     board_d: bool = False  # dgrad uses the board-tiled kernel
     wgrad3: bool = False   # wgrad uses the row-stripe kernel (conv_wgrad3.hip)
     fp8: bool = False      # forward on the e4m3 MX-MFMA kernel (conv_fp8.hip)
+    cinp_f: int = 0        # forward input-frame channels if != cinp (board-tiled layer 1: 64)
 
 
 class HipGoNet:
@@ -108,9 +109,18 @@ class HipGoNet:
             cinp = INPUT_CP if spec.index == 0 else spec.cin
             board = LY.board_ok(spec.k, cinp)
             bm, bn = LY.pick_tiles(npix, spec.cout, num_cus)
+            cinp_f = 0
             if board:
                 bm = LY.board_bm(spec.cout)
-            KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
+            elif (spec.index == 0 and spec.k in (1, 3, 5) and spec.pad <= 2
+                  and os.environ.get("DG_L1_BOARD", "0") == "1"):
+                # first layer on the board kernel: the expansion kernel also writes a
+                # 64-channel copy of the input frame (channels >= 37 zero); the wgrad keeps
+                # the 40-channel frame (60% less K).  BM 128: one 1-round grid of 256 boards.
+                board, cinp_f, bm = True, 64, 128
+            KP, KPw, Mpad = LY.conv_dims(spec.k, cinp_f or cinp, spec.cout, bm)
+            if cinp_f:
+                _, KPw, _ = LY.conv_dims(spec.k, cinp, spec.cout, bm)
             Mpad_w = LY.round_up(spec.cout, 128)
             w3 = LY.wgrad3_ok(spec.k, cinp, spec.pad) and os.environ.get("DG_WGRAD3", "0") == "1"
             if w3:
@@ -119,7 +129,7 @@ class HipGoNet:
             else:
                 splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
-                         Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3)
+                         Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3, cinp_f=cinp_f)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
             if spec.index > 0:
                 bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
@@ -141,6 +151,8 @@ class HipGoNet:
         B = batch
         pads = [s.pad for s in L]
         self.x0 = LY.alloc_frame(B, INPUT_CP, pads[0], dev)
+        self.x0b = (LY.alloc_frame(B, self.plans[0].cinp_f, pads[0], dev)
+                    if self.plans[0].cinp_f else None)
         # act[i]: output of layer i, framed with the pad of layer i+1
         self.act = [LY.alloc_frame(B, L[i].cout, pads[i + 1], dev) for i in range(self.L - 1)]
         # dz[i]: d loss / d pre-activation of layer i, framed with layer i's pad (>=1)
@@ -209,7 +221,7 @@ class HipGoNet:
             w = self.params[spec.w_off:spec.w_off + spec.w_numel]
             w8 = self.wf8[p.index]
             rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0,
-                         p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd, 0,
+                         p.cout, p.cin, p.k * p.k, p.cinp_f or p.cinp, p.KP, p.KPd, 0,
                          w8.data_ptr() if w8 is not None else 0,
                          self.fp8_scales.data_ptr() + 8 * p.index if w8 is not None else 0,
                          self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0,
@@ -226,9 +238,15 @@ class HipGoNet:
         self._pre: List[Tuple[Callable, tuple]] = []
         self._fwd: List[Tuple[Callable, tuple]] = []
         self._bwd: List[List[Tuple[Callable, tuple]]] = []  # per layer (index order)
-        self._pre.append((h.expand_features, (self.planes.data_ptr(), self.player.data_ptr(),
-                                              self.rank.data_ptr(), self.x0.data_ptr(), self.B,
-                                              self.plans[0].pad, INPUT_CP)))
+        if self.x0b is not None:
+            self._pre.append((h.expand_features2, (
+                self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
+                self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP, self.x0b.data_ptr(),
+                self.plans[0].cinp_f)))
+        else:
+            self._pre.append((h.expand_features, (
+                self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
+                self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP)))
         for p in self.plans:
             spec = lay.layers[p.index]
             xin = self.x0 if p.index == 0 else self.act[p.index - 1]
@@ -248,9 +266,12 @@ class HipGoNet:
                     self.relu_mask[i].data_ptr() if self.relu_mask[i] is not None else 0)))
             elif p.board:
                 msk = self.relu_mask[p.index]
+                if p.cinp_f:
+                    xin = self.x0b
                 self._fwd.append((h.conv_board_ex, (
                     h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
-                    xin.data_ptr(), x_pad, p.cinp, self.B, self.act[p.index].data_ptr(), y_pad,
+                    xin.data_ptr(), x_pad, p.cinp_f or p.cinp, self.B,
+                    self.act[p.index].data_ptr(), y_pad,
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
                     msk.data_ptr() if msk is not None else 0)))
             else:

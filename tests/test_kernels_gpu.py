@@ -70,7 +70,8 @@ def test_conv_dgrad(B, cin, cout, k):
 
 
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 64, 64, 3), (5, 128, 128, 3), (2, 256, 256, 3),
-                                          (3, 128, 64, 3), (2, 64, 128, 1), (1, 192, 128, 3)])
+                                          (3, 128, 64, 3), (2, 64, 128, 1), (1, 192, 128, 3),
+                                          (2, 64, 128, 5)])
 @pytest.mark.parametrize("bm", ["64", "128"])
 def test_conv_board_forward(B, cin, cout, k, bm, monkeypatch):
     monkeypatch.setenv("DG_BOARD_BM", bm)  # 64: single halo / 2 WGs per CU; 128: double halo

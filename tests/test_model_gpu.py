@@ -131,6 +131,20 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
+def test_board_tiled_first_layer_option(monkeypatch):
+    """DG_L1_BOARD=1: 5x5 first layer on the board kernel over a 64-channel input copy
+    (measured slower than the pixel-tiled kernel at K 1600 vs 1000; kept as an option)."""
+    monkeypatch.setenv("DG_L1_BOARD", "1")
+    _, net, data = _setup(3, 64, 5)
+    assert net.plans[0].board and net.plans[0].cinp_f == 64
+    net.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, _, g_ref = _oracle(net, data)
+    assert abs(net.mean_loss().item() - loss_ref) < 2e-2 * max(1.0, abs(loss_ref))
+    err = (net.grads.cpu() - g_ref).norm() / g_ref.norm()
+    assert err < 0.08
+
+
 def test_lr_decay_fused_into_weight_refresh():
     """lr_t = lr0 * (1 - decay)^t (optimizer.lua:25-26), applied by the refresh launch."""
     cfg, net, data = _setup(3, 64, 4, rateDecay=1e-3)
