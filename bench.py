@@ -42,6 +42,9 @@ def main():
                     help="after the timed run, N extra steps with roctx ranges (load / segments"
                          " / allreduce / optimizer) and a host phase breakdown; run under "
                          "rocprofv3 --marker-trace --kernel-trace to see them on the timeline")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="use the DP path (RCCL process group, bucketed all-reduces between "
+                         "graph segments) even on 1 GPU: measures its overhead")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
     args = ap.parse_args()
@@ -55,6 +58,15 @@ def main():
 
     info = dp.init_distributed()
     world = info.world
+    if args.force_dp and world == 1 and not torch.distributed.is_initialized():
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(sk.getsockname()[1]))
+        sk.close()
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1,
+                                             device_id=torch.device("cuda", 0))
     if world > 1:
         torch.cuda.set_device(info.local_rank)
     dev = torch.device("cuda", info.local_rank if world > 1 else 0)
@@ -80,7 +92,7 @@ def main():
         net.set_batch_packed(pool[i % args.pool])
 
     bucketer = None
-    if world > 1:
+    if world > 1 or args.force_dp:
         lay = net.layout
         ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
         buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20))
@@ -147,7 +159,7 @@ def main():
             "graphs": not args.no_graph,
             **({"profile_host_ms_per_step": phases} if phases else {}),
         }), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -30,6 +30,8 @@ hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int 
                             const float* bias, const float* posb, const void* pbias,
                             const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
+void dg_conv_wgrad_set_ring(int on);
+int dg_conv_wgrad_wgs_per_cu();
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
@@ -249,6 +251,9 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
+  m.def("conv_wgrad_set_ring", [](int on) { dg_conv_wgrad_set_ring(on); },
+        "1: 32-pixel 3-stage ring wgrad for 3x3/5x5 (3 workgroups per CU); 0: 64-pixel 2-stage");
+  m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
   m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });

@@ -39,22 +39,6 @@ constexpr int NSUB = (NPTS + PSTEP - 1) / PSTEP;  // 6
 
 DG_DEV int div19(int p) { return (p * 3450) >> 16; }  // exact for 0 <= p < 400
 
-// LDS-DMA issued from inline asm: the compiler's waitcnt pass does not see it, so it
-// neither waits for it in front of later LDS reads nor before barriers.  The kernel
-// accounts for it by hand: every wave issues exactly DMA_PER_STEP per K-step and waits
-// with s_waitcnt vmcnt(DMA_PER_STEP) — the newest stage stays in flight.
-DG_DEV void dma16(const void* gsrc, uint32_t lds_wave_base) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               :
-               : "s"(lds_wave_base), "v"(gsrc)
-               : "memory", "m0");
-}
-template <int N>
-DG_DEV void wait_vmcnt() {
-  static_assert(N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
 struct W3Args {
   const char* dZ;  // gradient frame [B][Fz][Fz][M] bf16
   const char* X;   // input frame [B][F][F][x_C] bf16
@@ -234,7 +218,7 @@ conv_wgrad3_kernel(W3Args a) {
   Geo cur = geo(st_begin);
   if (nst > 0) stage(0, cur);
   if (LOOK == 2 && nst > 1) stage(1, geo(st_begin + 1));
-  if (LOOK == 2 && nst > 1) wait_vmcnt<DMA_PER_STEP>(); else wait_vmcnt<0>();
+  if (LOOK == 2 && nst > 1) dma_wait<DMA_PER_STEP>(); else dma_wait<0>();
   __builtin_amdgcn_s_barrier();
   for (int st = st_begin; st < st_end; ++st) {
     const int ls = st - st_begin;
@@ -317,7 +301,7 @@ conv_wgrad3_kernel(W3Args a) {
     __builtin_amdgcn_sched_barrier(0);  // DMA wait + barrier stay below the MFMAs
     // stage ls+1 must have landed (every wave's part) before anyone reads it; stage ls+2
     // (issued this step) stays in flight
-    if (LOOK == 2 && more) wait_vmcnt<DMA_PER_STEP>(); else wait_vmcnt<0>();
+    if (LOOK == 2 && more) dma_wait<DMA_PER_STEP>(); else dma_wait<0>();
     __builtin_amdgcn_s_barrier();
     if (ls + 1 < nst) cur = geo(st + 1);
   }

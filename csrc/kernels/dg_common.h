@@ -36,6 +36,23 @@ DG_DEV void glds16(const void* gsrc, LDS_AS void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(gsrc, lds_wave_base, 16, 0, 0);
 }
 
+// LDS-DMA issued from inline asm: the compiler's waitcnt pass does not see it, so it neither
+// waits for it in front of later LDS reads (it cannot tell transposing-read addresses from
+// the DMA destination) nor before barriers.  Kernels using it count their own DMA
+// instructions per stage and wait with dma_wait<N>() = s_waitcnt vmcnt(N) (newest stages in
+// flight).  lds_wave_base must be wave-uniform (SGPR); each lane lands 16 B at base+lane*16.
+DG_DEV void dma16(const void* gsrc, uint32_t lds_wave_base) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :
+               : "s"(lds_wave_base), "v"(gsrc)
+               : "memory", "m0");
+}
+template <int N>
+DG_DEV void dma_wait() {
+  static_assert(N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 DG_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

@@ -127,7 +127,8 @@ class HipGoNet:
                 splits = LY.pick_wgrad3_splits(batch, self.h.wgrad3_tiles(Mpad_w, cinp),
                                                 self.h.wgrad3_wgs_per_cu(cinp), num_cus)
             else:
-                splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus)
+                splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
+                                               self.h.conv_wgrad_wgs_per_cu())
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
                          Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3, cinp_f=cinp_f)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))

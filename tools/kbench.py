@@ -78,16 +78,28 @@ def main():
             res.setdefault(f"nt_{bm}x{bn}", []).append(round(timeit(nt(bm, bn)), 2))
         dz = LY.alloc_frame(B, C, 1, dev)
         LY.frame_interior(dz, 1).copy_(torch.randn(B, 19, 19, C, device=dev))
-        splits = LY.pick_wgrad_splits(B * 361, KPw, 128)
+        h.conv_wgrad_set_ring(0)
+        splits = LY.pick_wgrad_splits(B * 361, KPw, 128, wgs_per_cu=2)
         slab = torch.empty(splits * 128 * KPw, device=dev)
 
         def wg():
             h.conv_wgrad(3, dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, splits,
                          slab.data_ptr(), s)
-        for mode in (0, 1, 2, 4, 8, 7, 15, 14, 30, 6, 3):
+        h.conv_wgrad_set_ring(0)
+        for mode in (0, 4, 6):
             h.conv_wgrad_set_ablate(mode)
             res.setdefault(f"wgrad_ablate{mode}", []).append(round(timeit(wg), 2))
         h.conv_wgrad_set_ablate(0)
+        h.conv_wgrad_set_ring(1)
+        spr = LY.pick_wgrad_splits(B * 361, KPw, 128, wgs_per_cu=3)
+        slabr = torch.empty(spr * 128 * KPw, device=dev)
+
+        def wgr():
+            h.conv_wgrad(3, dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, spr,
+                         slabr.data_ptr(), s)
+        res.setdefault("wgrad_ring", []).append(round(timeit(wgr), 2))
+        res.setdefault("splits_ring", []).append(spr)
+        h.conv_wgrad_set_ring(0)
         res.setdefault("splits", []).append(splits)
         gw = torch.empty(C * 9 * C, device=dev)
 
