@@ -82,7 +82,7 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
 // (sum over chunks -> gposb, gbias) runs inside the wgrad slab-reduce launch.
 // Reference: nn.Add / conv bias backward (experiments.lua:138,144).
 constexpr int BG_BT = 16;
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
                          float* __restrict__ part, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
@@ -96,7 +96,9 @@ bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
   const size_t board_stride = (size_t)F * F * C * 2;
   const char* row0 = dZ + ((size_t)((h + pad) * F + pad) * C) * 2;
   float* prow = part + ((size_t)chunk * NPTS + h * BOARD) * C;
-  for (int it = tid; it < items; it += 256) {
+  // blockDim covers all 19*C/8 items of the row in ONE pass (the 256-thread version ran a
+  // second pass on 48 threads whose load latency the whole workgroup waited for)
+  for (int it = tid; it < items; it += blockDim.x) {
     const int w = it / G, g = it - (it / G) * G;
     const char* src = row0 + ((size_t)w * C + g * 8) * 2;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -124,7 +126,7 @@ bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
   }
   __syncthreads();
   float* rowpart = part + (size_t)nchunks * NPTS * C + ((size_t)chunk * BOARD + h) * C;
-  for (int c = tid; c < C; c += 256) {
+  for (int c = tid; c < C; c += blockDim.x) {
     float sc = 0.f;
     for (int w = 0; w < BOARD; ++w) sc += s_row[w * C + c];
     rowpart[c] = sc;
@@ -291,7 +293,10 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
                                 hipStream_t s) {
   if (C % 8 != 0 || C > 2048) return hipErrorInvalidValue;
   const int nchunks = (B + BG_BT - 1) / BG_BT;
-  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks), dim3(256),
+  int threads = (BOARD * (C / 8) + 63) / 64 * 64;  // one item per thread (19*C/8)
+  if (threads > 1024) threads = 1024;
+  if (threads < 64) threads = 64;
+  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, (const char*)dZ, B, C, pad, part,
                      nchunks);
   return hipGetLastError();

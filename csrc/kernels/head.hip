@@ -130,15 +130,19 @@ __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
       float acc = 0.f;
       if (p < NPTS && lane < lanes_used) {
         const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+        // four independent accumulation chains (one serial chain of 4T dot2 was latency
+        // bound at 2 waves per SIMD)
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           const int f = (h + a.x_pad + t / KW - R) * F + (w + a.x_pad + t % KW - R);
           const uint4 xv = *(const uint4*)(s_x + (f * cc + lg * 8) * 2);
-          acc = dot2(xv.x, wp[t][0], acc);
-          acc = dot2(xv.y, wp[t][1], acc);
-          acc = dot2(xv.z, wp[t][2], acc);
-          acc = dot2(xv.w, wp[t][3], acc);
+          a0 = dot2(xv.x, wp[t][0], a0);
+          a1 = dot2(xv.y, wp[t][1], a1);
+          a2 = dot2(xv.z, wp[t][2], a2);
+          a3 = dot2(xv.w, wp[t][3], a3);
         }
+        acc = (a0 + a1) + (a2 + a3);
       }
       // reduce over the gcc lanes of this pixel
       for (int o = gcc / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -299,45 +303,79 @@ __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
   }
 }
 
-// Deterministic-order batch reduction of the head's per-board partials:
-//   gposb[p] = sum_b dzb[b][p], gbias = sum_p gposb[p], gw[i] = sum_b gw_part[b][i].
-// grid.x covers the n weight columns then the 361 position columns; grid.y = chunks of
-// 32 boards whose partial sums are combined with (8-way, low contention) float atomics.
-constexpr int HR_BT = 32;
-__global__ void __launch_bounds__(256)
+// Deterministic batch reduction of the head's per-board partials (plain stores: the
+// step needs no gradient zeroing):
+//   gw[j]    = sum_b gw_part[b][j]        (j < n = KW*KW*C)
+//   gposb[p] = sum_b dzb[b][p]
+//   gbias    = sum_b sum_p dzb[b][p]      (one dedicated workgroup)
+// Workgroup = 64 outputs x 16 board groups (1024 threads): each thread issues all loads of
+// its board group (<= 16 boards for B = 256) before summing; the 16 group sums are combined
+// in LDS in a fixed order.
+constexpr int HR_G = 16;
+__global__ void __launch_bounds__(1024)
 head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_part, int B, int n,
                    float* __restrict__ gw, float* __restrict__ gbias, float* __restrict__ gposb) {
-  __shared__ float s_red[256];
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int b0 = blockIdx.y * HR_BT;
-  const int b1 = min(B, b0 + HR_BT);
-  float s = 0.f;
-  bool pos = false;
-  if (j < n) {
-    for (int b = b0; b < b1; ++b) s += gw_part[(size_t)b * n + j];
-    atomicAdd(gw + j, s);
-  } else if (j - n < NPTS) {
-    const int p = j - n;
-    for (int b = b0; b < b1; ++b) s += dzb[(size_t)b * NPTS + p];
-    atomicAdd(gposb + p, s);
-    pos = true;
-  }
-  s_red[threadIdx.x] = pos ? s : 0.f;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) s_red[threadIdx.x] += s_red[threadIdx.x + o];
+  __shared__ float s_red[HR_G][64];
+  const int nout = n + NPTS;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x * 64 >= nout) {  // last workgroup: gbias
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    const int tot = B * NPTS;
+    int e = tid;
+    for (; e + 3072 < tot; e += 4096) {
+      a0 += dzb[e];
+      a1 += dzb[e + 1024];
+      a2 += dzb[e + 2048];
+      a3 += dzb[e + 3072];
+    }
+    for (; e < tot; e += 1024) a0 += dzb[e];
+    const float v = wave_sum((a0 + a1) + (a2 + a3));
+    if ((tid & 63) == 0) s_red[0][tid >> 6] = v;
     __syncthreads();
+    if (tid == 0) {
+      float t = 0.f;
+      for (int w = 0; w < 16; ++w) t += s_red[0][w];
+      *gbias = t;
+    }
+    return;
   }
-  if (threadIdx.x == 0 && (blockIdx.x + 1) * 256 > n) atomicAdd(gbias, s_red[0]);
+  const int o = blockIdx.x * 64 + (tid & 63);
+  const int grp = tid >> 6;
+  const bool is_w = o < n;
+  const float* src = is_w ? gw_part + o : dzb + (o - n);
+  const size_t stride = is_w ? (size_t)n : (size_t)NPTS;
+  const int per = (B + HR_G - 1) / HR_G;
+  const int b0 = grp * per, b1 = min(B, b0 + per);
+  float acc = 0.f;
+  if (o < nout) {
+    int b = b0;
+    for (; b + 16 <= b1; b += 16) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = src[(size_t)(b + k) * stride];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc += v[k];
+    }
+    for (; b < b1; ++b) acc += src[(size_t)b * stride];
+  }
+  s_red[grp][tid & 63] = acc;
+  __syncthreads();
+  if (grp == 0 && o < nout) {
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < HR_G; ++g) v += s_red[g][tid];
+    if (is_w) gw[o] = v;
+    else gposb[o - n] = v;
+  }
 }
 
 }  // namespace
 
 extern "C" hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n,
                                      float* gw, float* gbias, float* gposb, hipStream_t stream) {
-  dim3 grid((n + NPTS + 255) / 256, (B + HR_BT - 1) / HR_BT);
-  hipLaunchKernelGGL(head_reduce_kernel, grid, dim3(256), 0, stream, dzb, gw_part, B, n, gw,
-                     gbias, gposb);
+  const int blocks = (n + NPTS + 63) / 64 + 1;  // + the gbias workgroup
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(blocks), dim3(1024), 0, stream, dzb, gw_part, B, n,
+                     gw, gbias, gposb);
   return hipGetLastError();
 }
 

@@ -413,7 +413,8 @@ class HipGoNet:
         """Loss/pred into self.loss/self.pred; gradients (mean over global batch) in
         self.grads.  Registered grad hooks fire right after their layer's wgrad."""
         s = stream_handle()
-        self.grads.zero_()
+        # (no gradient zeroing: every gradient entry is written — not accumulated — by the
+        # slab reduces and the deterministic head reduce)
         self._run(self._pre, s)
         self._run(self._fwd, s)
         f, a = self._head_train
@@ -612,7 +613,6 @@ class SegmentedStep:
         def emit(fn):
             cur.append(fn)
 
-        emit(lambda: net.grads.zero_())
         emit(lambda: net._run(net._pre, stream_handle()))
         emit(lambda: net._run(net._fwd, stream_handle()))
         emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))

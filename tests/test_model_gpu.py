@@ -52,6 +52,22 @@ def test_model_matches_oracle(layers, ch, B):
         assert err < 0.08, (name, err.item())
 
 
+def test_every_gradient_is_written_each_step():
+    """The step does not zero the gradient buffer: all entries must be (over)written."""
+    cfg, net, data = _setup(4, 64, 5)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    g0 = net.grads.clone()
+    # poison every real gradient entry (the alignment padding between tensors is zero from
+    # allocation and never touched)
+    for _, off, n in net.layout.tensor_ranges():
+        net.grads[off:off + n] = float("nan")
+    net.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(net.grads).all()
+    assert torch.allclose(net.grads, g0, rtol=1e-5, atol=1e-8)
+
+
 def test_graph_replay_matches_eager():
     from deep_go_amd.models.hip_model import SegmentedStep
     cfg, net, data = _setup(4, 64, 6)
