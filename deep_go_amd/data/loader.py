@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from ..ops.native import cpu
+from .batch import packed_batch_bytes, unpack_views
 from .dataset import GameIndex, PackedDataset
 
 
@@ -26,12 +27,17 @@ class BatchLoader:
         self.prefetch = prefetch
         pin = torch.cuda.is_available() if pin is None else pin
         B = batch
-        self.planes = torch.zeros((prefetch, B, 9, 19, 19), dtype=torch.uint8, pin_memory=pin)
-        self.player = torch.zeros((prefetch, B), dtype=torch.uint8, pin_memory=pin)
-        self.rank = torch.zeros((prefetch, B), dtype=torch.uint8, pin_memory=pin)
-        self.label = torch.zeros((prefetch, B), dtype=torch.int32, pin_memory=pin)
-        slots = [(self.planes[i].data_ptr(), self.player[i].data_ptr(), self.rank[i].data_ptr(),
-                  self.label[i].data_ptr()) for i in range(prefetch)]
+        # ring slots in the packed layout (data/batch.py): a slot goes to the GPU in ONE
+        # async copy (next_packed_to); the named views are what the C++ workers fill
+        self.packed = torch.zeros((prefetch, packed_batch_bytes(B)), dtype=torch.uint8,
+                                  pin_memory=pin)
+        views = [unpack_views(self.packed[i], B) for i in range(prefetch)]
+        self.planes = [v[0] for v in views]
+        self.player = [v[1] for v in views]
+        self.rank = [v[2] for v in views]
+        self.label = [v[3] for v in views]
+        slots = [(v[0].data_ptr(), v[1].data_ptr(), v[2].data_ptr(), v[3].data_ptr())
+                 for v in views]
         self._keep = None
         if isinstance(source, PackedDataset):
             self._keep = source  # arrays must outlive the C++ loader
@@ -68,6 +74,12 @@ class BatchLoader:
                 self._impl.release(slot)
             else:
                 keep.append((slot, ev))
+        # slots held by in-flight copies cannot be refilled: bound them (oldest first) so the
+        # workers always have free slots and next_host() cannot wait on a slot only we hold
+        while len(keep) > max(1, self.prefetch - 2):
+            slot, ev = keep.pop(0)
+            ev.synchronize()
+            self._impl.release(slot)
         self._pending = keep
 
     def next_to(self, planes: torch.Tensor, player: torch.Tensor, rank: torch.Tensor,
@@ -75,7 +87,7 @@ class BatchLoader:
         """Asynchronously copy the next batch into (device) tensors on the current stream."""
         self._reap()
         slot, seq = self.next_host()
-        planes.copy_(self.planes[slot].view_as(planes), non_blocking=True)
+        planes.copy_(self.planes[slot].reshape(planes.shape), non_blocking=True)
         player.copy_(self.player[slot], non_blocking=True)
         rank.copy_(self.rank[slot], non_blocking=True)
         labels.copy_(self.label[slot].to(labels.dtype) if labels.dtype != torch.int32
@@ -90,11 +102,27 @@ class BatchLoader:
         self._pending.append((slot, ev))
         return seq
 
+    def next_packed_to(self, dst: torch.Tensor) -> int:
+        """One asynchronous copy of the next packed batch into ``dst`` (e.g. HipGoNet.inbuf)
+        on the current stream; the slot is released once that copy has completed."""
+        self._reap()
+        slot, seq = self.next_host()
+        dst.copy_(self.packed[slot], non_blocking=True)
+        if dst.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending.append((slot, ev))
+        else:
+            self._impl.release(slot)
+        return seq
+
     def next_numpy(self):
         """Copy the next batch out as numpy arrays (CPU path / tools)."""
         slot, seq = self.next_host()
-        out = (self.planes[slot].numpy().copy(), self.player[slot].numpy().copy(),
-               self.rank[slot].numpy().copy(), self.label[slot].numpy().copy())
+        B = self.batch
+        out = (self.planes[slot].numpy().reshape(B, 9, 19, 19).copy(),
+               self.player[slot].numpy().copy(), self.rank[slot].numpy().copy(),
+               self.label[slot].numpy().copy())
         self._impl.release(slot)
         return out
 

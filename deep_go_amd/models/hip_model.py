@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from ..config import NUM_POINTS, ExperimentConfig
+from ..data.batch import pack_batch, packed_batch_bytes, unpack_views  # noqa: F401
 from ..ops import layouts as LY
 from ..ops.native import hip, stream_handle
 from ..utils import trace
@@ -404,6 +405,12 @@ class HipGoNet:
         if not self._fp8_calibrated:
             self.calibrate_fp8()
 
+    def set_batch_packed_from(self, loader):
+        """Next batch of a BatchLoader with pinned packed slots: one async copy."""
+        loader.next_packed_to(self.inbuf)
+        if not self._fp8_calibrated:
+            self.calibrate_fp8()
+
     def forward(self):
         s = stream_handle()
         self._run(self._pre, s)
@@ -531,40 +538,6 @@ class HipGoNet:
         ts = [self.params, self.grads, self.slab, self.x0, *self.act, *self.dz, *self.wf,
               *[w for w in self.wd if w is not None]]
         return sum(t.numel() * t.element_size() for t in ts)
-
-
-def packed_batch_bytes(B: int) -> int:
-    n = B * 9 * NUM_POINTS + 2 * B
-    return n + (-n % 4) + 4 * B
-
-
-def unpack_views(buf: torch.Tensor, B: int):
-    """(planes [B,9,361] u8, player [B] u8, rank [B] u8, labels [B] i32) views of a packed
-    batch buffer (labels 4-byte aligned)."""
-    n = B * 9 * NUM_POINTS
-    planes = buf[:n].view(B, 9, NUM_POINTS)
-    player = buf[n:n + B]
-    rank = buf[n + B:n + 2 * B]
-    lo = n + 2 * B
-    lo += -lo % 4
-    labels = buf[lo:lo + 4 * B].view(torch.int32)
-    return planes, player, rank, labels
-
-
-def pack_batch(planes, player, rank, labels, device=None) -> torch.Tensor:
-    """Pack one batch (numpy arrays or tensors) into the HipGoNet input layout."""
-    def t(x, dt):
-        x = torch.as_tensor(x)
-        return x.to(dt)
-    planes = t(planes, torch.uint8)
-    B = planes.shape[0]
-    buf = torch.zeros(packed_batch_bytes(B), dtype=torch.uint8, device=device or planes.device)
-    p, pl, rk, lb = unpack_views(buf, B)
-    p.copy_(planes.reshape(B, 9, NUM_POINTS))
-    pl.copy_(t(player, torch.uint8))
-    rk.copy_(t(rank, torch.uint8))
-    lb.copy_(t(labels, torch.int32))
-    return buf
 
 
 class GraphedStep:

@@ -64,6 +64,11 @@ class CPUBackend:
     def rate(self) -> float:
         return self.opt.rate
 
+    def load_next(self, loader):
+        batch = loader.next_numpy()
+        self.set_batch(*batch)
+        return batch
+
     def set_batch(self, planes, player, rank, labels):
         pl = _np(planes, np.uint8).reshape(-1, 9, 19, 19)
         self._x = torch.from_numpy(cpu().expand(pl, _np(player, np.uint8), _np(rank, np.uint8)))
@@ -161,6 +166,18 @@ class HIPBackend:
     @property
     def params(self):
         return self.net.params
+
+    def load_next(self, loader):
+        """Next training batch straight from the loader's pinned packed slot into the
+        network's input buffer: one async H2D copy, ordered before the step on the same
+        stream.  Returns None (the host copy is gone; ``current_batch`` reads it back)."""
+        self.net.set_batch_packed_from(loader)
+        return None
+
+    def current_batch(self):
+        from ..data.batch import unpack_views
+        pl, py_, rk, lb = unpack_views(self.net.inbuf.cpu(), self.B)
+        return (pl.numpy().reshape(self.B, 9, 19, 19), py_.numpy(), rk.numpy(), lb.numpy())
 
     def set_batch(self, planes, player, rank, labels):
         dev = self.device

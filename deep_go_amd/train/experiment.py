@@ -165,11 +165,9 @@ class Experiment:
         last_val = None
         save_now = False
         for _ in range(iters):
-            with trace.range("loader_wait"):
-                batch = loader.next_numpy()
+            with trace.range("load_batch"):
+                batch = be.load_next(loader)
             self.loader_seq = loader.consumed
-            with trace.range("h2d"):
-                be.set_batch(*batch)
             with trace.range("fwd_bwd"):
                 be.forward_backward()
             step = self.iterations + 1
@@ -180,6 +178,8 @@ class Experiment:
                 loss = be.loss_sum() / self.local_batch
                 if inj == "nan":
                     loss = float("nan")
+                if batch is None and not np.isfinite(loss):
+                    batch = be.current_batch()  # only for the bad-batch dump
                 if not check_finite(loss, step, cfg.nan_policy, batch, cfg.checkpoint_dir):
                     loss = ema if ema is not None else 0.0
                 ema = loss if ema is None else 0.95 * ema + 0.05 * loss

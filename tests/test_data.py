@@ -106,3 +106,25 @@ def test_pack_batch_roundtrip(B):
     a, b, c, d = unpack_views(buf, B)
     assert (a.numpy() == pl.reshape(B, 9, 361)).all() and (b.numpy() == py).all()
     assert (c.numpy() == rk).all() and (d.numpy() == lb).all()
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_packed_slot_copy_matches_numpy(train_index, device):
+    """next_packed_to (one copy of the pinned packed slot) carries the same batches as
+    next_numpy, and many more batches than slots go through without a stall."""
+    import torch
+    from deep_go_amd.data.batch import packed_batch_bytes, unpack_views
+    pk = PackedDataset.from_index(train_index)
+    B = 24
+    la = BatchLoader(pk, B, threads=2, prefetch=3, seed=11, pin=(device == "cuda"))
+    lb = BatchLoader(pk, B, threads=2, prefetch=3, seed=11, pin=False)
+    dst = torch.zeros(packed_batch_bytes(B), dtype=torch.uint8, device=device)
+    for _ in range(12):
+        la.next_packed_to(dst)
+        want = lb.next_numpy()
+        got = unpack_views(dst.cpu(), B)
+        assert np.array_equal(got[0].numpy().reshape(B, 9, 19, 19), want[0])
+        for g, w in zip(got[1:], want[1:]):
+            assert np.array_equal(g.numpy(), w)
+    la.close()
+    lb.close()
