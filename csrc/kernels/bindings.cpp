@@ -25,6 +25,10 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
 void dg_conv_board_set_ablate(int mode);
 hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
                              hipStream_t stream);
+void dg_conv_stack_set_ablate(int mode);
+void dg_conv_stack_set_ring(int n);
+hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
+                         hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
                             const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
                             const float* bias, const float* posb, const void* pbias,
@@ -133,6 +137,12 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_conv_stack_fwd(P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
           "conv_stack_fwd");
   }, "fused forward of a run of 128->128 3x3 layers, board resident in LDS");
+  m.def("conv_stack", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                         uintptr_t stream) {
+    check(dg_conv_stack(epi, P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
+          "conv_stack");
+  }, "fused run of 128->128 3x3 layers, board resident in LDS: EPI_FWD forward (+bias, ReLU,"
+     " writes masks) or EPI_DGRAD backward-data chain (ReLU masks of the layers below)");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
                          int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {
@@ -250,6 +260,11 @@ PYBIND11_MODULE(_dghip, m) {
   });
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
+  m.def("conv_stack_set_ablate", [](int mode) { dg_conv_stack_set_ablate(mode); },
+        "timing ablations of conv_stack (forward): 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no"
+        " copy-out, 16 no barrier");
+  m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },
+        "weight-tile ring depth of conv_stack (2 or 3; 0 = default)");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
   m.def("conv_wgrad_set_ring", [](int on) { dg_conv_wgrad_set_ring(on); },
         "1: 32-pixel 3-stage ring wgrad for 3x3/5x5 (3 workgroups per CU); 0: 64-pixel 2-stage");

@@ -1,31 +1,43 @@
-// Fused forward of a run of hidden 3x3 layers (C -> C, C = 128, pad 1): the whole
-// board-resident forward stack in ONE launch.
+// Fused run of hidden 3x3 layers (C -> C, C = 128, pad 1), board-resident in LDS: the
+// whole forward stack, or the whole backward-data (dgrad) chain, in ONE launch.
 //
 // Per-layer kernels (conv_board.hip) end every layer with a burst of 23.6 MB of stores
 // from all workgroups at once, plus a prologue that re-reads the same activation from HBM;
 // ablations (profiles/) put that epilogue/prologue at ~14 of ~32 us per layer, and it
 // cannot overlap with anything because every workgroup reaches it at the same time.
+// A conv layer (and its transposed-weight dgrad) only mixes pixels of ONE board, so a
+// workgroup that owns a board can run the next layer without any grid-wide sync.
 //
 // Here one workgroup owns one board for ALL layers of the run:
-//   * the board's zero-bordered 21x21x128 activation frame lives in LDS (two 64-channel
-//     halo images, 112 KB, XOR-swizzled 128-B rows — the conv_board layout);
+//   * the board's zero-bordered 21x21x128 frame lives in LDS (two 64-channel halo images,
+//     112 KB, XOR-swizzled 128-B rows — the conv_board layout);
 //   * each layer is 18 K-steps (2 chunks x 9 taps) of v_mfma_f32_16x16x32_bf16 over that
-//     image, weight tiles [128 co][64 k] streamed by LDS-DMA (double-buffered, the next
-//     layer's first tile prefetched during the current layer's last step);
-//   * the epilogue (bias + pos-bias table, ReLU) writes the layer's bf16 output straight
-//     back INTO the LDS image (it is the next layer's input), and the global store of that
-//     output (activation frame for the backward + 1-bit ReLU mask) is spread over the next
-//     layer's first 12 K-steps, underneath its MFMAs.
+//     image; weight tiles [128 co][64 k] stream through a 3-deep LDS ring by LDS-DMA,
+//     issued two steps ahead (across layer boundaries) and retired with a COUNTED
+//     s_waitcnt vmcnt(2) + raw s_barrier, so a tile's L2 latency has two steps to land and
+//     the barrier never drains the newest DMA (a __syncthreads() would: vmcnt(0));
+//   * the epilogue writes the layer's bf16 output straight back INTO the LDS image (it is
+//     the next layer's input):
+//       EPI_FWD   : + (bias + pos-bias) table, ReLU          (forward; writes ReLU bitmask)
+//       EPI_DGRAD : * ReLU bitmask of the layer below       (dZ_{i-1} = mask * W_i^T dZ_i)
+//     and the global store of that output (activation / gradient frame for the wgrads,
+//     plus the forward's bitmask) is spread over the next layer's first 12 K-steps,
+//     underneath its MFMAs.
 // Only the first input load and the last layer's stores are exposed.
 //
+// LDS: 3 x 16 KB weight ring + 2 x 56 KB images = 160 KB (the whole CU): one workgroup of
+// 8 waves per CU, one board per workgroup.
+//
 // Reference ops: nn.SpatialZeroPadding + SpatialConvolutionMM + Add + ReLU per layer
-// (experiments.lua:137-147).
+// (experiments.lua:137-147) and their backward through the stack (train.lua:10).
 #include "dg_common.h"
 
 using namespace dg;
 
 namespace {
 
+constexpr int EPI_FWD = 1;
+constexpr int EPI_DGRAD = 2;
 constexpr int C = 128;
 constexpr int F = 21;                     // 19 + 2 * pad(1)
 constexpr int FF = F * F;                 // 441
@@ -37,13 +49,14 @@ constexpr int UNITS = NPTS * 16;          // 16-B output pieces of one board (57
 constexpr int MAXL = 24;
 constexpr int BM = 128;
 constexpr int A_BYTES = BM * 128;         // [128 co][64 k] bf16
+constexpr int DMA_PER_TILE = 2;           // LDS-DMA instructions per wave per tile
 constexpr int WN = 4, MF = 4, NF = 6;     // 2 x 4 waves, 64 co x 96 px per wave
 
 struct StackLayer {
-  const bf16_t* A;      // [128][KP] forward weights, k = tap*128 + ci
-  const bf16_t* pbias;  // [361][128] bf16 bias + pos-bias
+  const bf16_t* A;      // [128][KP] weights, k = tap*128 + ci (dgrad: flipped, transposed)
+  const bf16_t* pbias;  // [361][128] bf16 bias + pos-bias (EPI_FWD)
   char* Y;              // output frame [B][21][21][128] bf16
-  uint8_t* mask;        // [B][361][16] ReLU bits or null
+  uint8_t* mask;        // [B][361][16] ReLU bits: EPI_FWD writes (optional), EPI_DGRAD reads
 };
 struct StackArgs {
   const char* X0;       // input frame [B][21][21][128] bf16 of the first layer
@@ -51,7 +64,12 @@ struct StackArgs {
   StackLayer L[MAXL];
 };
 
-__global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
+// NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
+// ABL: timing ablations for tools/kbench_stack.py (0 in production): 1 no MFMA, 2 no
+// fragment LDS reads, 4 no weight DMA, 8 no in-loop copy-out, 16 no per-step barrier.
+template <int EPI, int NRING, int ABL>
+__global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
+  constexpr int AHEAD = NRING - 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -59,22 +77,30 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int b = blockIdx.x;
   char* sA0 = smem;
-  char* sH = smem + 2 * A_BYTES;  // image c at sH + c * H_BYTES
+  char* sH = smem + NRING * A_BYTES;  // image c at sH + c * H_BYTES
   const int g_src = (lane & 7) ^ (lane >> 3);
+  const int total = a.nl * NSTEP;     // global K-steps over all layers
 
-  auto stage_A = [&](int buf, const bf16_t* A, int step) {
-    const int c = step / T, t = step - (step / T) * T;
+  // weight tile of global step g into ring slot g % NRING: exactly DMA_PER_TILE LDS-DMA
+  // instructions per wave, issued from inline asm (dma16) so the compiler's waitcnt pass
+  // does not drain them in front of the copy-out's LDS reads; retired by dma_wait below
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
+  auto stage_A = [&](int g) {
+    if (ABL & 4) return;
+    const int l = g / NSTEP, s = g - l * NSTEP;
+    const int c = s / T, t = s - (s / T) * T;
     const int kcol = t * C + c * 64;
-    char* dst = sA0 + buf * A_BYTES;
+    const bf16_t* A = a.L[l].A;
+    const uint32_t dst = lds0 + (g % NRING) * A_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < DMA_PER_TILE; ++i) {
       const int r = (wave * 2 + i) * 8 + (lane >> 3);
-      glds16((const char*)A + ((size_t)r * a.KP + kcol + g_src * 8) * 2,
-             (LDS_AS void*)(dst + (wave * 2 + i) * 1024));
+      dma16((const char*)A + ((size_t)r * a.KP + kcol + g_src * 8) * 2,
+            __builtin_amdgcn_readfirstlane(dst + (wave * 2 + i) * 1024));
     }
   };
 
-  // ---- prologue: the first layer's input frame (both images) + its first weight tile ----
+  // ---- prologue: the first layer's input frame (both images) + weight tiles 0, 1 ----
   {
     const char* Xb = a.X0 + (size_t)b * FF * C * 2;
     for (int j = wave; j < 2 * (HROWS / 8); j += 8) {
@@ -84,7 +110,7 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
       glds16(Xb + ((size_t)r * C + c * 64 + g_src * 8) * 2,
              (LDS_AS void*)(sH + c * H_BYTES + jj * 1024));
     }
-    stage_A(0, a.L[0].A, 0);
+    for (int g = 0; g < AHEAD && g < total; ++g) stage_A(g);
   }
   __syncthreads();
 
@@ -99,7 +125,7 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
     fp[j] = (h + 1) * F + (w + 1);
   }
 
-  // store one 16-B piece (8 channels of one pixel) of the activation held in LDS
+  // store one 16-B piece (8 channels of one pixel) of the image held in LDS
   auto copy_out = [&](int u, const StackLayer& Lo) {
     const int p = u >> 4, q = u & 15;
     const int c = q >> 3, g = q & 7;
@@ -107,14 +133,14 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
     const int f = (h + 1) * F + (w + 1);
     const uint4 v = *(const uint4*)(sH + c * H_BYTES + f * 128 + ((g ^ (f & 7)) * 16));
     *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C + c * 64 + g * 8) * 2) = v;
-    if (Lo.mask) {
+    if (EPI == EPI_FWD && Lo.mask) {
       auto nz = [](uint32_t x) { return ((x & 0xFFFFu) ? 1u : 0u) | ((x >> 16) ? 2u : 0u); };
       Lo.mask[((size_t)b * NPTS + p) * 16 + q] =
           (uint8_t)(nz(v.x) | (nz(v.y) << 2) | (nz(v.z) << 4) | (nz(v.w) << 6));
     }
   };
 
-  int gs = 0;  // global step counter (A buffer parity)
+  int gs = 0;  // global step
   for (int l = 0; l < a.nl; ++l) {
     const StackLayer L = a.L[l];
     f32x4 acc[MF][NF];
@@ -125,15 +151,19 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
 
     for (int s = 0; s < NSTEP; ++s, ++gs) {
       const int c = s / T, t = s - (s / T) * T;
-      if (s + 1 < NSTEP) stage_A((gs + 1) & 1, L.A, s + 1);
-      else if (l + 1 < a.nl) stage_A((gs + 1) & 1, a.L[l + 1].A, 0);
       // the previous layer's output (already in the image) goes to HBM under this layer's
-      // MFMAs: 512 pieces per step over the first 12 steps
-      if (l > 0) {
+      // MFMAs: 512 pieces per step over the first 12 steps.  Issued BEFORE the weight DMA:
+      // hipcc puts an s_waitcnt vmcnt(0) in front of an LDS read that follows an LDS-DMA
+      // (it cannot prove they do not alias), which would expose the DMA's latency.
+      if (!(ABL & 8) && l > 0) {
         const int u = s * 512 + tid;
         if (u < UNITS) copy_out(u, a.L[l - 1]);
       }
-      const char* sA = sA0 + (gs & 1) * A_BYTES;
+      // ring slot (gs+AHEAD)%NRING was last read in step gs-1: every wave passed the
+      // barrier after it
+      const bool more = gs + AHEAD < total;
+      if (more) stage_A(gs + AHEAD);
+      const char* sA = sA0 + (gs % NRING) * A_BYTES;
       const char* sHc = sH + c * H_BYTES;
       const int toff = (t / 3 - 1) * F + (t % 3 - 1);
       // one k-half's fragments live at a time (register budget with the copy-out in the
@@ -145,38 +175,62 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           const int row = wm * 64 + i * 16 + lr;
-          af[i] = lds_read_b128((const LDS_AS char*)(sA + row * 128 + ((g ^ (row & 7)) * 16)));
+          af[i] = (ABL & 2) ? bf16x8{}
+                  : lds_read_b128((const LDS_AS char*)(sA + row * 128 + ((g ^ (row & 7)) * 16)));
         }
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
           const int row = fp[j] + toff;
-          bfr[j] = lds_read_b128((const LDS_AS char*)(sHc + row * 128 + ((g ^ (row & 7)) * 16)));
+          bfr[j] = (ABL & 2) ? bf16x8{}
+                   : lds_read_b128((const LDS_AS char*)(sHc + row * 128 + ((g ^ (row & 7)) * 16)));
         }
+        if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
+          for (int i = 0; i < MF; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
-          for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+          for (int j = 0; j < NF; ++j) asm volatile("" ::"v"(bfr[j]));
+        } else {
+#pragma unroll
+          for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();
+      // tile gs+1 must have landed for every wave; the newer tiles (the newest
+      // DMA_PER_TILE*(AHEAD-1) VMEM ops of this wave — the copy-out stores precede them)
+      // may stay in flight
+      if (more) dma_wait<DMA_PER_TILE * (AHEAD - 1)>(); else dma_wait<0>();
+      if (!(ABL & 16)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- epilogue: + (bias + pos-bias), ReLU, bf16 -> back into the LDS image ----
+    // ---- epilogue: write the layer's output back into the LDS image ----
     // (every wave is past its last read of the image: barrier above)
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = wn * NF * 16 + j * 16 + lr;
       if (p >= NPTS) continue;
       const int f = fp[j];
+      uint2 mb = {0u, 0u};
+      if constexpr (EPI == EPI_DGRAD)  // 64 channel bits of this wave's image half
+        mb = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8);
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
-        const uint2 u = *(const uint2*)(L.pbias + p * C + wm * 64 + cl);
         f32x4 v = acc[i][j];
-        v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
-        v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
-        v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
-        v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+        if constexpr (EPI == EPI_FWD) {
+          const uint2 u = *(const uint2*)(L.pbias + p * C + wm * 64 + cl);
+          v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
+          v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+          v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
+          v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+        } else {
+          const uint32_t word = (cl < 32) ? mb.x : mb.y;
+          const uint32_t bits = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] : 0.f;
+        }
         uint2 o;
         o.x = pack_bf16x2(v[0], v[1]);
         o.y = pack_bf16x2(v[2], v[3]);
@@ -190,14 +244,52 @@ __global__ void __launch_bounds__(512) conv_stack_fwd_kernel(StackArgs a) {
   for (int u = tid; u < UNITS; u += 512) copy_out(u, a.L[a.nl - 1]);
 }
 
+template <int EPI, int NRING, int ABL>
+hipError_t launch_stack(const StackArgs& a, int B, hipStream_t stream) {
+  constexpr size_t lds = NRING * (size_t)A_BYTES + 2 * (size_t)H_BYTES;
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_stack_kernel<EPI, NRING, ABL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+  hipLaunchKernelGGL((conv_stack_kernel<EPI, NRING, ABL>), dim3(B), dim3(512), lds, stream, a);
+  return hipGetLastError();
+}
+
+template <int NRING>
+hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s) {
+  switch (ablate) {  // forward only; see tools/kbench_stack.py
+    case 1: return launch_stack<EPI_FWD, NRING, 1>(a, B, s);
+    case 2: return launch_stack<EPI_FWD, NRING, 2>(a, B, s);
+    case 4: return launch_stack<EPI_FWD, NRING, 4>(a, B, s);
+    case 8: return launch_stack<EPI_FWD, NRING, 8>(a, B, s);
+    case 16: return launch_stack<EPI_FWD, NRING, 16>(a, B, s);
+    case 6: return launch_stack<EPI_FWD, NRING, 6>(a, B, s);
+    case 12: return launch_stack<EPI_FWD, NRING, 12>(a, B, s);
+    case 14: return launch_stack<EPI_FWD, NRING, 14>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace
+
+static int g_stack_ablate = 0;
+static int g_stack_ring = 0;  // 0: default (2)
 
 extern "C" {
 
-// table: nl rows of {A, pbias, Y, mask} (int64 pointers; mask may be 0)
-hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
-                             hipStream_t stream) {
+void dg_conv_stack_set_ablate(int mode) { g_stack_ablate = mode; }
+void dg_conv_stack_set_ring(int n) { g_stack_ring = n; }
+
+// table: nl rows of {A, pbias, Y, mask} (int64 pointers)
+//   epi 1 (forward): pbias required, mask optional (written)
+//   epi 2 (dgrad)  : mask required (read; ReLU bits of the layer below), pbias unused
+hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
+                         hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || KP < T * C || KP % 64 != 0 || B <= 0) return hipErrorInvalidValue;
+  if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
   StackArgs a;
   a.X0 = (const char*)X0;
   a.nl = nl;
@@ -207,17 +299,25 @@ hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int
     a.L[i].pbias = (const bf16_t*)table[4 * i + 1];
     a.L[i].Y = (char*)table[4 * i + 2];
     a.L[i].mask = (uint8_t*)table[4 * i + 3];
-    if (!a.L[i].A || !a.L[i].pbias || !a.L[i].Y) return hipErrorInvalidValue;
+    if (!a.L[i].A || !a.L[i].Y) return hipErrorInvalidValue;
+    if (epi == EPI_FWD && !a.L[i].pbias) return hipErrorInvalidValue;
+    if (epi == EPI_DGRAD && !a.L[i].mask) return hipErrorInvalidValue;
   }
-  constexpr size_t lds = 2 * (size_t)A_BYTES + 2 * (size_t)H_BYTES;
-  static bool done = false;
-  if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_fwd_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    done = true;
-  }
-  hipLaunchKernelGGL(conv_stack_fwd_kernel, dim3(B), dim3(512), lds, stream, a);
-  return hipGetLastError();
+  const int nring = g_stack_ring ? g_stack_ring : 2;
+  if (g_stack_ablate)
+    return epi == EPI_FWD ? (nring == 3 ? dispatch_ablate<3>(g_stack_ablate, a, B, stream)
+                                        : dispatch_ablate<2>(g_stack_ablate, a, B, stream))
+                          : hipErrorInvalidValue;
+  if (epi == EPI_FWD)
+    return nring == 3 ? launch_stack<EPI_FWD, 3, 0>(a, B, stream)
+                      : launch_stack<EPI_FWD, 2, 0>(a, B, stream);
+  return nring == 3 ? launch_stack<EPI_DGRAD, 3, 0>(a, B, stream)
+                    : launch_stack<EPI_DGRAD, 2, 0>(a, B, stream);
+}
+
+hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
+                             hipStream_t stream) {
+  return dg_conv_stack(EPI_FWD, table, nl, X0, KP, B, stream);
 }
 
 }  // extern "C"

@@ -181,12 +181,31 @@ class HipGoNet:
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self._fp8_calibrated = not self.fp8
-        slab = max(p.splits * p.Mpad_w * p.KPw for p in self.plans)
-        self.slab = torch.empty(slab, dtype=torch.float32, device=dev)
+        # backward side stream (off by default: both measured slower, profiles/README.md):
+        # "light" runs the bandwidth-bound bias-grad partials and split-K slab reduces beside
+        # the wgrads (each layer then needs its own slab / partial buffers: ~34 MB per
+        # 128-channel layer, nothing next to 288 GB) — 1.43 vs 1.37 ms/step: they compete
+        # with the wgrad's own L2->LDS traffic (wgrad 42 -> 49 us); "wgrad"
+        # (DG_SIDE_STREAM=1) runs the whole weight-gradient chain beside the dgrads
+        side_mode = os.environ.get("DG_SIDE_STREAM", "0")
+        self.side_mode = {"1": "wgrad", "0": "none"}.get(side_mode, side_mode)
+        if self.side_mode not in ("none", "wgrad", "light"):
+            raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0, 1 or light")
         self.bchunks = self.h.bias_chunks(batch)
-        cmax = max(p.cout for p in self.plans)
-        self.bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
-                                 device=dev)
+        if self.side_mode == "light":
+            self.slabs = [torch.empty(p.splits * p.Mpad_w * p.KPw, dtype=torch.float32,
+                                      device=dev) for p in self.plans]
+            self.bparts = [torch.empty(self.bchunks * (NUM_POINTS + 19) * p.cout,
+                                       dtype=torch.float32, device=dev) for p in self.plans]
+        else:
+            slab = torch.empty(max(p.splits * p.Mpad_w * p.KPw for p in self.plans),
+                               dtype=torch.float32, device=dev)
+            cmax = max(p.cout for p in self.plans)
+            bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
+                                device=dev)
+            self.slabs = [slab] * len(self.plans)
+            self.bparts = [bpart] * len(self.plans)
+        self.slab = self.slabs[0]
 
         # ---- step I/O ----
         # one packed uint8 input buffer (planes | player | rank | labels as int32), so a step's
@@ -207,9 +226,7 @@ class HipGoNet:
                                         device=dev)
         self.head_dzb = torch.zeros((B, NUM_POINTS), dtype=torch.float32, device=dev)
 
-        # weight-gradient chain of the backward runs on its own stream (backward_layer)
-        self.side = (torch.cuda.Stream(device=dev)
-                     if os.environ.get("DG_SIDE_STREAM", "0") == "1" else None)
+        self.side = torch.cuda.Stream(device=dev) if self.side_mode != "none" else None
         self._refresh_table = self._build_refresh_table()
         self._build_plans()
         self.refresh_weights()
@@ -315,19 +332,20 @@ class HipGoNet:
             xin = self.x0 if i == 0 else self.act[i - 1]
             # bias grads: pass 1 (per board-chunk partials); pass 2 runs inside the slab
             # reduce launch, which also finalises the weight grad
+            slab, bpart = self.slabs[i].data_ptr(), self.bparts[i].data_ptr()
             ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
-                                              self.bpart.data_ptr())))
+                                              bpart)))
             if p.wgrad3:
                 ops.append((h.conv_wgrad3, (self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
                                             xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                            p.splits, self.slab.data_ptr())))
+                                            p.splits, slab)))
             else:
                 ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
                                            xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                           p.splits, self.slab.data_ptr())))
-            ops.append((h.wgrad_reduce, (self.slab.data_ptr(), G + spec.w_off * f4, p.splits,
+                                           p.splits, slab)))
+            ops.append((h.wgrad_reduce, (slab, G + spec.w_off * f4, p.splits,
                                          p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp,
-                                         self.bpart.data_ptr(), self.bchunks,
+                                         bpart, self.bchunks,
                                          G + spec.pos_off * f4, G + spec.b_off * f4)))
             if i > 0:
                 prev = lay.layers[i - 1]
@@ -346,6 +364,7 @@ class HipGoNet:
                                             self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
                                             self.act[i - 1].data_ptr(), spec.pad)))
             self._bwd.append(ops)
+        self._fuse_dgrad_stack()
 
     def _fuse_forward_stack(self):
         """Replace the per-layer forward launches of the longest run of hidden 128->128 3x3
@@ -382,6 +401,40 @@ class HipGoNet:
             return
         # self._fwd holds exactly one launch per plan here
         self._fwd = self._fwd[:first] + [op] + self._fwd[best[-1] + 1:]
+
+    def _fuse_dgrad_stack(self):
+        """Run the backward-data chain of the longest run of hidden 128->128 3x3 layers as
+        ONE conv_stack launch in EPI_DGRAD mode: dZ_{i-1} = relu_mask_{i-1} * (W_i^T * dZ_i)
+        for i = top .. bottom, board-resident in LDS (csrc/kernels/conv_stack.hip).  The
+        per-layer dgrad launches of those layers are dropped from ``_bwd``; their weight
+        gradients run afterwards (they only read dZ_i).  DG_DSTACK=0 keeps per-layer dgrads."""
+        self.dstack: List[int] = []
+        self._bwd_pre: List[Tuple[Callable, tuple]] = []
+        if os.environ.get("DG_DSTACK", "1") == "0":
+            return
+        L = self.layout.layers
+
+        def ok(i):
+            p = self.plans[i]
+            return (i > 0 and p.board_d and p.k == 3 and p.cin == 128 and p.cout == 128
+                    and L[i].pad == 1 and max(1, L[i - 1].pad) == 1 and p.KPd == p.KP
+                    and self.relu_mask[i - 1] is not None)
+        run = []
+        for i in range(len(self.plans) - 1, 0, -1):   # must start at the top hidden layer
+            if not ok(i):
+                break
+            run.append(i)
+        if len(run) < 2:
+            return
+        self.dstack = run
+        rows = [[self.wd[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
+                 self.relu_mask[i - 1].data_ptr()] for i in run]
+        self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+        self._bwd_pre.append((self.h.conv_stack, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+                                                  len(run), self.dz[run[0]].data_ptr(),
+                                                  self.plans[run[0]].KPd, self.B)))
+        for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
+            self._bwd[i] = self._bwd[i][:3]
 
     # ------------------------------------------------------------------ execution
     @staticmethod
@@ -428,6 +481,7 @@ class HipGoNet:
         f(*a, s)
         f, a = self._head_red
         f(*a, s)
+        self._run(self._bwd_pre, s)
         hooks = dict()
         for li, fn in self.grad_hooks:
             hooks.setdefault(li, []).append(fn)
@@ -445,10 +499,23 @@ class HipGoNet:
         other stream's work.  Callers end the backward with ``join_side()``."""
         ops = self._bwd[i]
         main = torch.cuda.current_stream()
-        if self.side is None:
+        if self.side_mode == "none":
             self._run(ops[:3], main.cuda_stream)
             for fn in hooks:
                 fn()
+        elif self.side_mode == "light":
+            # side: bias-grad partials beside this layer's wgrad, then the slab reduce beside
+            # the next launches on the main stream (per-layer slabs: no reuse hazard)
+            side = self.side
+            side.wait_stream(main)               # dZ_i final, earlier wgrads issued
+            self._run(ops[:1], side.cuda_stream)
+            self._run(ops[1:2], main.cuda_stream)
+            side.wait_stream(main)               # wgrad(i) done
+            self._run(ops[2:3], side.cuda_stream)
+            if hooks:
+                main.wait_stream(side)           # layer i's gradients final on main
+                for fn in hooks:
+                    fn()
         else:
             self.side.wait_stream(main)          # dZ_i (dgrad of layer i+1 / head) ready
             with torch.cuda.stream(self.side):
@@ -535,7 +602,8 @@ class HipGoNet:
         return {"params": self.params, "lr": self.lr, "step": self.step_count}
 
     def memory_bytes(self) -> int:
-        ts = [self.params, self.grads, self.slab, self.x0, *self.act, *self.dz, *self.wf,
+        uniq = {t.data_ptr(): t for t in (*self.slabs, *self.bparts)}
+        ts = [self.params, self.grads, *uniq.values(), self.x0, *self.act, *self.dz, *self.wf,
               *[w for w in self.wd if w is not None]]
         return sum(t.numel() * t.element_size() for t in ts)
 
@@ -590,6 +658,7 @@ class SegmentedStep:
         emit(lambda: net._run(net._fwd, stream_handle()))
         emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
         emit(lambda: net._head_red[0](*net._head_red[1], stream_handle()))
+        emit(lambda: net._run(net._bwd_pre, stream_handle()))
         if net.L - 1 in fire_after:
             segs.append((cur, fire_after[net.L - 1]))
             cur = []

@@ -92,8 +92,9 @@ def test_graph_replay_matches_eager():
     assert abs(net.lr.item() - lr_eager) < 1e-15
 
 
-@pytest.mark.parametrize("layers,ch,B", [(4, 128, 6)])
-def test_side_stream_backward_matches_single_stream(layers, ch, B, monkeypatch):
+@pytest.mark.parametrize("mode", ["1", "light"])
+@pytest.mark.parametrize("layers,ch,B", [(4, 128, 6), (6, 128, 3)])
+def test_side_stream_backward_matches_single_stream(layers, ch, B, mode, monkeypatch):
     """The weight-gradient chain on a side stream (HipGoNet.backward_layer) must give the
     same gradients as the single-stream order, eager and inside a segmented graph with a
     DP-style bucket boundary."""
@@ -103,7 +104,7 @@ def test_side_stream_backward_matches_single_stream(layers, ch, B, monkeypatch):
     net0.forward_backward()
     torch.cuda.synchronize()
     g0 = net0.grads.clone()
-    monkeypatch.setenv("DG_SIDE_STREAM", "1")
+    monkeypatch.setenv("DG_SIDE_STREAM", mode)
     _, net1, _ = _setup(layers, ch, B)
     assert net1.side is not None
     net1.forward_backward()
@@ -144,6 +145,25 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
             assert torch.equal(m0, m1)
     assert torch.equal(n0.loss, n1.loss)
     # (head_reduce folds board partials with atomics: last-bit order effects only)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("layers", [5, 7])
+def test_fused_dgrad_stack_matches_per_layer(layers, monkeypatch):
+    """conv_stack in EPI_DGRAD mode (the backward-data chain of the hidden layers in one
+    board-resident launch) runs the per-layer board dgrad's exact MFMA sequence and ReLU-mask
+    gating: every dZ frame is bit-identical."""
+    monkeypatch.setenv("DG_DSTACK", "0")
+    _, n0, _ = _setup(layers, 128, 5, seed=9)
+    monkeypatch.setenv("DG_DSTACK", "1")
+    _, n1, _ = _setup(layers, 128, 5, seed=9)
+    assert not n0.dstack and n1.dstack == list(range(layers - 2, 1, -1))
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    for d0, d1 in zip(n0.dz, n1.dz):
+        assert torch.equal(d0, d1)
+    # (same dZ in, same wgrad kernels; the gradients agree up to reduction-order bits)
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
