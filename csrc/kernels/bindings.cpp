@@ -36,6 +36,9 @@ hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int 
 void dg_conv_wgrad_set_ablate(int mode);
 void dg_conv_wgrad_set_ring(int on);
 int dg_conv_wgrad_wgs_per_cu();
+void dg_conv_wgrad_set_t3(int on);
+int dg_conv_wgrad_ktile(int KP);
+int dg_conv_wgrad_wgs_per_cu_for(int KP);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
@@ -269,6 +272,10 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_wgrad_set_ring", [](int on) { dg_conv_wgrad_set_ring(on); },
         "1: 32-pixel 3-stage ring wgrad for 3x3/5x5 (3 workgroups per CU); 0: 64-pixel 2-stage");
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
+  m.def("conv_wgrad_set_t3", [](int on) { dg_conv_wgrad_set_t3(on); },
+        "three-slice (128 x 384) wgrad tiles on/off (default on; env DG_WGRAD_T3)");
+  m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });
+  m.def("conv_wgrad_wgs_per_cu_for", [](int KP) { return dg_conv_wgrad_wgs_per_cu_for(KP); });
   m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });

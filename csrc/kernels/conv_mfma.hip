@@ -566,6 +566,160 @@ conv_wgrad_ring_kernel(WgradArgs a) {
   }
 }
 
+
+// Three-tap variant of conv_wgrad_kernel: one workgroup (8 waves) owns a 128 co x 384 k
+// tile — three consecutive 128-k slices (e.g. the three dw taps of one kernel row) — so the
+// dZ rows staged for a 64-pixel step serve three slices instead of one: 64 KB of LDS-DMA
+// per step feed 384 MFMAs (171 B/MFMA vs 256 for the 128 x 128 tile, the limiter of the
+// im2col wgrad per the no-DMA ablation).  Wave (wm, wn) owns 64 co x 96 k (4 x 6
+// fragments); one workgroup per CU (2 x 64 KB stages).  Same swizzle, transposing reads,
+// XCD remap and slab layout as conv_wgrad_kernel.
+template <int KW>
+__global__ void __launch_bounds__(512, 1)
+conv_wgrad_t3_kernel(WgradArgs a) {
+  constexpr int BKN = 64;
+  constexpr int T_BYTES = BKN * 256;           // one 64 x 128 (bf16) tile
+  constexpr int STAGE = 4 * T_BYTES;           // dZ tile + 3 X slices
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = a.ktiles * a.mtiles * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, xslot = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
+  const int kt = lid % a.ktiles;
+  const int rest = lid / a.ktiles;
+  const int mt = rest % a.mtiles;
+  const int zsplit = rest / a.mtiles;
+  const int k_tile = kt * 384;
+  const int m_tile = mt * 128;
+  const int n_begin = zsplit * a.px_per_split;
+  int n_end = n_begin + a.px_per_split;
+  if (n_end > a.Npix) n_end = a.Npix;
+  const int nsteps = n_end > n_begin ? (n_end - n_begin + BKN - 1) / BKN : 0;
+
+  // staging: each wave-instruction = 4 rows x 16 slots of 16 B; rows (wave*2 + i)*4 + r_in
+  const int r_in = lane >> 4;
+  const int slot = lane & 15;
+  int koffs[3][2];
+  int dz_chunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 2 + i) * 4 + r_in;
+    const int c = slot ^ wg_swz(r);
+    dz_chunk[i] = (m_tile * 2) + c * 16;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) koffs[j][i] = koff_wg<KW>((k_tile + j * 128) / 8 + c, a);
+  }
+
+  auto stage = [&](int buf, int step) {
+    char* sA = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wave * 2 + i) * 4 + r_in;
+      int n = n_begin + step * BKN + r;
+      const bool ok = n < n_end;
+      if (!ok) n = n_begin;
+      const int b = n / NPTS;
+      const int p = n - b * NPTS;
+      const int h = p / BOARD;
+      const int w = p - h * BOARD;
+      const uint32_t dzo = frame_off(b, h, w, a.dz_pad, a.M);
+      const uint32_t xo = frame_off(b, h, w, a.x_pad, a.x_C);
+      const char* src_dz = ok ? (a.dZ + dzo + dz_chunk[i]) : (a.dZ + (slot * 16));
+      glds16(src_dz, (LDS_AS void*)(sA + (wave * 2 + i) * 1024));
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        glds16(a.X + xo + koffs[j][i],
+               (LDS_AS void*)(sA + (j + 1) * T_BYTES + (wave * 2 + i) * 1024));
+    }
+  };
+
+  f32x4 acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    stage(0, 0);
+    __syncthreads();
+  }
+  const int li = lane & 15;
+  const int g = lane >> 4;
+  const int q = li >> 2, pp = li & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const char* sA = smem + buf * STAGE;
+    s16x4 ta[2][2][4], tb[2][2][6];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int row = kk * 32 + 8 * g + 4 * half + q;
+        const int sw = wg_swz(row);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = (wm * 64 + i * 16) / 8 + (pp >> 1);
+          ta[kk][half][i] =
+              lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const int col = wn * 96 + j * 16;  // within the 384-k tile
+          const int c = (col & 127) / 8 + (pp >> 1);
+          tb[kk][half][j] = lds_read_tr((const LDS_AS char*)(
+              sA + (1 + (col >> 7)) * T_BYTES + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // next step's DMA after the tr-reads (else the compiler waits vmcnt(0) before them)
+    if (st + 1 < nsteps) stage(buf ^ 1, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[6];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s16x4 lo = ta[kk][0][i], hi = ta[kk][1][i];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const s16x4 lo = tb[kk][0][j], hi = tb[kk][1][j];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  }
+
+  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m_tile + wm * 64 + i * 16 + g * 4 + r;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int k = k_tile + wn * 96 + j * 16 + li;
+        slab[(size_t)co * a.KP + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // Sum the split-K slabs and scatter into the fp32 master-gradient layout OHWI
 // [co][kh][kw][ci] (only ci < Cin, co < M).  out is overwritten.  Each thread owns 4
 // consecutive k of one co (16-byte slab loads), the split loop is unrolled by 4 so
@@ -729,6 +883,22 @@ static bool wgrad_ring_enabled() {
 }
 void dg_conv_wgrad_set_ring(int on) { g_wgrad_ring = on; }
 int dg_conv_wgrad_wgs_per_cu() { return wgrad_ring_enabled() ? 3 : 2; }
+static int g_wgrad_t3 = -1;
+static bool wgrad_t3_enabled() {
+  if (g_wgrad_t3 < 0) {
+    const char* e = getenv("DG_WGRAD_T3");
+    g_wgrad_t3 = e ? atoi(e) : 1;
+  }
+  return g_wgrad_t3 != 0;
+}
+void dg_conv_wgrad_set_t3(int on) { g_wgrad_t3 = on; }
+// k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K
+int dg_conv_wgrad_ktile(int KP) {
+  return (wgrad_t3_enabled() && !wgrad_ring_enabled() && KP % 384 == 0) ? 384 : 128;
+}
+int dg_conv_wgrad_wgs_per_cu_for(int KP) {
+  return dg_conv_wgrad_ktile(KP) == 384 ? 1 : dg_conv_wgrad_wgs_per_cu();
+}
 
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
@@ -760,6 +930,19 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
   a.ktiles = KP / 128;
   a.mtiles = Mpad / 128;
   a.splits = splits;
+  if (dg_conv_wgrad_ktile(KP) == 384 && (kw == 3 || kw == 5)) {
+    a.ktiles = KP / 384;
+    dim3 grid3(a.ktiles * a.mtiles * splits);
+    constexpr size_t lds3 = 2 * 4 * 64 * 256;
+    if (kw == 3) {
+      allow_lds(conv_wgrad_t3_kernel<3>, lds3);
+      hipLaunchKernelGGL(conv_wgrad_t3_kernel<3>, grid3, dim3(512), lds3, stream, a);
+    } else {
+      allow_lds(conv_wgrad_t3_kernel<5>, lds3);
+      hipLaunchKernelGGL(conv_wgrad_t3_kernel<5>, grid3, dim3(512), lds3, stream, a);
+    }
+    return hipGetLastError();
+  }
   dim3 grid(a.ktiles * a.mtiles * splits);
   if (wgrad_ring_enabled() && (kw == 3 || kw == 5)) {
     constexpr size_t lds_r = 3 * 2 * 32 * 256;

@@ -273,6 +273,7 @@ hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s)
   }
 }
 
+
 }  // namespace
 
 static int g_stack_ablate = 0;

@@ -129,7 +129,8 @@ class HipGoNet:
                                                 self.h.wgrad3_wgs_per_cu(cinp), num_cus)
             else:
                 splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
-                                               self.h.conv_wgrad_wgs_per_cu())
+                                               self.h.conv_wgrad_wgs_per_cu_for(KPw),
+                                               self.h.conv_wgrad_ktile(KPw))
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
                          Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3, cinp_f=cinp_f)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))

@@ -156,7 +156,8 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
                                                   h.wgrad3_wgs_per_cu(cinp))
     else:
         splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad,
-                                                 wgs_per_cu=h.conv_wgrad_wgs_per_cu())
+                                                 wgs_per_cu=h.conv_wgrad_wgs_per_cu_for(KPw),
+                                                 ktile=h.conv_wgrad_ktile(KPw))
     dzf = LY.to_frame(dz, max(1, pad))
     xf = LY.to_frame(x.to(dev), pad, cinp)
     slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)

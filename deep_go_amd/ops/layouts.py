@@ -99,11 +99,11 @@ def pick_tiles(npix: int, cout: int, num_cus: int = 256) -> tuple[int, int]:
 
 
 def pick_wgrad_splits(npix: int, KPw: int, Mpad: int, num_cus: int = 256,
-                      wgs_per_cu: int = 2) -> int:
+                      wgs_per_cu: int = 2, ktile: int = 128) -> int:
     """Split-K count for the im2col wgrad: one dispatch round of (k-tiles x m-tiles x
     splits) workgroups at ``wgs_per_cu`` resident workgroups per CU (hip().
     conv_wgrad_wgs_per_cu(): 3 for the ring kernel, 2 for the 2-stage one)."""
-    tiles = (KPw // 128) * (Mpad // 128)
+    tiles = (KPw // ktile) * (Mpad // 128)
     target = max(1, (wgs_per_cu * num_cus) // tiles)
     max_split = max(1, npix // 256)
     return max(1, min(target, max_split))

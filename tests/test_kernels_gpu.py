@@ -174,20 +174,24 @@ def test_conv_board_dgrad(B, cin, cout, k, bm, monkeypatch):
 
 @pytest.mark.parametrize("B,cin,cout,k,splits", [(3, 64, 64, 3, None), (7, 128, 128, 3, None),
                                                  (2, 40, 128, 5, 3), (5, 256, 256, 3, None),
-                                                 (1, 16, 16, 3, 1), (2, 128, 128, 1, 2)])
-@pytest.mark.parametrize("ring", [1, 0])
-def test_conv_wgrad(B, cin, cout, k, splits, ring):
-    """im2col wgrad, ring (32-pixel 3-stage, asm LDS-DMA) and 2-stage variants."""
+                                                 (1, 16, 16, 3, 1), (2, 128, 128, 1, 2),
+                                                 (3, 128, 128, 3, 7), (2, 128, 256, 3, None)])
+@pytest.mark.parametrize("variant", ["ring", "plain", "t3"])
+def test_conv_wgrad(B, cin, cout, k, splits, variant):
+    """im2col wgrad: ring (32-pixel 3-stage, asm LDS-DMA), 2-stage 128x128 and three-slice
+    128x384 tiles (the t3 kernel runs where K % 384 == 0, else the 2-stage one)."""
     torch.manual_seed(3)
     from deep_go_amd.ops import functional as Fn
     from deep_go_amd.ops.native import hip
-    hip().conv_wgrad_set_ring(ring)
+    hip().conv_wgrad_set_ring(1 if variant == "ring" else 0)
+    hip().conv_wgrad_set_t3(1 if variant == "t3" else 0)
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
     try:
         got, gp, gb = Fn.conv_wgrad(dz, x, k, splits=splits, with_bias=True, algo="im2col")
     finally:
         hip().conv_wgrad_set_ring(0)
+        hip().conv_wgrad_set_t3(1)
     w0 = torch.zeros(cout, k, k, cin, device=DEV, requires_grad=True)
     y = conv_ref(x, w0, k)
     (gw,) = torch.autograd.grad(y, w0, dz)

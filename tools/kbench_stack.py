@@ -15,6 +15,7 @@ from tools.kbench import timeit  # noqa: E402
 
 
 def main():
+    ablations = "--ablate" in sys.argv
     h = hip()
     B, C, NL = 256, 128, 10
     dev = "cuda"
@@ -38,12 +39,21 @@ def main():
 
     def run(epi, table):
         return lambda: h.conv_stack(epi, table.ctypes.data, NL, x.data_ptr(), KP, B, s)
+    # correctness of the variants against each other (same inputs -> same outputs)
+    outs = {}
+    for ring in (2, 3):
+        h.conv_stack_set_ring(ring)
+        run(h.EPI_FWD, tf)()
+        torch.cuda.synchronize()
+        outs[ring] = [y.clone() for y in ys] + [m.clone() for m in ms]
+    h.conv_stack_set_ring(0)
+    res_ok = all(torch.equal(a, b) for a, b in zip(outs[2], outs[3]))
     for rnd in range(2):
         for ring in (2, 3):
             h.conv_stack_set_ring(ring)
             for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
                 res.setdefault(f"ring{ring}_{name}", []).append(round(timeit(run(epi, t)), 1))
-            for abl in (1, 2, 4, 8, 16, 6, 12, 14):
+            for abl in ((1, 2, 4, 8, 16, 6, 12, 14) if ablations and ring > 1 else ()):
                 h.conv_stack_set_ablate(abl)
                 res.setdefault(f"ring{ring}_fwd_abl{abl}", []).append(
                     round(timeit(run(h.EPI_FWD, tf)), 1))
@@ -51,6 +61,7 @@ def main():
         h.conv_stack_set_ring(0)
     out = {k: {"us": v, "us_per_layer": round(min(v) / NL, 2),
                "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
+    out["variants_bit_identical"] = res_ok
     print(json.dumps(out, indent=1))
 
 
