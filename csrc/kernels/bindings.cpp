@@ -27,6 +27,7 @@ hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int
                              hipStream_t stream);
 void dg_conv_stack_set_ablate(int mode);
 void dg_conv_stack_set_ring(int n);
+void dg_conv_stack_set_bpf(int on);
 hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
                          hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
@@ -266,6 +267,8 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_stack_set_ablate", [](int mode) { dg_conv_stack_set_ablate(mode); },
         "timing ablations of conv_stack (forward): 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no"
         " copy-out, 16 no barrier");
+  m.def("conv_stack_set_bpf", [](int on) { dg_conv_stack_set_bpf(on); },
+        "B-fragment prefetch across K-steps in conv_stack (default on)");
   m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },
         "weight-tile ring depth of conv_stack (2 or 3; 0 = default)");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });

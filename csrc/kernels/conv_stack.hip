@@ -52,6 +52,15 @@ constexpr int A_BYTES = BM * 128;         // [128 co][64 k] bf16
 constexpr int DMA_PER_TILE = 2;           // LDS-DMA instructions per wave per tile
 constexpr int WN = 4, MF = 4, NF = 6;     // 2 x 4 waves, 64 co x 96 px per wave
 
+// Image swizzle: the 16-B slot of 8-channel group g in frame row f is g ^ sig(f) with
+// sig(f) = (x + 3y) & 7, (y, x) = (f / 21, f % 21).  The plain f & 7 (conv_board) is
+// conflict-free for 16 consecutive rows, but a 16-pixel B fragment crosses a board-row
+// wrap (+2 frame rows) in 3 of 4 cases: 75% of the fragment reads were 2-way bank
+// conflicts (avg 1.75 LDS cycles per lane group, modelled over every tap / fragment);
+// (x + 3y) & 7 brings that to 1.04.  Linear in (x, y), so a tap shift (dh, dw) adds the
+// uniform dw + 3 dh.
+DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+
 struct StackLayer {
   const bf16_t* A;      // [128][KP] weights, k = tap*128 + ci (dgrad: flipped, transposed)
   const bf16_t* pbias;  // [361][128] bf16 bias + pos-bias (EPI_FWD)
@@ -67,7 +76,7 @@ struct StackArgs {
 // NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
 // ABL: timing ablations for tools/kbench_stack.py (0 in production): 1 no MFMA, 2 no
 // fragment LDS reads, 4 no weight DMA, 8 no in-loop copy-out, 16 no per-step barrier.
-template <int EPI, int NRING, int ABL>
+template <int EPI, int NRING, int ABL, bool BPF = true>
 __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   constexpr int AHEAD = NRING - 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -107,7 +116,9 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
       int r = jj * 8 + (lane >> 3);
       r = r < FF ? r : FF - 1;
-      glds16(Xb + ((size_t)r * C + c * 64 + g_src * 8) * 2,
+      const int rl = jj * 8 + (lane >> 3);  // LDS row this lane fills (slot lane & 7)
+      const int gs_ = (lane & 7) ^ fsig(rl);
+      glds16(Xb + ((size_t)r * C + c * 64 + gs_ * 8) * 2,
              (LDS_AS void*)(sH + c * H_BYTES + jj * 1024));
     }
     for (int g = 0; g < AHEAD && g < total; ++g) stage_A(g);
@@ -116,13 +127,14 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
 
   const int lr = lane & 15;
   const int lq = lane >> 4;
-  int fp[NF];
+  int fp[NF], fs[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     int p = wn * NF * 16 + j * 16 + lr;
     if (p >= NPTS) p = 0;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     fp[j] = (h + 1) * F + (w + 1);
+    fs[j] = (w + 1) + 3 * (h + 1);  // fsig(fp[j]) before the & 7
   }
 
   // store one 16-B piece (8 channels of one pixel) of the image held in LDS
@@ -131,7 +143,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     const int c = q >> 3, g = q & 7;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    const uint4 v = *(const uint4*)(sH + c * H_BYTES + f * 128 + ((g ^ (f & 7)) * 16));
+    const uint4 v = *(const uint4*)(sH + c * H_BYTES + f * 128 + ((g ^ fsig(f)) * 16));
     *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C + c * 64 + g * 8) * 2) = v;
     if (EPI == EPI_FWD && Lo.mask) {
       auto nz = [](uint32_t x) { return ((x & 0xFFFFu) ? 1u : 0u) | ((x >> 16) ? 2u : 0u); };
@@ -139,6 +151,44 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
           (uint8_t)(nz(v.x) | (nz(v.y) << 2) | (nz(v.z) << 4) | (nz(v.w) << 6));
     }
   };
+
+  auto read_A = [&](const char* sA, int kk, bf16x8 (&af)[MF]) {
+    const int g = kk * 4 + lq;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int row = wm * 64 + i * 16 + lr;
+      af[i] = (ABL & 2) ? bf16x8{}
+              : lds_read_b128((const LDS_AS char*)(sA + row * 128 + ((g ^ (row & 7)) * 16)));
+    }
+  };
+  auto read_B = [&](int s_, int kk, bf16x8 (&bfr)[NF]) {
+    const int c = s_ / T, t = s_ - (s_ / T) * T;
+    const char* sHc = sH + c * H_BYTES;
+    const int toff = (t / 3 - 1) * F + (t % 3 - 1);
+    const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
+    const int g = kk * 4 + lq;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int row = fp[j] + toff;
+      bfr[j] = (ABL & 2) ? bf16x8{}
+               : lds_read_b128((const LDS_AS char*)(sHc + row * 128 +
+                                                   ((g ^ ((fs[j] + tsig) & 7)) * 16)));
+    }
+  };
+  auto mma = [&](const bf16x8 (&af)[MF], const bf16x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+      for (int i = 0; i < MF; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < NF; ++j) asm volatile("" ::"v"(bfr[j]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+  };
+  bf16x8 bpre[NF];
 
   int gs = 0;  // global step
   for (int l = 0; l < a.nl; ++l) {
@@ -149,8 +199,8 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    if constexpr (BPF) read_B(0, 0, bpre);  // image of this layer is ready (barrier)
     for (int s = 0; s < NSTEP; ++s, ++gs) {
-      const int c = s / T, t = s - (s / T) * T;
       // the previous layer's output (already in the image) goes to HBM under this layer's
       // MFMAs: 512 pieces per step over the first 12 steps.  Issued BEFORE the weight DMA:
       // hipcc puts an s_waitcnt vmcnt(0) in front of an LDS read that follows an LDS-DMA
@@ -164,38 +214,22 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       const bool more = gs + AHEAD < total;
       if (more) stage_A(gs + AHEAD);
       const char* sA = sA0 + (gs % NRING) * A_BYTES;
-      const char* sHc = sH + c * H_BYTES;
-      const int toff = (t / 3 - 1) * F + (t % 3 - 1);
-      // one k-half's fragments live at a time (register budget with the copy-out in the
-      // loop); the compiler overlaps half 1's reads with half 0's MFMAs
+      bf16x8 af[MF], bfr[NF];
+      // k-half 0: B fragments were prefetched during the previous step (BPF)
+      read_A(sA, 0, af);
+      if constexpr (BPF) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int g = kk * 4 + lq;
-        bf16x8 af[MF], bfr[NF];
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          const int row = wm * 64 + i * 16 + lr;
-          af[i] = (ABL & 2) ? bf16x8{}
-                  : lds_read_b128((const LDS_AS char*)(sA + row * 128 + ((g ^ (row & 7)) * 16)));
-        }
-#pragma unroll
-        for (int j = 0; j < NF; ++j) {
-          const int row = fp[j] + toff;
-          bfr[j] = (ABL & 2) ? bf16x8{}
-                   : lds_read_b128((const LDS_AS char*)(sHc + row * 128 + ((g ^ (row & 7)) * 16)));
-        }
-        if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-          for (int i = 0; i < MF; ++i) asm volatile("" ::"v"(af[i]));
-#pragma unroll
-          for (int j = 0; j < NF; ++j) asm volatile("" ::"v"(bfr[j]));
-        } else {
-#pragma unroll
-          for (int i = 0; i < MF; ++i)
-#pragma unroll
-            for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-        }
+        for (int j = 0; j < NF; ++j) bfr[j] = bpre[j];
+      } else {
+        read_B(s, 0, bfr);
       }
+      mma(af, bfr, acc);
+      // k-half 1, and the next step's k-half-0 B fragments (the image is resident: no DMA
+      // dependency) issued before these MFMAs so their LDS latency hides under them
+      read_A(sA, 1, af);
+      read_B(s, 1, bfr);
+      if (BPF && s + 1 < NSTEP) read_B(s + 1, 0, bpre);
+      mma(af, bfr, acc);
       __builtin_amdgcn_sched_barrier(0);
       // tile gs+1 must have landed for every wave; the newer tiles (the newest
       // DMA_PER_TILE*(AHEAD-1) VMEM ops of this wave — the copy-out stores precede them)
@@ -234,7 +268,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
         uint2 o;
         o.x = pack_bf16x2(v[0], v[1]);
         o.y = pack_bf16x2(v[2], v[3]);
-        const int slot = (cl >> 3) ^ (f & 7);
+        const int slot = (cl >> 3) ^ (fs[j] & 7);
         *(uint2*)(sH + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
       }
     }
@@ -244,17 +278,18 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   for (int u = tid; u < UNITS; u += 512) copy_out(u, a.L[a.nl - 1]);
 }
 
-template <int EPI, int NRING, int ABL>
+template <int EPI, int NRING, int ABL, bool BPF = true>
 hipError_t launch_stack(const StackArgs& a, int B, hipStream_t stream) {
   constexpr size_t lds = NRING * (size_t)A_BYTES + 2 * (size_t)H_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_kernel<EPI, NRING, ABL>,
+    (void)hipFuncSetAttribute((const void*)conv_stack_kernel<EPI, NRING, ABL, BPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack_kernel<EPI, NRING, ABL>), dim3(B), dim3(512), lds, stream, a);
+  hipLaunchKernelGGL((conv_stack_kernel<EPI, NRING, ABL, BPF>), dim3(B), dim3(512), lds, stream,
+                     a);
   return hipGetLastError();
 }
 
@@ -278,11 +313,13 @@ hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s)
 
 static int g_stack_ablate = 0;
 static int g_stack_ring = 0;  // 0: default (2)
+static int g_stack_bpf = 1;   // B-fragment prefetch across K-steps
 
 extern "C" {
 
 void dg_conv_stack_set_ablate(int mode) { g_stack_ablate = mode; }
 void dg_conv_stack_set_ring(int n) { g_stack_ring = n; }
+void dg_conv_stack_set_bpf(int on) { g_stack_bpf = on; }
 
 // table: nl rows of {A, pbias, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)
@@ -309,6 +346,9 @@ hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0
     return epi == EPI_FWD ? (nring == 3 ? dispatch_ablate<3>(g_stack_ablate, a, B, stream)
                                         : dispatch_ablate<2>(g_stack_ablate, a, B, stream))
                           : hipErrorInvalidValue;
+  if (!g_stack_bpf)
+    return epi == EPI_FWD ? launch_stack<EPI_FWD, 2, 0, false>(a, B, stream)
+                          : launch_stack<EPI_DGRAD, 2, 0, false>(a, B, stream);
   if (epi == EPI_FWD)
     return nring == 3 ? launch_stack<EPI_FWD, 3, 0>(a, B, stream)
                       : launch_stack<EPI_FWD, 2, 0>(a, B, stream);

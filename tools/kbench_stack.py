@@ -59,6 +59,10 @@ def main():
                     round(timeit(run(h.EPI_FWD, tf)), 1))
                 h.conv_stack_set_ablate(0)
         h.conv_stack_set_ring(0)
+        h.conv_stack_set_bpf(0)
+        for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
+            res.setdefault(f"ring2_nobpf_{name}", []).append(round(timeit(run(epi, t)), 1))
+        h.conv_stack_set_bpf(1)
     out = {k: {"us": v, "us_per_layer": round(min(v) / NL, 2),
                "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     out["variants_bit_identical"] = res_ok
