@@ -40,6 +40,9 @@ int dg_conv_wgrad_wgs_per_cu();
 void dg_conv_wgrad_set_t3(int on);
 int dg_conv_wgrad_ktile(int KP);
 int dg_conv_wgrad_wgs_per_cu_for(int KP);
+hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pad, int M,
+                               int Mpad, int x_pad, int x_C, int B, int KP, int splits,
+                               hipStream_t stream);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
@@ -277,6 +280,12 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
   m.def("conv_wgrad_set_t3", [](int on) { dg_conv_wgrad_set_t3(on); },
         "three-slice (128 x 384) wgrad tiles on/off (default on; env DG_WGRAD_T3)");
+  m.def("conv_wgrad_multi", [](int kw, uintptr_t table, int nl, int dz_pad, int M, int Mpad,
+                               int x_pad, int x_C, int B, int KP, int splits, uintptr_t stream) {
+    check(dg_conv_wgrad_multi(kw, P<long long>(table), nl, dz_pad, M, Mpad, x_pad, x_C, B, KP,
+                              splits, S(stream)),
+          "conv_wgrad_multi");
+  }, "weight gradients of several same-shape layers in one three-slice launch");
   m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });
   m.def("conv_wgrad_wgs_per_cu_for", [](int KP) { return dg_conv_wgrad_wgs_per_cu_for(KP); });
   m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });

@@ -227,6 +227,15 @@ struct WgradArgs {
   uint64_t gpt_magic;
   int ablate;  // diagnostics: 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no slab store, 16 no barrier
   int ktiles, mtiles, splits;  // logical grid (launched flat, XCD-remapped)
+  int nlayers;                 // t3 kernel: layers of identical geometry in one launch
+};
+
+// Per-layer operands of a multi-layer weight-gradient launch (conv_wgrad_t3_kernel).
+constexpr int MAXWL = 16;
+struct WgradLayers {
+  const char* dZ[MAXWL];
+  const char* X[MAXWL];
+  float* slab[MAXWL];
 };
 
 DG_DEV int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
@@ -576,7 +585,7 @@ conv_wgrad_ring_kernel(WgradArgs a) {
 // XCD remap and slab layout as conv_wgrad_kernel.
 template <int KW>
 __global__ void __launch_bounds__(512, 1)
-conv_wgrad_t3_kernel(WgradArgs a) {
+conv_wgrad_t3_kernel(WgradArgs a, WgradLayers Ls) {
   constexpr int BKN = 64;
   constexpr int T_BYTES = BKN * 256;           // one 64 x 128 (bf16) tile
   constexpr int STAGE = 4 * T_BYTES;           // dZ tile + 3 X slices
@@ -586,7 +595,7 @@ conv_wgrad_t3_kernel(WgradArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const int nwg = a.ktiles * a.mtiles * a.splits;
+  const int nwg = a.ktiles * a.mtiles * a.splits * a.nlayers;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, xslot = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
@@ -594,7 +603,11 @@ conv_wgrad_t3_kernel(WgradArgs a) {
   const int kt = lid % a.ktiles;
   const int rest = lid / a.ktiles;
   const int mt = rest % a.mtiles;
-  const int zsplit = rest / a.mtiles;
+  const int rest2 = rest / a.mtiles;
+  const int zsplit = rest2 % a.splits;
+  const int layer = rest2 / a.splits;
+  const char* __restrict__ dZl = Ls.dZ[layer];
+  const char* __restrict__ Xl = Ls.X[layer];
   const int k_tile = kt * 384;
   const int m_tile = mt * 128;
   const int n_begin = zsplit * a.px_per_split;
@@ -617,6 +630,7 @@ conv_wgrad_t3_kernel(WgradArgs a) {
   }
 
   auto stage = [&](int buf, int step) {
+    if (a.ablate & 4) return;
     char* sA = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -630,11 +644,11 @@ conv_wgrad_t3_kernel(WgradArgs a) {
       const int w = p - h * BOARD;
       const uint32_t dzo = frame_off(b, h, w, a.dz_pad, a.M);
       const uint32_t xo = frame_off(b, h, w, a.x_pad, a.x_C);
-      const char* src_dz = ok ? (a.dZ + dzo + dz_chunk[i]) : (a.dZ + (slot * 16));
+      const char* src_dz = ok ? (dZl + dzo + dz_chunk[i]) : (dZl + (slot * 16));
       glds16(src_dz, (LDS_AS void*)(sA + (wave * 2 + i) * 1024));
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        glds16(a.X + xo + koffs[j][i],
+        glds16(Xl + xo + koffs[j][i],
                (LDS_AS void*)(sA + (j + 1) * T_BYTES + (wave * 2 + i) * 1024));
     }
   };
@@ -656,6 +670,17 @@ conv_wgrad_t3_kernel(WgradArgs a) {
     const int buf = st & 1;
     const char* sA = smem + buf * STAGE;
     s16x4 ta[2][2][4], tb[2][2][6];
+    if (a.ablate & 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ta[kk][half][i] = s16x4{};
+#pragma unroll
+          for (int j = 0; j < 6; ++j) tb[kk][half][j] = s16x4{};
+        }
+    } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -696,6 +721,12 @@ conv_wgrad_t3_kernel(WgradArgs a) {
         const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[j] = __builtin_bit_cast(bf16x8, v);
       }
+      if (a.ablate & 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < 6; ++j) asm volatile("" ::"v"(bfr[j]));
+      } else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -705,7 +736,16 @@ conv_wgrad_t3_kernel(WgradArgs a) {
     __syncthreads();
   }
 
-  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
+  if (a.ablate & 8) {
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) keep += acc[i][j][0];
+    if (keep == 1234.5f) Ls.slab[layer][0] = keep;
+    return;
+  }
+  float* slab = Ls.slab[layer] + (size_t)zsplit * a.Mpad * a.KP;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -805,6 +845,20 @@ static void allow_lds(K kernel, size_t bytes) {
                               (int)bytes);
     done = true;
   }
+}
+
+static hipError_t launch_t3(int kw, WgradArgs a, const WgradLayers& Ls, hipStream_t stream) {
+  a.ktiles = a.KP / 384;
+  dim3 grid3(a.ktiles * a.mtiles * a.splits * a.nlayers);
+  constexpr size_t lds3 = 2 * 4 * 64 * 256;
+  if (kw == 3) {
+    allow_lds(conv_wgrad_t3_kernel<3>, lds3);
+    hipLaunchKernelGGL(conv_wgrad_t3_kernel<3>, grid3, dim3(512), lds3, stream, a, Ls);
+  } else {
+    allow_lds(conv_wgrad_t3_kernel<5>, lds3);
+    hipLaunchKernelGGL(conv_wgrad_t3_kernel<5>, grid3, dim3(512), lds3, stream, a, Ls);
+  }
+  return hipGetLastError();
 }
 
 template <int KW, int MF, int NF, int EPI>
@@ -930,18 +984,13 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
   a.ktiles = KP / 128;
   a.mtiles = Mpad / 128;
   a.splits = splits;
+  a.nlayers = 1;
   if (dg_conv_wgrad_ktile(KP) == 384 && (kw == 3 || kw == 5)) {
-    a.ktiles = KP / 384;
-    dim3 grid3(a.ktiles * a.mtiles * splits);
-    constexpr size_t lds3 = 2 * 4 * 64 * 256;
-    if (kw == 3) {
-      allow_lds(conv_wgrad_t3_kernel<3>, lds3);
-      hipLaunchKernelGGL(conv_wgrad_t3_kernel<3>, grid3, dim3(512), lds3, stream, a);
-    } else {
-      allow_lds(conv_wgrad_t3_kernel<5>, lds3);
-      hipLaunchKernelGGL(conv_wgrad_t3_kernel<5>, grid3, dim3(512), lds3, stream, a);
-    }
-    return hipGetLastError();
+    WgradLayers Ls{};
+    Ls.dZ[0] = a.dZ;
+    Ls.X[0] = a.X;
+    Ls.slab[0] = a.slab;
+    return launch_t3(kw, a, Ls, stream);
   }
   dim3 grid(a.ktiles * a.mtiles * splits);
   if (wgrad_ring_enabled() && (kw == 3 || kw == 5)) {
@@ -961,6 +1010,48 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// Weight gradients of nl layers of identical geometry in ONE launch (three-slice tiles):
+// table = nl rows of {dZ frame, X frame, slab} pointers; each layer gets `splits` pixel
+// splits.  Fewer splits per layer than a one-layer launch at the same machine fill, so
+// proportionally fewer fp32 partial slabs to write and reduce.
+hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pad, int M,
+                               int Mpad, int x_pad, int x_C, int B, int KP, int splits,
+                               hipStream_t stream) {
+  const int Npix = B * NPTS;
+  if (nl <= 0 || nl > MAXWL || KP % 384 != 0 || Mpad % 128 != 0 || x_C % 8 != 0 ||
+      M % 8 != 0 || splits <= 0 || (kw != 3 && kw != 5))
+    return hipErrorInvalidValue;
+  WgradArgs a{};
+  a.dz_pad = dz_pad;
+  a.M = M;
+  a.Mpad = Mpad;
+  a.KP = KP;
+  a.Npix = Npix;
+  int per = (Npix + splits - 1) / splits;
+  a.px_per_split = (per + 63) / 64 * 64;
+  a.x_pad = x_pad;
+  a.x_C = x_C;
+  a.gpt = x_C / 8;
+  a.ngroups = kw * kw * a.gpt;
+  a.gpt_magic = magic_for(a.gpt);
+  a.ablate = g_wgrad_ablate;
+  if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
+  a.mtiles = Mpad / 128;
+  a.splits = splits;
+  a.nlayers = nl;
+  WgradLayers Ls{};
+  for (int i = 0; i < nl; ++i) {
+    Ls.dZ[i] = (const char*)table[3 * i];
+    Ls.X[i] = (const char*)table[3 * i + 1];
+    Ls.slab[i] = (float*)table[3 * i + 2];
+    if (!Ls.dZ[i] || !Ls.X[i] || !Ls.slab[i]) return hipErrorInvalidValue;
+  }
+  a.dZ = Ls.dZ[0];
+  a.X = Ls.X[0];
+  a.slab = Ls.slab[0];
+  return launch_t3(kw, a, Ls, stream);
 }
 
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,

@@ -410,6 +410,7 @@ class HipGoNet:
         per-layer dgrad launches of those layers are dropped from ``_bwd``; their weight
         gradients run afterwards (they only read dZ_i).  DG_DSTACK=0 keeps per-layer dgrads."""
         self.dstack: List[int] = []
+        self.wgroups: List[List[int]] = []
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         if os.environ.get("DG_DSTACK", "1") == "0":
             return
@@ -436,6 +437,84 @@ class HipGoNet:
                                                   self.plans[run[0]].KPd, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
             self._bwd[i] = self._bwd[i][:3]
+        self._group_wgrads(set([run[0]] + [i - 1 for i in run]))
+
+    @staticmethod
+    def _noop(*_):
+        pass
+
+    def _group_wgrads(self, dz_ready):
+        """Weight gradients of up to DG_WGRAD_GROUP (default 5) consecutive same-shape
+        layers whose dZ the dgrad stack has already produced run as ONE three-slice launch
+        (conv_wgrad_multi).  The machine is filled by the layers instead of by pixel
+        splits, so each layer is cut into ~5x fewer splits: ~5x fewer fp32 partial slabs
+        to write and reduce (50 -> 10 MB per 128-channel layer)."""
+        self.wgroups: List[List[int]] = []
+        G = int(os.environ.get("DG_WGRAD_GROUP", "5"))
+        if G < 2 or self.side_mode != "none":
+            return
+        lay = self.layout.layers
+        h = self.h
+
+        def key(i):
+            p = self.plans[i]
+            if (i not in dz_ready or p.wgrad3 or p.k not in (3, 5)
+                    or h.conv_wgrad_ktile(p.KPw) != 384):
+                return None
+            return (p.k, p.cout, p.Mpad_w, p.KPw, p.cinp, lay[i].pad)
+        groups, cur = [], []
+        for i in range(len(self.plans) - 1, -1, -1):
+            k = key(i)
+            if cur and (k is None or k != key(cur[0]) or len(cur) == G):
+                groups.append(cur)
+                cur = []
+            if k is not None:
+                cur.append(i)
+        if cur:
+            groups.append(cur)
+        groups = [g for g in groups if len(g) >= 2]
+        if not groups:
+            return
+        self.wgroups = groups
+        wgs = h.conv_wgrad_wgs_per_cu_for(self.plans[groups[0][0]].KPw)
+        gslab_elems = 0
+        plan_splits = {}
+        for g in groups:
+            p = self.plans[g[0]]
+            tiles = (p.KPw // 384) * (p.Mpad_w // 128) * len(g)
+            S = max(1, min((self.num_cus * wgs) // tiles, self.npix // 256))
+            plan_splits[tuple(g)] = S
+            gslab_elems = max(gslab_elems, len(g) * S * p.Mpad_w * p.KPw)
+        self.gslab = torch.empty(gslab_elems, dtype=torch.float32, device=self.device)
+        G_ = self.grads.data_ptr()
+        f4 = 4
+        self._wgroup_tables = []
+        for g in groups:
+            S = plan_splits[tuple(g)]
+            p0 = self.plans[g[0]]
+            per = S * p0.Mpad_w * p0.KPw
+            rows = []
+            for j, i in enumerate(g):
+                xin = self.x0 if i == 0 else self.act[i - 1]
+                slab = self.gslab.data_ptr() + 4 * j * per
+                rows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
+                spec = lay[i]
+                p = self.plans[i]
+                p.splits = S
+                ops = self._bwd[i]
+                # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
+                # launches the whole group; the reduces read their layer's slab
+                ops[1] = (self._noop, ())
+                ops[2] = (h.wgrad_reduce, (slab, G_ + spec.w_off * f4, S, p.cout, p.Mpad_w,
+                                           p.KPw, p.k * p.k, p.cin, p.cinp,
+                                           self.bparts[i].data_ptr(), self.bchunks,
+                                           G_ + spec.pos_off * f4, G_ + spec.b_off * f4))
+            tab = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+            self._wgroup_tables.append(tab)
+            spec0 = lay[g[0]]
+            self._bwd[g[0]][1] = (h.conv_wgrad_multi, (
+                p0.k, tab.ctypes.data, len(g), max(1, spec0.pad), p0.cout, p0.Mpad_w,
+                spec0.pad, p0.cinp, self.B, p0.KPw, S))
 
     # ------------------------------------------------------------------ execution
     @staticmethod

@@ -167,6 +167,22 @@ def test_fused_dgrad_stack_matches_per_layer(layers, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.parametrize("layers,group", [(7, 5), (9, 3), (6, 2)])
+def test_grouped_wgrads_match_per_layer(layers, group, monkeypatch):
+    """conv_wgrad_multi (several layers' weight gradients in one launch, fewer pixel splits
+    per layer) gives the per-layer launches' gradients up to fp32 summation order."""
+    monkeypatch.setenv("DG_WGRAD_GROUP", "1")
+    _, n0, _ = _setup(layers, 128, 6, seed=11)
+    monkeypatch.setenv("DG_WGRAD_GROUP", str(group))
+    _, n1, _ = _setup(layers, 128, 6, seed=11)
+    assert not n0.wgroups and n1.wgroups and max(len(g) for g in n1.wgroups) <= group
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(n0.loss, n1.loss)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-4, atol=1e-7)
+
+
 def test_board_tiled_first_layer_option(monkeypatch):
     """DG_L1_BOARD=1: 5x5 first layer on the board kernel over a 64-channel input copy
     (measured slower than the pixel-tiled kernel at K 1600 vs 1000; kept as an option)."""
