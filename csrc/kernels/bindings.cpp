@@ -63,6 +63,11 @@ hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad, const voi
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int splits, int M, int Mpad,
+                                 int KP, int taps, int cin, int cinp, int bchunks,
+                                 hipStream_t stream);
+hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
+                                      hipStream_t s);
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
                            float* gposb, float* gbias, hipStream_t stream);
@@ -194,6 +199,17 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_frame_to_fp8(P<void>(src), P<void>(dst), n, P<float>(scale), P<unsigned>(amax),
                           S(stream)),
           "frame_to_fp8");
+  });
+  m.def("wgrad_reduce_multi", [](uintptr_t table, int nl, int splits, int M, int Mpad, int KP,
+                                 int taps, int cin, int cinp, int bchunks, uintptr_t stream) {
+    check(dg_wgrad_reduce_multi(P<long long>(table), nl, splits, M, Mpad, KP, taps, cin, cinp,
+                                bchunks, S(stream)),
+          "wgrad_reduce_multi");
+  });
+  m.def("bias_grad_partial_multi", [](uintptr_t table, int nl, int B, int C, int pad,
+                                      uintptr_t stream) {
+    check(dg_bias_grad_partial_multi(P<long long>(table), nl, B, C, pad, S(stream)),
+          "bias_grad_partial_multi");
   });
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,

@@ -765,11 +765,23 @@ conv_wgrad_t3_kernel(WgradArgs a, WgradLayers Ls) {
 // consecutive k of one co (16-byte slab loads), the split loop is unrolled by 4 so
 // several loads are in flight; the slabs are normally still resident in the Infinity
 // Cache when this runs.
+constexpr int RD_MAXL = 16;
+struct ReduceLayers {  // blockIdx.y = layer (several same-shape layers in one launch)
+  const float* slab[RD_MAXL];
+  float* out[RD_MAXL];
+  const float* bpart[RD_MAXL];
+  float* gposb[RD_MAXL];
+  float* gbias[RD_MAXL];
+};
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits, int M,
-                    int Mpad, int KP, int taps, int cin, int cinp, const float* __restrict__ bpart,
-                    int bchunks, float* __restrict__ gposb, float* __restrict__ gbias,
-                    int main_blocks) {
+wgrad_reduce_kernel(ReduceLayers Ls, int splits, int M, int Mpad, int KP, int taps, int cin,
+                    int cinp, int bchunks, int main_blocks) {
+  const int ly = blockIdx.y;
+  const float* __restrict__ slab = Ls.slab[ly];
+  float* __restrict__ out = Ls.out[ly];
+  const float* __restrict__ bpart = Ls.bpart[ly];
+  float* __restrict__ gposb = Ls.gposb[ly];
+  float* __restrict__ gbias = Ls.gbias[ly];
   const int pos_blocks = (NPTS * M + 255) / 256;
   if ((int)blockIdx.x >= main_blocks + pos_blocks) {
     // gbias[c] = sum over (chunk, row) of rowpart; one workgroup per channel
@@ -1061,8 +1073,38 @@ hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int
   int blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   const int extra = bpart ? (NPTS * M + 255) / 256 + M : 0;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra), dim3(256), 0, stream, slab, out,
-                     splits, M, Mpad, KP, taps, cin, cinp, bpart, bchunks, gposb, gbias, blocks);
+  ReduceLayers Ls{};
+  Ls.slab[0] = slab;
+  Ls.out[0] = out;
+  Ls.bpart[0] = bpart;
+  Ls.gposb[0] = gposb;
+  Ls.gbias[0] = gbias;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra, 1), dim3(256), 0, stream, Ls,
+                     splits, M, Mpad, KP, taps, cin, cinp, bchunks, blocks);
+  return hipGetLastError();
+}
+
+// Slab reduce + bias-gradient pass 2 of nl same-shape layers in one launch: table = nl
+// rows of {slab, out (weight grad), bpart, gposb, gbias}.
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int splits, int M, int Mpad,
+                                 int KP, int taps, int cin, int cinp, int bchunks,
+                                 hipStream_t stream) {
+  if (nl <= 0 || nl > RD_MAXL) return hipErrorInvalidValue;
+  const int total = M * (KP / 4);
+  int blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  ReduceLayers Ls{};
+  for (int i = 0; i < nl; ++i) {
+    Ls.slab[i] = (const float*)table[5 * i];
+    Ls.out[i] = (float*)table[5 * i + 1];
+    Ls.bpart[i] = (const float*)table[5 * i + 2];
+    Ls.gposb[i] = (float*)table[5 * i + 3];
+    Ls.gbias[i] = (float*)table[5 * i + 4];
+    if (!Ls.slab[i] || !Ls.out[i] || !Ls.bpart[i]) return hipErrorInvalidValue;
+  }
+  const int extra = (NPTS * M + 255) / 256 + M;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra, nl), dim3(256), 0, stream, Ls,
+                     splits, M, Mpad, KP, taps, cin, cinp, bchunks, blocks);
   return hipGetLastError();
 }
 

@@ -82,12 +82,18 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
 // (sum over chunks -> gposb, gbias) runs inside the wgrad slab-reduce launch.
 // Reference: nn.Add / conv bias backward (experiments.lua:138,144).
 constexpr int BG_BT = 16;
+constexpr int BG_MAXL = 16;
+struct BiasLayers {  // blockIdx.z = layer (several same-shape layers in one launch)
+  const char* dZ[BG_MAXL];
+  float* part[BG_MAXL];
+};
 __global__ void __launch_bounds__(1024)
-bias_grad_partial_kernel(const char* __restrict__ dZ, int B, int C, int pad,
-                         float* __restrict__ part, int nchunks) {
+bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
   const int h = blockIdx.x;
   const int chunk = blockIdx.y;
+  const char* __restrict__ dZ = Ls.dZ[blockIdx.z];
+  float* __restrict__ part = Ls.part[blockIdx.z];
   const int b0 = chunk * BG_BT;
   const int G = C / 8;
   const int F = BOARD + 2 * pad;
@@ -296,9 +302,29 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
   int threads = (BOARD * (C / 8) + 63) / 64 * 64;  // one item per thread (19*C/8)
   if (threads > 1024) threads = 1024;
   if (threads < 64) threads = 64;
-  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks), dim3(threads),
-                     (size_t)BOARD * C * sizeof(float), s, (const char*)dZ, B, C, pad, part,
-                     nchunks);
+  BiasLayers Ls{};
+  Ls.dZ[0] = (const char*)dZ;
+  Ls.part[0] = part;
+  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, 1), dim3(threads),
+                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
+  return hipGetLastError();
+}
+
+// Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part}.
+hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
+                                      hipStream_t s) {
+  if (C % 8 != 0 || C > 2048 || nl <= 0 || nl > BG_MAXL) return hipErrorInvalidValue;
+  const int nchunks = (B + BG_BT - 1) / BG_BT;
+  int threads = (BOARD * (C / 8) + 63) / 64 * 64;
+  if (threads > 1024) threads = 1024;
+  if (threads < 64) threads = 64;
+  BiasLayers Ls{};
+  for (int i = 0; i < nl; ++i) {
+    Ls.dZ[i] = (const char*)table[2 * i];
+    Ls.part[i] = (float*)table[2 * i + 1];
+  }
+  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, nl), dim3(threads),
+                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
   return hipGetLastError();
 }
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }

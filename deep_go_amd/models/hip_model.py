@@ -486,35 +486,43 @@ class HipGoNet:
             plan_splits[tuple(g)] = S
             gslab_elems = max(gslab_elems, len(g) * S * p.Mpad_w * p.KPw)
         self.gslab = torch.empty(gslab_elems, dtype=torch.float32, device=self.device)
+        bpart_per = self.bchunks * (NUM_POINTS + 19) * max(self.plans[g[0]].cout for g in groups)
+        self.gbpart = torch.empty(G * bpart_per, dtype=torch.float32, device=self.device)
         G_ = self.grads.data_ptr()
         f4 = 4
         self._wgroup_tables = []
         for g in groups:
             S = plan_splits[tuple(g)]
             p0 = self.plans[g[0]]
+            spec0 = lay[g[0]]
             per = S * p0.Mpad_w * p0.KPw
-            rows = []
+            wrows, brows, rrows = [], [], []
             for j, i in enumerate(g):
                 xin = self.x0 if i == 0 else self.act[i - 1]
                 slab = self.gslab.data_ptr() + 4 * j * per
-                rows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
+                bpart = self.gbpart.data_ptr() + 4 * j * bpart_per
                 spec = lay[i]
-                p = self.plans[i]
-                p.splits = S
-                ops = self._bwd[i]
+                wrows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
+                brows.append([self.dz[i].data_ptr(), bpart])
+                rrows.append([slab, G_ + spec.w_off * f4, bpart, G_ + spec.pos_off * f4,
+                              G_ + spec.b_off * f4])
+                self.plans[i].splits = S
                 # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
-                # launches the whole group; the reduces read their layer's slab
-                ops[1] = (self._noop, ())
-                ops[2] = (h.wgrad_reduce, (slab, G_ + spec.w_off * f4, S, p.cout, p.Mpad_w,
-                                           p.KPw, p.k * p.k, p.cin, p.cinp,
-                                           self.bparts[i].data_ptr(), self.bchunks,
-                                           G_ + spec.pos_off * f4, G_ + spec.b_off * f4))
-            tab = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-            self._wgroup_tables.append(tab)
-            spec0 = lay[g[0]]
-            self._bwd[g[0]][1] = (h.conv_wgrad_multi, (
-                p0.k, tab.ctypes.data, len(g), max(1, spec0.pad), p0.cout, p0.Mpad_w,
-                spec0.pad, p0.cinp, self.B, p0.KPw, S))
+                # launches all three passes for the whole group
+                self._bwd[i][0:3] = [(self._noop, ())] * 3
+            tabs = [np.ascontiguousarray(np.array(r, dtype=np.int64))
+                    for r in (wrows, brows, rrows)]
+            self._wgroup_tables.extend(tabs)
+            wt, bt, rt = tabs
+            self._bwd[g[0]][0:3] = [
+                (h.bias_grad_partial_multi, (bt.ctypes.data, len(g), self.B, p0.cout,
+                                             max(1, spec0.pad))),
+                (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), max(1, spec0.pad),
+                                      p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
+                                      S)),
+                (h.wgrad_reduce_multi, (rt.ctypes.data, len(g), S, p0.cout, p0.Mpad_w, p0.KPw,
+                                        p0.k * p0.k, p0.cin, p0.cinp, self.bchunks)),
+            ]
 
     # ------------------------------------------------------------------ execution
     @staticmethod
