@@ -14,6 +14,10 @@
 namespace py = pybind11;
 
 extern "C" {
+hipError_t dg_conv_nt_ex(int epi, int kw, int bm, int bn, const void* A, int KP, int M,
+                         int Mpad, const void* X, int x_pad, int x_C, int Npix, void* Y,
+                         int y_pad, const float* bias, const float* posb, const void* aux,
+                         int aux_pad, void* mask, hipStream_t stream);
 hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, int M, int Mpad,
                       const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
                       const float* bias, const float* posb, const void* aux, int aux_pad,
@@ -133,6 +137,16 @@ PYBIND11_MODULE(_dghip, m) {
                               aux_pad, S(stream)),
                 "conv_board");
         });
+  m.def("conv_nt_ex",
+        [](int epi, int kw, int bm, int bn, uintptr_t A, int KP, int M, int Mpad, uintptr_t X,
+           int x_pad, int x_C, int Npix, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
+           uintptr_t aux, int aux_pad, uintptr_t mask, uintptr_t stream) {
+          check(dg_conv_nt_ex(epi, kw, bm, bn, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C,
+                              Npix, P<void>(Y), y_pad, P<float>(bias), P<float>(posb),
+                              P<void>(aux), aux_pad, P<void>(mask), S(stream)),
+                "conv_nt_ex");
+        },
+        "conv_nt + optional ReLU bitmask output (EPI_FWD)");
   m.def("conv_board_ex",
         [](int epi, int kw, int bm, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
            int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,

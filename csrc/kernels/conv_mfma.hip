@@ -48,6 +48,7 @@ struct ConvNTArgs {
   int ngroups;         // valid k-groups = KW*KW*x_C/8
   int gpt;             // k-groups per tap = x_C/8
   uint64_t gpt_magic;  // fastdiv magic for gpt
+  uint8_t* mask;       // EPI_FWD (optional): ReLU bitmask [Npix][M/8], bit k = channel 8q+k
 };
 
 // Byte offset (relative to the pixel centre) of k-group kg.
@@ -179,6 +180,28 @@ conv_nt_kernel(ConvNTArgs a) {
   }
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
+    if constexpr (EPI == EPI_FWD) {
+      // ReLU bitmask (what the board dgrad / dgrad stack gate with): lanes l and l ^ 16
+      // hold channels co..co+3 and co+4..co+7 of the same pixel -> one byte; computed by
+      // every lane before the divergent stores below (the shuffle needs them all)
+      if (a.mask) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int co = m_tile + wm * MF * 16 + i * 16 + lq * 4;
+          const int coc = co < a.M ? co : 0;
+          uint32_t nib = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = fmaxf(acc[i][j][r] + bias_v[i][r] + pos_v[j][i][r], 0.f);
+            nib |= (f2bf(y) != 0 ? 1u : 0u) << r;
+          }
+          const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 16, 64);
+          if (!(lq & 1) && pb_[j] >= 0 && co < a.M)
+            a.mask[(size_t)(bb_[j] * NPTS + pb_[j]) * (a.M >> 3) + (coc >> 3)] =
+                (uint8_t)(nib | (hi << 4));
+        }
+      }
+    }
     if (pb_[j] < 0) continue;
     const int b = bb_[j];
     const int p = pb_[j];
@@ -905,10 +928,10 @@ static hipError_t dispatch_tile(int epi, const ConvNTArgs& a, int Mpad, int bm, 
 extern "C" {
 
 // Conv (forward / dgrad / linear) via the NT implicit-GEMM kernel.
-hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, int M, int Mpad,
-                      const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
-                      const float* bias, const float* posb, const void* aux, int aux_pad,
-                      hipStream_t stream) {
+hipError_t dg_conv_nt_ex(int epi, int kw, int bm, int bn, const void* A, int KP, int M,
+                         int Mpad, const void* X, int x_pad, int x_C, int Npix, void* Y,
+                         int y_pad, const float* bias, const float* posb, const void* aux,
+                         int aux_pad, void* mask, hipStream_t stream) {
   if (KP % 64 != 0 || x_C % 8 != 0 || M % 4 != 0 || Mpad % bm != 0 || Npix <= 0)
     return hipErrorInvalidValue;
   ConvNTArgs a;
@@ -928,6 +951,8 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
   a.gpt = x_C / 8;
   a.ngroups = kw * kw * a.gpt;
   a.gpt_magic = magic_for(a.gpt);
+  a.mask = (uint8_t*)mask;
+  if (mask && (epi != EPI_FWD || M % 8 != 0)) return hipErrorInvalidValue;
   if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
   switch (kw) {
     case 1: return dispatch_tile<1>(epi, a, Mpad, bm, bn, stream);
@@ -935,6 +960,14 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
     case 5: return dispatch_tile<5>(epi, a, Mpad, bm, bn, stream);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, int M, int Mpad,
+                      const void* X, int x_pad, int x_C, int Npix, void* Y, int y_pad,
+                      const float* bias, const float* posb, const void* aux, int aux_pad,
+                      hipStream_t stream) {
+  return dg_conv_nt_ex(epi, kw, bm, bn, A, KP, M, Mpad, X, x_pad, x_C, Npix, Y, y_pad, bias,
+                       posb, aux, aux_pad, nullptr, stream);
 }
 
 static int g_wgrad_ablate = 0;

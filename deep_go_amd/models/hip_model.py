@@ -159,7 +159,11 @@ class HipGoNet:
         # act[i]: output of layer i, framed with the pad of layer i+1
         self.act = [LY.alloc_frame(B, L[i].cout, pads[i + 1], dev) for i in range(self.L - 1)]
         # dz[i]: d loss / d pre-activation of layer i, framed with layer i's pad (>=1)
-        self.dz = [LY.alloc_frame(B, L[i].cout, max(1, pads[i]), dev) for i in range(self.L - 1)]
+        # (layer i's dgrad reads dz[i] with its own taps: halo = pad_i; layer 0 has no dgrad,
+        # so dz[0] keeps pad 1 whatever the first layer's kernel size — the 21x21 geometry
+        # of the board-resident dgrad stack)
+        self.dzp = [max(1, pads[i]) if i > 0 else 1 for i in range(self.L - 1)]
+        self.dz = [LY.alloc_frame(B, L[i].cout, self.dzp[i], dev) for i in range(self.L - 1)]
         # fp8 shadow of the input frame of every fp8 layer (same geometry, 1 byte/elem);
         # per conv layer l: scales[2l] = s_w, scales[2l+1] = s_y (scale of act[l]'s fp8
         # shadow), amax[l] = observed max of act[l] (float bits), delayed scaling
@@ -175,7 +179,12 @@ class HipGoNet:
         self.relu_mask = [None] * len(self.plans)
         for p in self.plans[:-1]:
             nxt = self.plans[p.index + 1]
-            if p.board and nxt.board_d and os.environ.get("DG_RELU_MASK", "1") == "1":
+            # board forwards write the bitmask; the pixel-tiled first layer can too
+            # (conv_nt_ex), but its byte stores cost +13 us vs the ~5 us the dgrad stack then
+            # saves on layer 1 (measured): DG_L0_MASK=1 opts in
+            l0 = p.index == 0 and os.environ.get("DG_L0_MASK", "0") == "1"
+            if ((p.board or l0) and nxt.board_d
+                    and os.environ.get("DG_RELU_MASK", "1") == "1"):
                 self.relu_mask[p.index] = torch.zeros((B, NUM_POINTS, p.cout // 8),
                                                       dtype=torch.uint8, device=dev)
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
@@ -295,11 +304,13 @@ class HipGoNet:
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
                     msk.data_ptr() if msk is not None else 0)))
             else:
-                self._fwd.append((h.conv_nt, (h.EPI_FWD, p.k, p.bm, p.bn,
-                                              self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
-                                              xin.data_ptr(), x_pad, p.cinp, self.npix,
-                                              self.act[p.index].data_ptr(), y_pad,
-                                              P + spec.b_off * f4, P + spec.pos_off * f4, 0, 0)))
+                msk = self.relu_mask[p.index]
+                self._fwd.append((h.conv_nt_ex, (h.EPI_FWD, p.k, p.bm, p.bn,
+                                                 self.wf[p.index].data_ptr(), p.KP, p.cout,
+                                                 p.Mpad, xin.data_ptr(), x_pad, p.cinp,
+                                                 self.npix, self.act[p.index].data_ptr(), y_pad,
+                                                 P + spec.b_off * f4, P + spec.pos_off * f4, 0,
+                                                 0, msk.data_ptr() if msk is not None else 0)))
             if nxt is not None and nxt.fp8 and not p.fp8:
                 # bf16 producer feeding an fp8 layer: quantize its output frame
                 i = p.index
@@ -314,7 +325,7 @@ class HipGoNet:
                                      P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
                                      self.labels.data_ptr(), self.loss.data_ptr(),
                                      self.pred.data_ptr(), 0, self.dz[-1].data_ptr(),
-                                     max(1, lay.layers[-2].pad), self.head_gw_part.data_ptr(),
+                                     self.dzp[-1], self.head_gw_part.data_ptr(),
                                      0, self.head_dzb.data_ptr(),
                                      int(self.cfg.head_relu), 1.0 / self.global_batch))
         self._head_red = (h.head_reduce, (self.head_dzb.data_ptr(), self.head_gw_part.data_ptr(),
@@ -329,7 +340,7 @@ class HipGoNet:
             spec = lay.layers[p.index]
             i = p.index
             ops = []
-            dzp = max(1, spec.pad)
+            dzp = self.dzp[i]
             xin = self.x0 if i == 0 else self.act[i - 1]
             # bias grads: pass 1 (per board-chunk partials); pass 2 runs inside the slab
             # reduce launch, which also finalises the weight grad
@@ -355,14 +366,14 @@ class HipGoNet:
                     ops.append((h.conv_board_ex, (
                         h.EPI_DGRAD, p.k, p.bm_d, self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
                         self.dz[i].data_ptr(), dzp, p.cout, self.B, self.dz[i - 1].data_ptr(),
-                        max(1, prev.pad), 0, 0, 0,
+                        self.dzp[i - 1], 0, 0, 0,
                         0 if msk is not None else self.act[i - 1].data_ptr(), spec.pad,
                         msk.data_ptr() if msk is not None else 0)))
                 else:
                     ops.append((h.conv_nt, (h.EPI_DGRAD, p.k, p.bm_d, p.bn_d,
                                             self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
                                             self.dz[i].data_ptr(), dzp, p.cout, self.npix,
-                                            self.dz[i - 1].data_ptr(), max(1, prev.pad), 0, 0,
+                                            self.dz[i - 1].data_ptr(), self.dzp[i - 1], 0, 0,
                                             self.act[i - 1].data_ptr(), spec.pad)))
             self._bwd.append(ops)
         self._fuse_dgrad_stack()
@@ -419,7 +430,7 @@ class HipGoNet:
         def ok(i):
             p = self.plans[i]
             return (i > 0 and p.board_d and p.k == 3 and p.cin == 128 and p.cout == 128
-                    and L[i].pad == 1 and max(1, L[i - 1].pad) == 1 and p.KPd == p.KP
+                    and L[i].pad == 1 and self.dzp[i - 1] == 1 and p.KPd == p.KP
                     and self.relu_mask[i - 1] is not None)
         run = []
         for i in range(len(self.plans) - 1, 0, -1):   # must start at the top hidden layer
@@ -516,8 +527,8 @@ class HipGoNet:
             wt, bt, rt = tabs
             self._bwd[g[0]][0:3] = [
                 (h.bias_grad_partial_multi, (bt.ctypes.data, len(g), self.B, p0.cout,
-                                             max(1, spec0.pad))),
-                (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), max(1, spec0.pad),
+                                             self.dzp[g[0]])),
+                (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
                                       S)),
                 (h.wgrad_reduce_multi, (rt.ctypes.data, len(g), S, p0.cout, p0.Mpad_w, p0.KPw,

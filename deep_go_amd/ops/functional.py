@@ -46,6 +46,30 @@ def conv_forward(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: st
     return LY.from_frame(yf, 1, cout)
 
 
+def conv_nt_mask(x: torch.Tensor, w: torch.Tensor, bias, posb):
+    """Pixel-tiled forward that also writes the ReLU bitmask [B][361][Cout/8] (bit k of
+    byte q = channel 8q + k > 0).  Returns (NCHW output, mask)."""
+    h = hip()
+    dev = w.device
+    B, cin = x.shape[:2]
+    cout, k, _, _ = w.shape
+    pad = (k - 1) // 2
+    cinp = LY.round_up(cin, 8)
+    npix = B * NPTS
+    bm, bn = LY.pick_tiles(npix, cout)
+    KP, _, Mpad = LY.conv_dims(k, cinp, cout, bm)
+    xf = LY.to_frame(x.to(dev), pad, cinp)
+    yf = LY.alloc_frame(B, cout, 1, dev)
+    mask = torch.zeros(B, NPTS, cout // 8, dtype=torch.uint8, device=dev)
+    A = LY.fwd_weight(w.float(), cinp, KP, Mpad)
+    bias = bias.float().contiguous().to(dev)
+    posb = posb.float().contiguous().to(dev)
+    h.conv_nt_ex(h.EPI_FWD, k, bm, bn, A.data_ptr(), KP, cout, Mpad, xf.data_ptr(), pad, cinp,
+                 npix, yf.data_ptr(), 1, bias.data_ptr(), posb.data_ptr(), 0, 0,
+                 mask.data_ptr(), stream_handle())
+    return LY.from_frame(yf, 1, cout), mask
+
+
 def conv_board(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: str = "fwd",
                aux=None) -> torch.Tensor:
     """Board-tiled kernel (1x1/3x3, Cin % 64 == 0).  epi='fwd'|'linear' as conv_forward;

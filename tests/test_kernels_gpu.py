@@ -88,6 +88,23 @@ def test_conv_board_forward(B, cin, cout, k, bm, monkeypatch):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 40, 128, 5), (2, 37, 64, 5), (5, 64, 128, 3)])
+def test_conv_nt_relu_mask(B, cin, cout, k):
+    """The pixel-tiled forward (first layer) writes the same ReLU bitmask layout as the
+    board kernels: bit = bf16 output != 0."""
+    torch.manual_seed(8)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = torch.randn(cout, k, k, cin, device=DEV) / (k * cin ** 0.5)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y, mask = Fn.conv_nt_mask(x, w, b, pb)
+    assert torch.equal(y, Fn.conv_forward(x, w, b, pb, tiles=None))
+    bits = torch.stack([(mask >> e) & 1 for e in range(8)], -1).reshape(B, 361, cout)
+    ref = (y.permute(0, 2, 3, 1).reshape(B, 361, cout) != 0).to(bits.dtype)
+    assert torch.equal(bits, ref)
+
+
 @pytest.mark.parametrize("bm", [64, 128])
 def test_conv_board_pbias_and_relu_mask(bm):
     """Forward with the combined bf16 bias table writes the ReLU bitmask; dgrad gated by the

@@ -148,16 +148,18 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.parametrize("l0_mask", ["0", "1"])
 @pytest.mark.parametrize("layers", [5, 7])
-def test_fused_dgrad_stack_matches_per_layer(layers, monkeypatch):
+def test_fused_dgrad_stack_matches_per_layer(layers, l0_mask, monkeypatch):
     """conv_stack in EPI_DGRAD mode (the backward-data chain of the hidden layers in one
     board-resident launch) runs the per-layer board dgrad's exact MFMA sequence and ReLU-mask
     gating: every dZ frame is bit-identical."""
     monkeypatch.setenv("DG_DSTACK", "0")
     _, n0, _ = _setup(layers, 128, 5, seed=9)
     monkeypatch.setenv("DG_DSTACK", "1")
+    monkeypatch.setenv("DG_L0_MASK", l0_mask)  # "1": layer 0 writes a bitmask -> down to 1
     _, n1, _ = _setup(layers, 128, 5, seed=9)
-    assert not n0.dstack and n1.dstack == list(range(layers - 2, 1, -1))
+    assert not n0.dstack and n1.dstack == list(range(layers - 2, 0 if l0_mask == "1" else 1, -1))
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
