@@ -77,6 +77,7 @@ hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int
                            float* gposb, float* gbias, hipStream_t stream);
 hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n, float* gw,
                           float* gbias, float* gposb, hipStream_t stream);
+void dg_head_set_mfma(int on);
 hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                    const float* bias, const float* posb, const int* labels, float* loss,
                    int* pred, float* logp_out, void* dZ, int dz_pad, float* gw_part,
@@ -300,6 +301,8 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_stack_set_ablate", [](int mode) { dg_conv_stack_set_ablate(mode); },
         "timing ablations of conv_stack (forward): 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no"
         " copy-out, 16 no barrier");
+  m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },
+        "3x3/128-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
   m.def("conv_stack_set_bpf", [](int on) { dg_conv_stack_set_bpf(on); },
         "B-fragment prefetch across K-steps in conv_stack (default on)");
   m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },

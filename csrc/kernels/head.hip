@@ -13,6 +13,8 @@
 // and the weight-gradient partials all read it from LDS.  Lane mapping: 16 lanes cover
 // the 16 8-channel groups of one pixel (256 contiguous bytes -> conflict-free
 // ds_read_b128), 4 pixels per wave.
+#include <stdlib.h>
+
 #include "dg_common.h"
 
 using namespace dg;
@@ -389,12 +391,27 @@ static void allow_lds_once(K kernel, size_t bytes) {
   }
 }
 
+extern "C" hipError_t dg_head_mfma(const void* X, int B, const float* w, const float* bias,
+                                   const float* posb, const int* labels, float* loss, int* pred,
+                                   float* logp_out, void* dZ, float* gw_part, float* dzb,
+                                   int head_relu, float grad_scale, hipStream_t stream);
+static int g_head_mfma = -1;
+extern "C" void dg_head_set_mfma(int on) { g_head_mfma = on; }
+
 extern "C" hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                               const float* bias, const float* posb, const int* labels,
                               float* loss, int* pred, float* logp_out, void* dZ, int dz_pad,
                               float* gw_part, float* unused, float* dzb, int head_relu,
                               float grad_scale, hipStream_t stream) {
   if (C % 8 != 0 || B <= 0) return hipErrorInvalidValue;
+  if (g_head_mfma < 0) {
+    const char* e = getenv("DG_HEAD_MFMA");
+    g_head_mfma = e ? atoi(e) : 1;
+  }
+  // 3x3 head over a 128-channel pad-1 frame: the MFMA kernel (head_mfma.hip)
+  if (g_head_mfma && kw == 3 && C == 128 && x_pad == 1 && (!dZ || dz_pad == 1))
+    return dg_head_mfma(X, B, w, bias, posb, labels, loss, pred, logp_out, dZ, gw_part, dzb,
+                        head_relu, grad_scale, stream);
   if (C > CCH && C % CCH != 0) return hipErrorInvalidValue;
   if (C < CCH && (64 % (C / 8)) != 0) return hipErrorInvalidValue;  // lanes per pixel
   HeadArgs a{(const char*)X, w, bias, posb, labels, loss, pred, logp_out, (char*)dZ, gw_part,

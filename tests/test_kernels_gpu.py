@@ -243,17 +243,25 @@ def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
         hip().wgrad3_set_variant(1)
 
 
-@pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True), (2, 32, 1, False),
-                                        (4, 256, 3, True)])
-def test_head(B, C, k, relu):
+@pytest.mark.parametrize("B,C,k,relu,mfma", [(3, 64, 3, True, 1), (7, 128, 3, True, 1),
+                                             (7, 128, 3, True, 0), (5, 128, 3, False, 1),
+                                             (2, 32, 1, False, 1), (4, 256, 3, True, 1)])
+def test_head(B, C, k, relu, mfma):
+    """Fused head (3x3/128: MFMA kernel unless mfma=0; other shapes: VALU kernel) vs fp32
+    autograd."""
     torch.manual_seed(4)
     from deep_go_amd.ops import functional as Fn
+    from deep_go_amd.ops.native import hip
+    hip().head_set_mfma(mfma)
     x = bf(torch.relu(torch.randn(B, C, 19, 19, device=DEV)))
     w = bf(torch.randn(1, k, k, C, device=DEV) * 0.05)  # fwd dots use bf16 weights
     b = torch.randn(1, device=DEV) * 0.1
     pb = torch.randn(361, device=DEV) * 0.1
     labels = torch.randint(0, 361, (B,), device=DEV)
-    out = Fn.head(x, w, b, pb, labels, head_relu=relu)
+    try:
+        out = Fn.head(x, w, b, pb, labels, head_relu=relu)
+    finally:
+        hip().head_set_mfma(1)
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)
