@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic batches")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--bucket-mb", type=float, default=3.0,
+                    help="DP gradient bucket size (3 MB: head + one 5-layer wgrad group)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="after the timed run, N extra steps with roctx ranges (load / segments"
@@ -95,7 +96,7 @@ def main():
     if world > 1 or args.force_dp:
         lay = net.layout
         ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
-        buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20))
+        buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20), groups=net.wgroups)
         bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=args.grad_dtype)
     load(0)
     step = SegmentedStep(net, bucketer, use_graphs=not args.no_graph)

@@ -68,26 +68,43 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
 
 
 def make_buckets(layer_ranges: Sequence[Tuple[int, int]], bucket_bytes: int,
-                 elem_size: int = 4) -> List[Tuple[int, int, int]]:
+                 elem_size: int = 4,
+                 groups: Optional[Sequence[Sequence[int]]] = None) -> List[Tuple[int, int, int]]:
     """Group layers (given as [start, end) element ranges in flat order) into buckets,
     walking from the LAST layer backwards (the order gradients become final).
 
-    Returns a list of (start, end, first_layer) in firing order; ``first_layer`` is the
-    lowest layer index in the bucket — the bucket is ready after that layer's wgrad."""
+    ``groups``: layers whose gradients become final together (HipGoNet.wgroups: one
+    grouped weight-gradient launch, listed top layer first); a group is never split
+    across buckets and is ready at its top layer.
+
+    Returns a list of (start, end, ready_layer) in firing order: the bucket's gradients
+    are final after ``backward_layer(ready_layer)`` (without groups: its lowest layer)."""
+    top_of = {}
+    for g in groups or ():
+        for i in g:
+            top_of[i] = max(g)
     buckets = []
     cur_start = cur_end = None
-    cur_first = None
-    for i in range(len(layer_ranges) - 1, -1, -1):
-        s, e = layer_ranges[i]
+    cur_ready = None
+    i = len(layer_ranges) - 1
+    while i >= 0:
+        # one unit: a whole group (contiguous layers lo..top) or a single layer
+        top = i
+        lo = i
+        if i in top_of:
+            lo = min(j for j, t in top_of.items() if t == top_of[i])
+        s, e = layer_ranges[lo][0], layer_ranges[top][1]
         if cur_end is None:
-            cur_start, cur_end, cur_first = s, e, i
+            cur_start, cur_end = s, e
         else:
-            cur_start, cur_first = s, i
+            cur_start = s
+        cur_ready = top_of.get(lo, lo)
         if (cur_end - cur_start) * elem_size >= bucket_bytes:
-            buckets.append((cur_start, cur_end, cur_first))
+            buckets.append((cur_start, cur_end, cur_ready))
             cur_start = cur_end = None
+        i = lo - 1
     if cur_end is not None:
-        buckets.append((cur_start, cur_end, cur_first))
+        buckets.append((cur_start, cur_end, cur_ready))
     return buckets
 
 

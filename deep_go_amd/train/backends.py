@@ -153,7 +153,8 @@ class HIPBackend:
         if world > 1:
             ranges = [self.layout.layer_range(i) for i in range(len(self.layout.layers))]
             self.bucketer = dp.GradBucketer(self.net.grads,
-                                            dp.make_buckets(ranges, int(bucket_mb * 2 ** 20)),
+                                            dp.make_buckets(ranges, int(bucket_mb * 2 ** 20),
+                                                            groups=self.net.wgroups),
                                             grad_dtype=grad_dtype)
         self._step = SegmentedStep(self.net, self.bucketer, use_graphs=use_graphs)
         self._eval_n = batch

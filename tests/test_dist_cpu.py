@@ -24,6 +24,20 @@ def _free_port():
     return p
 
 
+def test_make_buckets_keeps_groups_whole():
+    """Layers whose gradients become final together (a grouped wgrad launch) stay in one
+    bucket, which is ready at the group's top layer."""
+    ranges = [(0, 100), (100, 200), (200, 300), (300, 400), (400, 500), (500, 520)]
+    b = make_buckets(ranges, bucket_bytes=4 * 150, groups=[[4, 3, 2]])
+    # walk: layer 5 (20 elems), group 2..4 (300) -> bucket [200, 520) ready at 4; then 1, 0
+    assert b[0] == (200, 520, 4)
+    assert b[1] == (0, 200, 0)
+    assert sum(e - s for s, e, _ in b) == 520
+    # without groups: plain per-layer walk
+    b2 = make_buckets(ranges, bucket_bytes=4 * 150)
+    assert b2[0] == (300, 520, 3)
+
+
 def test_make_buckets_reverse_order_and_sizes():
     ranges = [(0, 100), (100, 300), (300, 350), (350, 1000)]
     b = make_buckets(ranges, bucket_bytes=4 * 250)
