@@ -30,6 +30,8 @@ void dg_conv_board_set_ablate(int mode);
 hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
                              hipStream_t stream);
 void dg_conv_stack_set_ablate(int mode);
+void dg_conv_stack_set_prof(void* p);
+void dg_conv_stack_set_stagger(int on);
 void dg_conv_stack_set_ring(int n);
 void dg_conv_stack_set_bpf(int on);
 hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
@@ -303,6 +305,10 @@ PYBIND11_MODULE(_dghip, m) {
         " copy-out, 16 no barrier");
   m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },
         "3x3/128-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
+  m.def("conv_stack_set_prof", [](uintptr_t p) { dg_conv_stack_set_prof(P<void>(p)); },
+        "ablate 32: per-wave phase cycle sums [B][8][8] (s_memtime)");
+  m.def("conv_stack_set_stagger", [](int on) { dg_conv_stack_set_stagger(on); },
+        "1: half the waves copy the previous layer out after their first MFMAs");
   m.def("conv_stack_set_bpf", [](int on) { dg_conv_stack_set_bpf(on); },
         "B-fragment prefetch across K-steps in conv_stack (default on)");
   m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },

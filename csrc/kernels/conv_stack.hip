@@ -30,6 +30,8 @@
 //
 // Reference ops: nn.SpatialZeroPadding + SpatialConvolutionMM + Add + ReLU per layer
 // (experiments.lua:137-147) and their backward through the stack (train.lua:10).
+#include <stdlib.h>
+
 #include "dg_common.h"
 
 using namespace dg;
@@ -63,7 +65,8 @@ DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
 
 struct StackLayer {
   const bf16_t* A;      // [128][KP] weights, k = tap*128 + ci (dgrad: flipped, transposed)
-  const bf16_t* pbias;  // [361][128] bf16 bias + pos-bias (EPI_FWD)
+  const bf16_t* pbias;  // EPI_FWD: bf16 bias + pos-bias in fragment order (weight_refresh's
+                        // pbias_frag: [24][2][4][64] x 4 bf16)
   char* Y;              // output frame [B][21][21][128] bf16
   uint8_t* mask;        // [B][361][16] ReLU bits: EPI_FWD writes (optional), EPI_DGRAD reads
 };
@@ -71,6 +74,8 @@ struct StackArgs {
   const char* X0;       // input frame [B][21][21][128] bf16 of the first layer
   int nl, KP;
   StackLayer L[MAXL];
+  unsigned long long* prof;  // ABL & 32: per-wave phase cycle sums [B][8 waves][8]
+  int stagger;               // 1: waves 4-7 copy out after their k-half-0 MFMAs
 };
 
 // NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
@@ -152,6 +157,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     }
   };
 
+
   auto read_A = [&](const char* sA, int kk, bf16x8 (&af)[MF]) {
     const int g = kk * 4 + lq;
 #pragma unroll
@@ -189,6 +195,9 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     }
   };
   bf16x8 bpre[NF];
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp0 = 0, te0 = 0;
+  (void)tp0;
+  (void)te0;
 
   int gs = 0;  // global step
   for (int l = 0; l < a.nl; ++l) {
@@ -201,11 +210,15 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
 
     if constexpr (BPF) read_B(0, 0, bpre);  // image of this layer is ready (barrier)
     for (int s = 0; s < NSTEP; ++s, ++gs) {
+      if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); tp0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
       // the previous layer's output (already in the image) goes to HBM under this layer's
       // MFMAs: 512 pieces per step over the first 12 steps.  Issued BEFORE the weight DMA:
       // hipcc puts an s_waitcnt vmcnt(0) in front of an LDS read that follows an LDS-DMA
       // (it cannot prove they do not alias), which would expose the DMA's latency.
-      if (!(ABL & 8) && l > 0) {
+      // waves 0-3 copy out before their k-half-0 MFMAs, waves 4-7 (the other wave of each
+      // SIMD) after them: one wave of every SIMD always has MFMAs to issue meanwhile
+      const bool co_early = !a.stagger || wave < 4;
+      if (!(ABL & 8) && l > 0 && co_early) {
         const int u = s * 512 + tid;
         if (u < UNITS) copy_out(u, a.L[l - 1]);
       }
@@ -213,6 +226,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       // barrier after it
       const bool more = gs + AHEAD < total;
       if (more) stage_A(gs + AHEAD);
+      if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       const char* sA = sA0 + (gs % NRING) * A_BYTES;
       bf16x8 af[MF], bfr[NF];
       // k-half 0: B fragments were prefetched during the previous step (BPF)
@@ -224,6 +238,11 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
         read_B(s, 0, bfr);
       }
       mma(af, bfr, acc);
+      if (!(ABL & 8) && l > 0 && !co_early) {
+        const int u = s * 512 + tid;
+        if (u < UNITS) copy_out(u, a.L[l - 1]);
+      }
+      if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       // k-half 1, and the next step's k-half-0 B fragments (the image is resident: no DMA
       // dependency) issued before these MFMAs so their LDS latency hides under them
       read_A(sA, 1, af);
@@ -231,36 +250,53 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       if (BPF && s + 1 < NSTEP) read_B(s + 1, 0, bpre);
       mma(af, bfr, acc);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((ABL & 32) != 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[2] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       // tile gs+1 must have landed for every wave; the newer tiles (the newest
       // DMA_PER_TILE*(AHEAD-1) VMEM ops of this wave — the copy-out stores precede them)
       // may stay in flight
       if (more) dma_wait<DMA_PER_TILE * (AHEAD - 1)>(); else dma_wait<0>();
+      if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[3] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       if (!(ABL & 16)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((ABL & 32) != 0) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
     }
 
     // ---- epilogue: write the layer's output back into the LDS image ----
     // (every wave is past its last read of the image: barrier above)
+    if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); te0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
+    // every global load of the epilogue is issued before the first use (one latency, not
+    // 24 dependent ones: the phase timer put the old loop at 12.5k cycles per layer)
+    uint2 eu[NF][EPI == EPI_FWD ? MF : 1];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
+      if constexpr (EPI == EPI_FWD) {
+        // fragment-ordered table (weight_refresh writes it): 512 contiguous bytes per load;
+        // the [361][128] table read with this lane mapping touched 16 rows per load (4x
+        // the L2 traffic; the phase timer put the epilogue at 12.5k cycles per layer)
+        const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+      } else {  // 64 channel bits of this wave's image half
+        eu[j][0] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = wn * NF * 16 + j * 16 + lr;
-      if (p >= NPTS) continue;
       const int f = fp[j];
-      uint2 mb = {0u, 0u};
-      if constexpr (EPI == EPI_DGRAD)  // 64 channel bits of this wave's image half
-        mb = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8);
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
         f32x4 v = acc[i][j];
         if constexpr (EPI == EPI_FWD) {
-          const uint2 u = *(const uint2*)(L.pbias + p * C + wm * 64 + cl);
+          const uint2 u = eu[j][i];
           v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
           v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
           v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
           v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
         } else {
-          const uint32_t word = (cl < 32) ? mb.x : mb.y;
+          const uint32_t word = (cl < 32) ? eu[j][0].x : eu[j][0].y;
           const uint32_t bits = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] : 0.f;
@@ -269,13 +305,21 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
         o.x = pack_bf16x2(v[0], v[1]);
         o.y = pack_bf16x2(v[2], v[3]);
         const int slot = (cl >> 3) ^ (fs[j] & 7);
-        *(uint2*)(sH + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
+        if (p < NPTS) *(uint2*)(sH + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
       }
     }
     __syncthreads();
+    if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); ph[5] += __builtin_amdgcn_s_memtime() - te0; __builtin_amdgcn_sched_barrier(0); }
   }
   // last layer's output: exposed copy-out
   for (int u = tid; u < UNITS; u += 512) copy_out(u, a.L[a.nl - 1]);
+  if constexpr ((ABL & 32) != 0) {
+    if (lane == 0 && a.prof) {
+      ph[6] = (unsigned long long)a.nl * NSTEP;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a.prof[((size_t)b * 8 + wave) * 8 + k] = ph[k];
+    }
+  }
 }
 
 template <int EPI, int NRING, int ABL, bool BPF = true>
@@ -304,6 +348,7 @@ hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s)
     case 6: return launch_stack<EPI_FWD, NRING, 6>(a, B, s);
     case 12: return launch_stack<EPI_FWD, NRING, 12>(a, B, s);
     case 14: return launch_stack<EPI_FWD, NRING, 14>(a, B, s);
+    case 32: return launch_stack<EPI_FWD, NRING, 32>(a, B, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -312,12 +357,16 @@ hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s)
 }  // namespace
 
 static int g_stack_ablate = 0;
+static int g_stack_stagger = -1;
+static unsigned long long* g_stack_prof = nullptr;
 static int g_stack_ring = 0;  // 0: default (2)
 static int g_stack_bpf = 1;   // B-fragment prefetch across K-steps
 
 extern "C" {
 
 void dg_conv_stack_set_ablate(int mode) { g_stack_ablate = mode; }
+void dg_conv_stack_set_stagger(int on) { g_stack_stagger = on; }
+void dg_conv_stack_set_prof(void* p) { g_stack_prof = (unsigned long long*)p; }
 void dg_conv_stack_set_ring(int n) { g_stack_ring = n; }
 void dg_conv_stack_set_bpf(int on) { g_stack_bpf = on; }
 
@@ -332,6 +381,12 @@ hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0
   a.X0 = (const char*)X0;
   a.nl = nl;
   a.KP = KP;
+  a.prof = g_stack_prof;
+  if (g_stack_stagger < 0) {
+    const char* e = getenv("DG_STACK_STAGGER");
+    g_stack_stagger = e ? atoi(e) : 0;
+  }
+  a.stagger = g_stack_stagger;
   for (int i = 0; i < nl; ++i) {
     a.L[i].A = (const bf16_t*)table[4 * i];
     a.L[i].pbias = (const bf16_t*)table[4 * i + 1];

@@ -213,6 +213,8 @@ struct WRefreshLayer {
   const float* bias;   // [cout]            } pbias[p][co] = bf16(bias[co] + posb[p][co]):
   const float* posb;   // [361][cout]       } the forward epilogue's single bias table
   bf16_t* pbias;       // [361][cout] or null
+  uint2* pbias_frag;   // the same table in the board-resident stack's accumulator-fragment
+                       // order (cout == 128): [24 px frags][2 co halves][4][64 lanes] x 4 bf16
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -276,6 +278,19 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
     const int n = NPTS * L.cout;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256)
       L.pbias[e] = f2bf(L.bias[e % L.cout] + L.posb[e]);
+  }
+  if (L.pbias_frag) {
+    // element e = ((jg * 2 + wm) * 4 + i) * 64 + lane: pixel jg*16 + (lane & 15), channels
+    // wm*64 + i*16 + (lane >> 4)*4 .. +3 — one coalesced 512-B load per epilogue fragment
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < 24 * 2 * 4 * 64; e += gridDim.x * 256) {
+      const int lane = e & 63, i = (e >> 6) & 3, wm = (e >> 8) & 1, jg = e >> 9;
+      int p = jg * 16 + (lane & 15);
+      p = p < NPTS ? p : NPTS - 1;
+      const int c = wm * 64 + i * 16 + (lane >> 4) * 4;
+      const float* pb = L.posb + (size_t)p * 128 + c;
+      L.pbias_frag[e] = uint2{pack_bf16x2(L.bias[c] + pb[0], L.bias[c + 1] + pb[1]),
+                              pack_bf16x2(L.bias[c + 2] + pb[2], L.bias[c + 3] + pb[3])};
+    }
   }
 }
 
@@ -359,7 +374,8 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
 }
 
 // layers: n entries of 16 int64 words
-//   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, unused, wf8, s_w, amax_w, bias, posb, pbias}
+//   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, pbias_frag, wf8, s_w, amax_w, bias, posb,
+//    pbias}  (pbias_frag: stack-order table, cout 128 only, or 0)
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -384,6 +400,8 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].bias = (const float*)t[13];
     a.L[i].posb = (const float*)t[14];
     a.L[i].pbias = (bf16_t*)t[15];
+    a.L[i].pbias_frag = (uint2*)t[9];
+    if (a.L[i].pbias_frag && a.L[i].cout != 128) return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;
   }

@@ -176,6 +176,11 @@ class HipGoNet:
         # and ReLU bitmasks of the board-kernel outputs consumed by a board dgrad
         self.pbias = [torch.zeros((NUM_POINTS, p.cout), dtype=torch.bfloat16, device=dev)
                       if p.board and not p.fp8 else None for p in self.plans]
+        # the same table in the forward stack's accumulator-fragment order (coalesced
+        # epilogue loads), for every 128-channel board layer
+        self.pbias_frag = [torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=dev)
+                           if pb is not None and p.cout == 128 else None
+                           for p, pb in zip(self.plans, self.pbias)]
         self.relu_mask = [None] * len(self.plans)
         for p in self.plans[:-1]:
             nxt = self.plans[p.index + 1]
@@ -250,7 +255,9 @@ class HipGoNet:
             w = self.params[spec.w_off:spec.w_off + spec.w_numel]
             w8 = self.wf8[p.index]
             rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0,
-                         p.cout, p.cin, p.k * p.k, p.cinp_f or p.cinp, p.KP, p.KPd, 0,
+                         p.cout, p.cin, p.k * p.k, p.cinp_f or p.cinp, p.KP, p.KPd,
+                         self.pbias_frag[p.index].data_ptr()
+                         if self.pbias_frag[p.index] is not None else 0,
                          w8.data_ptr() if w8 is not None else 0,
                          self.fp8_scales.data_ptr() + 8 * p.index if w8 is not None else 0,
                          self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0,
@@ -401,8 +408,8 @@ class HipGoNet:
         rows = []
         for i in best:
             m = self.relu_mask[i]
-            rows.append([self.wf[i].data_ptr(), self.pbias[i].data_ptr(), self.act[i].data_ptr(),
-                         m.data_ptr() if m is not None else 0])
+            rows.append([self.wf[i].data_ptr(), self.pbias_frag[i].data_ptr(),
+                         self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
         self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
         op = (self.h.conv_stack_fwd, (self._stack_table.ctypes.data, len(best),

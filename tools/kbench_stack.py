@@ -28,7 +28,7 @@ def main():
         ws.append(LY.fwd_weight(w, C, KP, Mpad))
         ys.append(LY.alloc_frame(B, C, 1, dev))
         ms.append(torch.randint(0, 255, (B, 361, 16), dtype=torch.uint8, device=dev))
-        pbs.append((0.01 * torch.randn(361, C, device=dev)).to(torch.bfloat16))
+        pbs.append((0.01 * torch.randn(24 * 2 * 4 * 64 * 4, device=dev)).to(torch.bfloat16))  # fragment order
     tf = np.array([[ws[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr()]
                    for i in range(NL)], dtype=np.int64)
     td = np.array([[ws[i].data_ptr(), 0, ys[i].data_ptr(), ms[i].data_ptr()]
@@ -63,9 +63,27 @@ def main():
         for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
             res.setdefault(f"ring2_nobpf_{name}", []).append(round(timeit(run(epi, t)), 1))
         h.conv_stack_set_bpf(1)
+        h.conv_stack_set_stagger(1)
+        for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
+            res.setdefault(f"ring2_stagger_{name}", []).append(round(timeit(run(epi, t)), 1))
+        h.conv_stack_set_stagger(0)
     out = {k: {"us": v, "us_per_layer": round(min(v) / NL, 2),
                "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     out["variants_bit_identical"] = res_ok
+    # phase breakdown (s_memtime per wave; the timestamps pin the schedule, ~+10%)
+    prof = torch.zeros(B * 8 * 8, dtype=torch.int64, device=dev)
+    h.conv_stack_set_prof(prof.data_ptr())
+    h.conv_stack_set_ablate(32)
+    run(h.EPI_FWD, tf)()
+    torch.cuda.synchronize()
+    h.conv_stack_set_ablate(0)
+    h.conv_stack_set_prof(0)
+    pr = prof.view(B, 8, 8).double()
+    steps = pr[..., 6].mean().item()
+    names = ["copyout+dma_issue", "kk0(readA+mma)", "kk1(reads+mma)", "dma_wait", "barrier"]
+    out["phase_cycles_per_step"] = {n: round(pr[..., k].mean().item() / steps, 1)
+                                    for k, n in enumerate(names)}
+    out["epilogue_cycles_per_layer"] = round(pr[..., 5].mean().item() / NL, 1)
     print(json.dumps(out, indent=1))
 
 
