@@ -99,6 +99,18 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   // instructions per wave, issued from inline asm (dma16) so the compiler's waitcnt pass
   // does not drain them in front of the copy-out's LDS reads; retired by dma_wait below
   const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
+  // per-lane part of the weight-tile source address (row r of the tile, swizzled group)
+  const uint32_t a_lane0 = (uint32_t)((((wave * 2) * 8 + (lane >> 3)) * a.KP + g_src * 8) * 2);
+  const uint32_t a_lane1 = a_lane0 + (uint32_t)(8 * a.KP * 2);
+  // tile (layer weights A, step s of that layer) into ring slot `slot`
+  auto stage_A_at = [&](const bf16_t* A, int s, int slot) {
+    if (ABL & 4) return;
+    const int c = s / T, t = s - (s / T) * T;
+    const char* Ak = (const char*)A + (t * C + c * 64) * 2;
+    const uint32_t dst = lds0 + slot * A_BYTES;
+    dma16(Ak + a_lane0, __builtin_amdgcn_readfirstlane(dst + (wave * 2) * 1024));
+    dma16(Ak + a_lane1, __builtin_amdgcn_readfirstlane(dst + (wave * 2 + 1) * 1024));
+  };
   auto stage_A = [&](int g) {
     if (ABL & 4) return;
     const int l = g / NSTEP, s = g - l * NSTEP;
@@ -202,6 +214,8 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   int gs = 0;  // global step
   for (int l = 0; l < a.nl; ++l) {
     const StackLayer L = a.L[l];
+    const bf16_t* A_next = l + 1 < a.nl ? a.L[l + 1].A : L.A;
+    const StackLayer Lprev = a.L[l > 0 ? l - 1 : 0];
     f32x4 acc[MF][NF];
 #pragma unroll
     for (int i = 0; i < MF; ++i)
@@ -220,12 +234,16 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       const bool co_early = !a.stagger || wave < 4;
       if (!(ABL & 8) && l > 0 && co_early) {
         const int u = s * 512 + tid;
-        if (u < UNITS) copy_out(u, a.L[l - 1]);
+        if (u < UNITS) copy_out(u, Lprev);
       }
       // ring slot (gs+AHEAD)%NRING was last read in step gs-1: every wave passed the
       // barrier after it
       const bool more = gs + AHEAD < total;
-      if (more) stage_A(gs + AHEAD);
+      // (no dynamic kernel-argument indexing in the loop: a.L[l + 1].A is hoisted below)
+      if (more) {
+        if (s + AHEAD < NSTEP) stage_A_at(L.A, s + AHEAD, (gs + AHEAD) % NRING);
+        else stage_A_at(A_next, s + AHEAD - NSTEP, (gs + AHEAD) % NRING);
+      }
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       const char* sA = sA0 + (gs % NRING) * A_BYTES;
       bf16x8 af[MF], bfr[NF];
@@ -240,7 +258,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       mma(af, bfr, acc);
       if (!(ABL & 8) && l > 0 && !co_early) {
         const int u = s * 512 + tid;
-        if (u < UNITS) copy_out(u, a.L[l - 1]);
+        if (u < UNITS) copy_out(u, Lprev);
       }
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       // k-half 1, and the next step's k-half-0 B fragments (the image is resident: no DMA
@@ -349,6 +367,7 @@ hipError_t dispatch_ablate(int ablate, const StackArgs& a, int B, hipStream_t s)
     case 12: return launch_stack<EPI_FWD, NRING, 12>(a, B, s);
     case 14: return launch_stack<EPI_FWD, NRING, 14>(a, B, s);
     case 32: return launch_stack<EPI_FWD, NRING, 32>(a, B, s);
+    case 40: return launch_stack<EPI_FWD, NRING, 40>(a, B, s);
     default: return hipErrorInvalidValue;
   }
 }

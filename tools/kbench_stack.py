@@ -71,19 +71,20 @@ def main():
                "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     out["variants_bit_identical"] = res_ok
     # phase breakdown (s_memtime per wave; the timestamps pin the schedule, ~+10%)
-    prof = torch.zeros(B * 8 * 8, dtype=torch.int64, device=dev)
-    h.conv_stack_set_prof(prof.data_ptr())
-    h.conv_stack_set_ablate(32)
-    run(h.EPI_FWD, tf)()
-    torch.cuda.synchronize()
-    h.conv_stack_set_ablate(0)
-    h.conv_stack_set_prof(0)
-    pr = prof.view(B, 8, 8).double()
-    steps = pr[..., 6].mean().item()
     names = ["copyout+dma_issue", "kk0(readA+mma)", "kk1(reads+mma)", "dma_wait", "barrier"]
-    out["phase_cycles_per_step"] = {n: round(pr[..., k].mean().item() / steps, 1)
-                                    for k, n in enumerate(names)}
-    out["epilogue_cycles_per_layer"] = round(pr[..., 5].mean().item() / NL, 1)
+    for mode, tag in ((32, ""), (40, "_nocopyout")):
+        prof = torch.zeros(B * 8 * 8, dtype=torch.int64, device=dev)
+        h.conv_stack_set_prof(prof.data_ptr())
+        h.conv_stack_set_ablate(mode)
+        run(h.EPI_FWD, tf)()
+        torch.cuda.synchronize()
+        h.conv_stack_set_ablate(0)
+        h.conv_stack_set_prof(0)
+        pr = prof.view(B, 8, 8).double()
+        steps = pr[..., 6].mean().item()
+        out["phase_cycles_per_step" + tag] = {n: round(pr[..., k].mean().item() / steps, 1)
+                                              for k, n in enumerate(names)}
+        out["epilogue_cycles_per_layer" + tag] = round(pr[..., 5].mean().item() / NL, 1)
     print(json.dumps(out, indent=1))
 
 
