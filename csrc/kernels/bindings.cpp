@@ -34,6 +34,7 @@ void dg_conv_stack_set_prof(void* p);
 void dg_conv_stack_set_stagger(int on);
 void dg_conv_stack_set_ring(int n);
 void dg_conv_stack_set_bpf(int on);
+void dg_conv_stack_set_waves(int n);
 hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
                          hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
@@ -309,6 +310,8 @@ PYBIND11_MODULE(_dghip, m) {
         "ablate 32: per-wave phase cycle sums [B][8][8] (s_memtime)");
   m.def("conv_stack_set_stagger", [](int on) { dg_conv_stack_set_stagger(on); },
         "1: half the waves copy the previous layer out after their first MFMAs");
+  m.def("conv_stack_set_waves", [](int n) { dg_conv_stack_set_waves(n); },
+        "conv_stack waves per workgroup: 8 (64x96 per wave) or 16 (64x48 per wave)");
   m.def("conv_stack_set_bpf", [](int on) { dg_conv_stack_set_bpf(on); },
         "B-fragment prefetch across K-steps in conv_stack (default on)");
   m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },

@@ -51,8 +51,7 @@ constexpr int UNITS = NPTS * 16;          // 16-B output pieces of one board (57
 constexpr int MAXL = 24;
 constexpr int BM = 128;
 constexpr int A_BYTES = BM * 128;         // [128 co][64 k] bf16
-constexpr int DMA_PER_TILE = 2;           // LDS-DMA instructions per wave per tile
-constexpr int WN = 4, MF = 4, NF = 6;     // 2 x 4 waves, 64 co x 96 px per wave
+constexpr int MF = 4;                     // 64 co per wave (4 fragments of 16)
 
 // Image swizzle: the 16-B slot of 8-channel group g in frame row f is g ^ sig(f) with
 // sig(f) = (x + 3y) & 7, (y, x) = (f / 21, f % 21).  The plain f & 7 (conv_board) is
@@ -81,8 +80,14 @@ struct StackArgs {
 // NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
 // ABL: timing ablations for tools/kbench_stack.py (0 in production): 1 no MFMA, 2 no
 // fragment LDS reads, 4 no weight DMA, 8 no in-loop copy-out, 16 no per-step barrier.
-template <int EPI, int NRING, int ABL, bool BPF = true>
-__global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
+template <int EPI, int NRING, int ABL, bool BPF = true, int NW = 8>
+__global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
+  // NW waves: 2 (co halves) x NW/2 pixel groups; 8 waves: 64 co x 96 px per wave (2 per
+  // SIMD), 16 waves: 64 co x 48 px per wave (4 per SIMD, half the accumulators)
+  constexpr int NT = NW * 64;
+  constexpr int WN = NW / 2;
+  constexpr int NF = 24 / WN;
+  constexpr int DMA_PER_TILE = 16 / NW;
   constexpr int AHEAD = NRING - 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -100,7 +105,8 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   // does not drain them in front of the copy-out's LDS reads; retired by dma_wait below
   const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
   // per-lane part of the weight-tile source address (row r of the tile, swizzled group)
-  const uint32_t a_lane0 = (uint32_t)((((wave * 2) * 8 + (lane >> 3)) * a.KP + g_src * 8) * 2);
+  const uint32_t a_lane0 =
+      (uint32_t)((((wave * DMA_PER_TILE) * 8 + (lane >> 3)) * a.KP + g_src * 8) * 2);
   const uint32_t a_lane1 = a_lane0 + (uint32_t)(8 * a.KP * 2);
   // tile (layer weights A, step s of that layer) into ring slot `slot`
   auto stage_A_at = [&](const bf16_t* A, int s, int slot) {
@@ -108,8 +114,9 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     const int c = s / T, t = s - (s / T) * T;
     const char* Ak = (const char*)A + (t * C + c * 64) * 2;
     const uint32_t dst = lds0 + slot * A_BYTES;
-    dma16(Ak + a_lane0, __builtin_amdgcn_readfirstlane(dst + (wave * 2) * 1024));
-    dma16(Ak + a_lane1, __builtin_amdgcn_readfirstlane(dst + (wave * 2 + 1) * 1024));
+    dma16(Ak + a_lane0, __builtin_amdgcn_readfirstlane(dst + (wave * DMA_PER_TILE) * 1024));
+    if constexpr (DMA_PER_TILE == 2)
+      dma16(Ak + a_lane1, __builtin_amdgcn_readfirstlane(dst + (wave * 2 + 1) * 1024));
   };
   auto stage_A = [&](int g) {
     if (ABL & 4) return;
@@ -120,16 +127,16 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     const uint32_t dst = lds0 + (g % NRING) * A_BYTES;
 #pragma unroll
     for (int i = 0; i < DMA_PER_TILE; ++i) {
-      const int r = (wave * 2 + i) * 8 + (lane >> 3);
+      const int r = (wave * DMA_PER_TILE + i) * 8 + (lane >> 3);
       dma16((const char*)A + ((size_t)r * a.KP + kcol + g_src * 8) * 2,
-            __builtin_amdgcn_readfirstlane(dst + (wave * 2 + i) * 1024));
+            __builtin_amdgcn_readfirstlane(dst + (wave * DMA_PER_TILE + i) * 1024));
     }
   };
 
   // ---- prologue: the first layer's input frame (both images) + weight tiles 0, 1 ----
   {
     const char* Xb = a.X0 + (size_t)b * FF * C * 2;
-    for (int j = wave; j < 2 * (HROWS / 8); j += 8) {
+    for (int j = wave; j < 2 * (HROWS / 8); j += NW) {
       const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
       int r = jj * 8 + (lane >> 3);
       r = r < FF ? r : FF - 1;
@@ -233,7 +240,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
       // SIMD) after them: one wave of every SIMD always has MFMAs to issue meanwhile
       const bool co_early = !a.stagger || wave < 4;
       if (!(ABL & 8) && l > 0 && co_early) {
-        const int u = s * 512 + tid;
+        const int u = s * NT + tid;
         if (u < UNITS) copy_out(u, Lprev);
       }
       // ring slot (gs+AHEAD)%NRING was last read in step gs-1: every wave passed the
@@ -256,8 +263,11 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
         read_B(s, 0, bfr);
       }
       mma(af, bfr, acc);
+      // 16 waves (4 per SIMD, 128 VGPRs): keep k-half 1's reads below these MFMAs (the other
+      // waves of the SIMD hide their latency) instead of two live fragment sets
+      if constexpr (NW == 16) __builtin_amdgcn_sched_barrier(0);
       if (!(ABL & 8) && l > 0 && !co_early) {
-        const int u = s * 512 + tid;
+        const int u = s * NT + tid;
         if (u < UNITS) copy_out(u, Lprev);
       }
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
@@ -330,7 +340,7 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
     if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); ph[5] += __builtin_amdgcn_s_memtime() - te0; __builtin_amdgcn_sched_barrier(0); }
   }
   // last layer's output: exposed copy-out
-  for (int u = tid; u < UNITS; u += 512) copy_out(u, a.L[a.nl - 1]);
+  for (int u = tid; u < UNITS; u += NT) copy_out(u, a.L[a.nl - 1]);
   if constexpr ((ABL & 32) != 0) {
     if (lane == 0 && a.prof) {
       ph[6] = (unsigned long long)a.nl * NSTEP;
@@ -340,18 +350,18 @@ __global__ void __launch_bounds__(512) conv_stack_kernel(StackArgs a) {
   }
 }
 
-template <int EPI, int NRING, int ABL, bool BPF = true>
+template <int EPI, int NRING, int ABL, bool BPF = true, int NW = 8>
 hipError_t launch_stack(const StackArgs& a, int B, hipStream_t stream) {
   constexpr size_t lds = NRING * (size_t)A_BYTES + 2 * (size_t)H_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_kernel<EPI, NRING, ABL, BPF>,
+    (void)hipFuncSetAttribute((const void*)conv_stack_kernel<EPI, NRING, ABL, BPF, NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack_kernel<EPI, NRING, ABL, BPF>), dim3(B), dim3(512), lds, stream,
-                     a);
+  hipLaunchKernelGGL((conv_stack_kernel<EPI, NRING, ABL, BPF, NW>), dim3(B), dim3(NW * 64), lds,
+                     stream, a);
   return hipGetLastError();
 }
 
@@ -380,6 +390,7 @@ static int g_stack_stagger = -1;
 static unsigned long long* g_stack_prof = nullptr;
 static int g_stack_ring = 0;  // 0: default (2)
 static int g_stack_bpf = 1;   // B-fragment prefetch across K-steps
+static int g_stack_waves = 8; // waves per workgroup (8 or 16)
 
 extern "C" {
 
@@ -388,6 +399,7 @@ void dg_conv_stack_set_stagger(int on) { g_stack_stagger = on; }
 void dg_conv_stack_set_prof(void* p) { g_stack_prof = (unsigned long long*)p; }
 void dg_conv_stack_set_ring(int n) { g_stack_ring = n; }
 void dg_conv_stack_set_bpf(int on) { g_stack_bpf = on; }
+void dg_conv_stack_set_waves(int n) { g_stack_waves = n; }
 
 // table: nl rows of {A, pbias, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)
@@ -420,6 +432,9 @@ hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0
     return epi == EPI_FWD ? (nring == 3 ? dispatch_ablate<3>(g_stack_ablate, a, B, stream)
                                         : dispatch_ablate<2>(g_stack_ablate, a, B, stream))
                           : hipErrorInvalidValue;
+  if (g_stack_waves == 16)
+    return epi == EPI_FWD ? launch_stack<EPI_FWD, 2, 0, false, 16>(a, B, stream)
+                          : launch_stack<EPI_DGRAD, 2, 0, false, 16>(a, B, stream);
   if (!g_stack_bpf)
     return epi == EPI_FWD ? launch_stack<EPI_FWD, 2, 0, false>(a, B, stream)
                           : launch_stack<EPI_DGRAD, 2, 0, false>(a, B, stream);

@@ -41,13 +41,18 @@ def main():
         return lambda: h.conv_stack(epi, table.ctypes.data, NL, x.data_ptr(), KP, B, s)
     # correctness of the variants against each other (same inputs -> same outputs)
     outs = {}
-    for ring in (2, 3):
-        h.conv_stack_set_ring(ring)
+    for ring in (2, 3, 16):
+        if ring == 16:
+            h.conv_stack_set_waves(16)
+        else:
+            h.conv_stack_set_ring(ring)
         run(h.EPI_FWD, tf)()
         torch.cuda.synchronize()
         outs[ring] = [y.clone() for y in ys] + [m.clone() for m in ms]
     h.conv_stack_set_ring(0)
+    h.conv_stack_set_waves(8)
     res_ok = all(torch.equal(a, b) for a, b in zip(outs[2], outs[3]))
+    res_ok16 = all(torch.equal(a, b) for a, b in zip(outs[2], outs[16]))
     for rnd in range(2):
         for ring in (2, 3):
             h.conv_stack_set_ring(ring)
@@ -63,6 +68,10 @@ def main():
         for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
             res.setdefault(f"ring2_nobpf_{name}", []).append(round(timeit(run(epi, t)), 1))
         h.conv_stack_set_bpf(1)
+        h.conv_stack_set_waves(16)
+        for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
+            res.setdefault(f"w16_{name}", []).append(round(timeit(run(epi, t)), 1))
+        h.conv_stack_set_waves(8)
         h.conv_stack_set_stagger(1)
         for name, epi, t in (("fwd", h.EPI_FWD, tf), ("dgrad", h.EPI_DGRAD, td)):
             res.setdefault(f"ring2_stagger_{name}", []).append(round(timeit(run(epi, t)), 1))
@@ -70,6 +79,7 @@ def main():
     out = {k: {"us": v, "us_per_layer": round(min(v) / NL, 2),
                "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     out["variants_bit_identical"] = res_ok
+    out["w16_bit_identical"] = res_ok16
     # phase breakdown (s_memtime per wave; the timestamps pin the schedule, ~+10%)
     names = ["copyout+dma_issue", "kk0(readA+mma)", "kk1(reads+mma)", "dma_wait", "barrier"]
     for mode, tag in ((32, ""), (40, "_nocopyout")):
