@@ -431,6 +431,7 @@ class HipGoNet:
         self.wgroups: List[List[int]] = []
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         if os.environ.get("DG_DSTACK", "1") == "0":
+            self._dgrads_first()
             return
         L = self.layout.layers
 
@@ -445,6 +446,7 @@ class HipGoNet:
                 break
             run.append(i)
         if len(run) < 2:
+            self._dgrads_first()
             return
         self.dstack = run
         rows = [[self.wd[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
@@ -456,6 +458,24 @@ class HipGoNet:
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
             self._bwd[i] = self._bwd[i][:3]
         self._group_wgrads(set([run[0]] + [i - 1 for i in run]))
+
+    def _dgrads_first(self):
+        """No board-resident dgrad stack for this shape (e.g. 256 channels): still run the
+        whole backward-data chain first — the per-layer dgrad launches, top to bottom, right
+        after the head — so every dZ exists before the weight gradients and those can run
+        as grouped launches (fewer split-K partials).  DG_DGRAD_FIRST=0 keeps the
+        interleaved per-layer order."""
+        if os.environ.get("DG_DGRAD_FIRST", "1") == "0" or self.side_mode != "none":
+            return
+        moved = []
+        for i in range(len(self.plans) - 1, 0, -1):
+            ops = self._bwd[i]
+            if len(ops) > 3:
+                self._bwd_pre.extend(ops[3:])
+                self._bwd[i] = ops[:3]
+                moved.append(i)
+        if moved:
+            self._group_wgrads(set(range(len(self.plans))))
 
     @staticmethod
     def _noop(*_):

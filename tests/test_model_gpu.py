@@ -169,14 +169,21 @@ def test_fused_dgrad_stack_matches_per_layer(layers, l0_mask, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("layers,group", [(7, 5), (9, 3), (6, 2)])
-def test_grouped_wgrads_match_per_layer(layers, group, monkeypatch):
+@pytest.mark.parametrize("layers,group,ch,dstack", [(7, 5, 128, "1"), (9, 3, 128, "1"),
+                                                    (6, 2, 128, "1"), (6, 3, 128, "0"),
+                                                    (5, 3, 256, "1")])
+def test_grouped_wgrads_match_per_layer(layers, group, ch, dstack, monkeypatch):
     """conv_wgrad_multi (several layers' weight gradients in one launch, fewer pixel splits
-    per layer) gives the per-layer launches' gradients up to fp32 summation order."""
+    per layer) gives the per-layer launches' gradients up to fp32 summation order — after
+    the dgrad stack (128 channels) or after the per-layer dgrads run first (256 channels,
+    or DG_DSTACK=0)."""
+    monkeypatch.setenv("DG_DSTACK", dstack)
     monkeypatch.setenv("DG_WGRAD_GROUP", "1")
-    _, n0, _ = _setup(layers, 128, 6, seed=11)
+    monkeypatch.setenv("DG_DGRAD_FIRST", "0")
+    _, n0, _ = _setup(layers, ch, 6, seed=11)
     monkeypatch.setenv("DG_WGRAD_GROUP", str(group))
-    _, n1, _ = _setup(layers, 128, 6, seed=11)
+    monkeypatch.setenv("DG_DGRAD_FIRST", "1")
+    _, n1, _ = _setup(layers, ch, 6, seed=11)
     assert not n0.wgroups and n1.wgroups and max(len(g) for g in n1.wgroups) <= group
     n0.forward_backward()
     n1.forward_backward()
