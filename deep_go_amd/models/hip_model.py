@@ -482,13 +482,20 @@ class HipGoNet:
         pass
 
     def _group_wgrads(self, dz_ready):
-        """Weight gradients of up to DG_WGRAD_GROUP (default 5) consecutive same-shape
-        layers whose dZ the dgrad stack has already produced run as ONE three-slice launch
+        """Weight gradients of up to DG_WGRAD_GROUP consecutive same-shape layers whose dZ
+        the dgrad stack has already produced run as ONE three-slice launch
         (conv_wgrad_multi).  The machine is filled by the layers instead of by pixel
         splits, so each layer is cut into ~5x fewer splits: ~5x fewer fp32 partial slabs
-        to write and reduce (50 -> 10 MB per 128-channel layer)."""
+        to write and reduce (50 -> 10 MB per 128-channel layer).
+
+        Default group size: 5 under data parallelism (a DP bucket fires at a group's top
+        layer, so two groups let the first all-reduce overlap the second group), and all
+        hidden layers in one launch on a single GPU (12x128: 245k -> 248k boards/s,
+        gpurun_out/ab.txt sweep of 4/5/7/10)."""
         self.wgroups: List[List[int]] = []
-        G = int(os.environ.get("DG_WGRAD_GROUP", "5"))
+        G = int(os.environ.get("DG_WGRAD_GROUP",
+                               "5" if self.global_batch != self.B else "16"))
+        G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
         if G < 2 or self.side_mode != "none":
             return
         lay = self.layout.layers
