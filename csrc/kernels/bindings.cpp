@@ -50,6 +50,11 @@ int dg_conv_wgrad_wgs_per_cu_for(int KP);
 hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pad, int M,
                                int Mpad, int x_pad, int x_C, int B, int KP, int splits,
                                hipStream_t stream);
+void dg_conv_wgrad_win_set_ablate(int mode);
+void dg_conv_wgrad_win_set_pd(int pd);
+int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
+hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
+                             int KP, int splits, hipStream_t stream);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
@@ -328,6 +333,17 @@ PYBIND11_MODULE(_dghip, m) {
                               splits, S(stream)),
           "conv_wgrad_multi");
   }, "weight gradients of several same-shape layers in one three-slice launch");
+  m.def("conv_wgrad_win", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
+                             int splits, uintptr_t stream) {
+    check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
+          "conv_wgrad_win");
+  }, "sliding-window 3x3 weight gradients (frame-linear K, 9 taps per staged X window)");
+  m.def("conv_wgrad_win_splits", [](int nl, int M, int Cx, int B, int num_cus) {
+    return dg_conv_wgrad_win_splits(nl, M, Cx, B, num_cus);
+  });
+  m.def("conv_wgrad_win_set_ablate", [](int mode) { dg_conv_wgrad_win_set_ablate(mode); });
+  m.def("conv_wgrad_win_set_pd", [](int pd) { dg_conv_wgrad_win_set_pd(pd); },
+        "LDS-DMA prefetch distance of conv_wgrad_win in K-steps (1..4, default 4)");
   m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });
   m.def("conv_wgrad_wgs_per_cu_for", [](int KP) { return dg_conv_wgrad_wgs_per_cu_for(KP); });
   m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });

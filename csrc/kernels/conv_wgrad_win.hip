@@ -1,0 +1,319 @@
+// Sliding-window weight gradient of 3x3 layers on the frame-linear pixel axis.
+//
+//   dW[co][t][ci] = sum_G dZ[G][co] * X[G + off_t][ci],   off_t = (kh-1)*21 + (kw-1)
+//
+// G runs over the rows of the zero-bordered 21x21 frames of consecutive boards (frames are
+// contiguous in memory, so G is a plain row index into both the dZ and the X frame
+// arrays).  dZ is zero on every border position, so the product never leaks across a board
+// edge and the 9 taps are 9 constant row shifts of ONE X window: per 32-row K-step a
+// workgroup stages 32 new dZ rows and ~32 new X rows (a ring indexed by G mod 256) and runs
+// all 9 taps against them.  The im2col wgrad (conv_mfma.hip, conv_wgrad_t3_kernel) stages
+// X once per kernel row instead (64 KB of LDS-DMA per 384 MFMAs = 171 B/MFMA, its measured
+// limiter); here it is 12 KB per 288 MFMAs = 43 B/MFMA.
+//
+// Per board the K-steps cover frame rows 1..19 only (G = b*441 + 21 + 32j, j < 13, 416 of
+// 441 rows; the last step's tail is border row 20, zero in dZ), so the MFMA work is 416/361
+// of the useful products.  Both operands are read with transposing LDS reads
+// (ds_read_b64_tr_b16): rows = pixels (K), columns = channels.
+//
+// Workgroup = 8 waves, tile 128 co x 9 taps x 64 ci (wave (wm, wn): 64 co x 9 taps x 16 ci,
+// 4 x 9 accumulator fragments); grid = layers x co-chunks x ci-chunks x pixel splits, one
+// workgroup per CU, XCD-remapped so the chunks of one (layer, split) share an L2.  Output:
+// fp32 split slabs slab[z][co][t*Cx + ci] in the layout wgrad_reduce_multi sums.
+//
+// Reference semantics: SpatialConvolutionMM accGradParameters (experiments.lua:138, EXTERNAL
+// nn) — the gradient of the 3x3 hidden convolutions of getBasicModel (experiments.lua:135-149).
+#include "dg_common.h"
+
+using namespace dg;
+
+namespace {
+
+constexpr int WF = 21;              // frame width (pad 1)
+constexpr int WFF = WF * WF;        // 441 rows per board
+constexpr int STEPS_PER_BOARD = 13; // 13 x 32 = 416 rows from frame row 1
+constexpr int XR = 256;             // X ring rows (128 B each)
+constexpr int XRING = XR * 128;     // 32 KB
+constexpr int DZB = 32 * 256;       // one dZ step: 32 rows x 128 co bf16
+constexpr int MAXL = 16;
+
+struct WinLayers {
+  const char* dZ[MAXL];
+  const char* X[MAXL];
+  float* slab[MAXL];
+};
+
+struct WinArgs {
+  int M;       // dZ channels (co), multiple of 128
+  int Mpad;    // slab rows
+  int Cx;      // X channels (ci), multiple of 64
+  int KP;      // slab row length (>= 9 * Cx)
+  int B;       // boards
+  int splits;  // pixel splits per (layer, chunk pair)
+  int nl;      // layers
+};
+
+// 16-B slot swizzle of a 128-B X ring row: a 32-lane half of a transposing read takes rows
+// {s..s+3, s+8..s+11} for ANY shift s (the 9 taps); this keeps its 256 B on 64 distinct
+// banks (checked exhaustively over s and the chunk pair).
+DG_DEV int xswz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+// 256-B dZ rows (step-local, 8-aligned groups): same swizzle as conv_wgrad_kernel.
+DG_DEV int dswz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+DG_DEV int step_g0(int s) {
+  const int b = s / STEPS_PER_BOARD;
+  return b * WFF + WF + 32 * (s - b * STEPS_PER_BOARD);
+}
+
+// ABL: ablation bits (diagnostics; 0 in production): 1 no MFMA, 2 no LDS reads, 4 no DMA.
+// PD: LDS-DMA prefetch distance in K-steps (dZ buffers = PD + 1; the X ring holds the
+// current window plus PD steps ahead: <= 22 + 54 + 57 + 32 (PD - 1) + 8 rows < 256 for
+// PD <= 4).  The DMAs are issued from inline asm (dma16) with hand vmcnt accounting: every
+// wave issues exactly 2 per steady-state step (one dZ block, one X block; a wave with no
+// new X block re-loads one that another wave loads, same bytes), so "DMAs of step st+1
+// landed" = vmcnt(2 (PD - 1)).
+template <int ABL, int PD>
+__global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
+  static_assert(PD >= 1 && PD <= 4, "prefetch distance");
+  __shared__ __attribute__((aligned(16))) char smem[XRING + (PD + 1) * DZB];
+  char* xring = smem;
+  char* dzbuf = smem + XRING;
+  const uint32_t xring_u = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
+  const uint32_t dz_u = xring_u + XRING;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nci = a.Cx / 64, nco = a.M / 128;
+  const int nwg = a.nl * nco * nci * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, xslot = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
+  const int cich = lid % nci;
+  int rest = lid / nci;
+  const int coch = rest % nco;
+  rest /= nco;
+  const int zsplit = rest % a.splits;
+  const int layer = rest / a.splits;
+
+  const char* __restrict__ dZl = Ls.dZ[layer] + coch * 256;
+  const char* __restrict__ Xl = Ls.X[layer] + cich * 128;
+  const int Mb = a.M * 2, Xb = a.Cx * 2;
+  const int Gmax = a.B * WFF;
+  const int T = a.B * STEPS_PER_BOARD;
+  const int s0 = (int)((long long)zsplit * T / a.splits);
+  const int s1 = (int)((long long)(zsplit + 1) * T / a.splits);
+
+  // one 1-KB block of X ring rows r0 .. r0+7
+  auto x_block = [&](int r0) {
+    if constexpr (ABL & 4) return;
+    const int row = r0 + (lane >> 3);
+    const int c = (lane & 7) ^ xswz(row & (XR - 1));
+    int gr = row < 0 ? 0 : row;
+    gr = gr >= Gmax ? Gmax - 1 : gr;
+    dma16(Xl + (size_t)gr * Xb + c * 16,
+          __builtin_amdgcn_readfirstlane(xring_u + (r0 & (XR - 1)) * 128));
+  };
+  // 32 dZ rows of step g0 into buffer buf: one 1-KB block (4 rows) per wave
+  auto dz_block = [&](int buf, int g0) {
+    if constexpr (ABL & 4) return;
+    const int r = wave * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ dswz(r);
+    dma16(dZl + (size_t)(g0 + r) * Mb + c * 16,
+          __builtin_amdgcn_readfirstlane(dz_u + buf * DZB + wave * 1024));
+  };
+  int loaded_hi = 0;
+  // steady-state issue for step sn into dZ buffer buf: exactly 2 DMAs per wave
+  auto issue = [&](int sn, int buf) {
+    const int g0n = step_g0(sn);
+    int lo = (g0n - 22) & ~7;
+    if (lo < loaded_hi) lo = loaded_hi;
+    const int hi = (g0n + 54 + 7) & ~7;
+    const int nblk = (hi - lo) >> 3;  // 4 .. 8 (4 inside a board, 7-8 across boards)
+    x_block(lo + 8 * (wave < nblk ? wave : wave - nblk));
+    loaded_hi = hi;
+    dz_block(buf, g0n);
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int g = lane >> 4;
+  const int q = li >> 2, pp = li & 3;
+  const int p1 = pp >> 1, p0 = (pp & 1) * 8;
+
+  if (s0 < s1) {
+    const int g0 = step_g0(s0);
+    const int lo = (g0 - 22) & ~7;
+    loaded_hi = (g0 + 54 + 7) & ~7;
+    for (int k = wave; k < ((loaded_hi - lo) >> 3); k += 8) x_block(lo + 8 * k);
+    dz_block(0, g0);
+    dma_wait<0>();
+    __syncthreads();
+#pragma unroll
+    for (int p = 1; p < PD; ++p)
+      if (s0 + p < s1) issue(s0 + p, p);
+  }
+  // Per-lane LDS read addresses.  dZ: fixed per (i, h) + the step's buffer base.  X: the
+  // ring slot of tap t / half h is (g0 + off_t + rl) & 255 and its 16-B chunk is XOR-ed by
+  // bits 1 and 3 of the slot; inside a board g0 advances by 32 (slot += 32 keeps bits 1, 3),
+  // so the address is (rel + 4096 j) & 0x7fff with rel computed once per board.
+  int rel_d[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int rl = 8 * g + 4 * h + q;
+    const int sw = dswz(rl);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rel_d[h][i] = rl * 256 + (((8 * wm + 2 * i + p1) ^ sw) * 16) + p0;
+  }
+  int rel_x[9][2];
+  auto board_rel = [&](int gb) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int off = (t / 3 - 1) * WF + (t % 3 - 1);
+        const int slot = (gb + off + 8 * g + 4 * h + q) & (XR - 1);
+        rel_x[t][h] = slot * 128 + (((2 * wn + p1) ^ xswz(slot)) * 16) + p0;
+      }
+  };
+  int bsteps = s0 / STEPS_PER_BOARD;           // board of step st
+  int j = s0 - bsteps * STEPS_PER_BOARD;       // step within the board
+  board_rel(bsteps * WFF + WF);
+  int buf = 0;        // dZ buffer of step st
+  int buf_pd = PD;    // dZ buffer of step st + PD
+  for (int st = s0; st < s1; ++st) {
+    if (st + PD < s1) issue(st + PD, buf_pd);
+    if (j == STEPS_PER_BOARD) {
+      j = 0;
+      ++bsteps;
+      board_rel(bsteps * WFF + WF);
+    }
+    const int jo = j * 4096;
+    const char* sD = dzbuf + buf * DZB;
+    s16x4 ta[2][4], tb[2][9];
+    if constexpr (ABL & 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ta[h][i] = s16x4{};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) tb[h][t] = s16x4{};
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ta[h][i] = lds_read_tr((const LDS_AS char*)(sD + rel_d[h][i]));
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          tb[h][t] = lds_read_tr((const LDS_AS char*)(xring + ((rel_x[t][h] + jo) & (XRING - 1))));
+    }
+    bf16x8 af[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const s16x4 lo = ta[0][i], hi = ta[1][i];
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const s16x4 lo = tb[0][t], hi = tb[1][t];
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, v);
+      if constexpr (ABL & 1) {
+        asm volatile("" ::"v"(bfr));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
+      }
+    }
+    if (st + PD < s1)
+      dma_wait<2 * (PD - 1)>();  // this wave's DMAs of step st+1 landed
+    else
+      dma_wait<0>();
+    __syncthreads();
+    buf = buf == PD ? 0 : buf + 1;
+    buf_pd = buf_pd == PD ? 0 : buf_pd + 1;
+    ++j;
+  }
+
+  float* slab = Ls.slab[layer] + (size_t)zsplit * a.Mpad * a.KP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = coch * 128 + wm * 64 + i * 16 + g * 4 + r;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int k = t * a.Cx + cich * 64 + wn * 16 + li;
+        slab[(size_t)co * a.KP + k] = acc[i][t][r];
+      }
+    }
+  }
+}
+
+int g_win_ablate = 0;
+int g_win_pd = 4;
+
+}  // namespace
+
+extern "C" {
+
+void dg_conv_wgrad_win_set_ablate(int mode) { g_win_ablate = mode; }
+void dg_conv_wgrad_win_set_pd(int pd) { g_win_pd = pd; }
+
+// Splits per (layer, chunk pair) that fill num_cus CUs with one workgroup each in one round.
+// At least 8 K-steps per split (the prologue loads a full window).
+int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
+  const int pairs = nl * (M / 128) * (Cx / 64);
+  int s = pairs > 0 ? num_cus / pairs : 1;
+  const int smax = B * STEPS_PER_BOARD / 8;
+  if (s > smax) s = smax;
+  return s < 1 ? 1 : s;
+}
+
+// table = nl rows of {dZ frame (pad 1, M channels), X frame (pad 1, Cx channels), slab}.
+hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
+                             int KP, int splits, hipStream_t stream) {
+  if (nl <= 0 || nl > MAXL || M % 128 != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
+      B <= 0 || splits <= 0 || splits > B * STEPS_PER_BOARD)
+    return hipErrorInvalidValue;
+  WinLayers Ls{};
+  for (int i = 0; i < nl; ++i) {
+    Ls.dZ[i] = (const char*)table[3 * i];
+    Ls.X[i] = (const char*)table[3 * i + 1];
+    Ls.slab[i] = (float*)table[3 * i + 2];
+    if (!Ls.dZ[i] || !Ls.X[i] || !Ls.slab[i]) return hipErrorInvalidValue;
+  }
+  WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
+  const dim3 grid(nl * (M / 128) * (Cx / 64) * splits);
+  if (g_win_ablate & 7) {
+    switch (g_win_ablate & 7) {
+#define WIN_CASE(n) \
+  case n: hipLaunchKernelGGL((conv_wgrad_win_kernel<n, 2>), grid, dim3(512), 0, stream, a, Ls); break;
+      WIN_CASE(1) WIN_CASE(2) WIN_CASE(3) WIN_CASE(4) WIN_CASE(5) WIN_CASE(6) WIN_CASE(7)
+#undef WIN_CASE
+    }
+  } else if (g_win_pd == 1) {
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 1>), grid, dim3(512), 0, stream, a, Ls);
+  } else if (g_win_pd == 3) {
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 3>), grid, dim3(512), 0, stream, a, Ls);
+  } else if (g_win_pd == 4) {
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 4>), grid, dim3(512), 0, stream, a, Ls);
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 2>), grid, dim3(512), 0, stream, a, Ls);
+  }
+  return hipGetLastError();
+}
+
+}  // extern "C"

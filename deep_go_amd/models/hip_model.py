@@ -493,6 +493,7 @@ class HipGoNet:
         hidden layers in one launch on a single GPU (12x128: 245k -> 248k boards/s,
         gpurun_out/ab.txt sweep of 4/5/7/10)."""
         self.wgroups: List[List[int]] = []
+        self.win_groups = set()
         G = int(os.environ.get("DG_WGRAD_GROUP",
                                "5" if self.global_batch != self.B else "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
@@ -524,8 +525,18 @@ class HipGoNet:
         wgs = h.conv_wgrad_wgs_per_cu_for(self.plans[groups[0][0]].KPw)
         gslab_elems = 0
         plan_splits = {}
+        win_ok = os.environ.get("DG_WGRAD_WIN", "1") != "0"
         for g in groups:
             p = self.plans[g[0]]
+            if (win_ok and p.k == 3 and lay[g[0]].pad == 1 and self.dzp[g[0]] == 1
+                    and p.cout % 128 == 0 and p.cinp % 64 == 0 and p.KPw >= 9 * p.cinp):
+                # sliding-window kernel (conv_wgrad_win.hip): one X window per K-step for
+                # all 9 taps, 43 instead of 171 B of LDS-DMA per MFMA
+                self.win_groups.add(tuple(g))
+                S = h.conv_wgrad_win_splits(len(g), p.cout, p.cinp, self.B, self.num_cus)
+                plan_splits[tuple(g)] = S
+                gslab_elems = max(gslab_elems, len(g) * S * p.Mpad_w * p.KPw)
+                continue
             tiles = (p.KPw // 384) * (p.Mpad_w // 128) * len(g)
             S = max(1, min((self.num_cus * wgs) // tiles, self.npix // 256))
             plan_splits[tuple(g)] = S
@@ -562,6 +573,9 @@ class HipGoNet:
             self._bwd[g[0]][0:3] = [
                 (h.bias_grad_partial_multi, (bt.ctypes.data, len(g), self.B, p0.cout,
                                              self.dzp[g[0]])),
+                (h.conv_wgrad_win, (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp,
+                                    self.B, p0.KPw, S))
+                if tuple(g) in self.win_groups else
                 (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
                                       S)),

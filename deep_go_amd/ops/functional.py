@@ -174,6 +174,22 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     npix = B * NPTS
     _, KPw, _ = LY.conv_dims(k, cinp, cout, 128)
     Mpad = LY.round_up(cout, 128)
+    if algo == "win":
+        # sliding-window kernel (conv_wgrad_win.hip): 3x3, pad-1 frames, 128-co / 64-ci chunks
+        assert k == 3 and cout % 128 == 0 and cinp % 64 == 0 and KPw >= 9 * cinp
+        splits = splits or h.conv_wgrad_win_splits(
+            1, cout, cinp, B, torch.cuda.get_device_properties(dev).multi_processor_count)
+        dzf = LY.to_frame(dz, 1)
+        xf = LY.to_frame(x.to(dev), 1, cinp)
+        slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)
+        out = torch.empty((cout, k, k, cin), dtype=torch.float32, device=dev)
+        table = torch.tensor([[dzf.data_ptr(), xf.data_ptr(), slab.data_ptr()]], dtype=torch.int64)
+        s = stream_handle()
+        h.conv_wgrad_win(table.data_ptr(), 1, cout, Mpad, cinp, B, KPw, splits, s)
+        h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, 9, cin, cinp,
+                       0, 0, 0, 0, s)
+        torch.cuda.synchronize(dev)
+        return out
     w3 = algo == "rows" or (algo == "auto" and LY.wgrad3_ok(k, cinp, pad))
     if w3:
         splits = splits or LY.pick_wgrad3_splits(B, h.wgrad3_tiles(Mpad, cinp),

@@ -169,15 +169,16 @@ def test_fused_dgrad_stack_matches_per_layer(layers, l0_mask, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("layers,group,ch,dstack", [(7, 5, 128, "1"), (9, 3, 128, "1"),
-                                                    (6, 2, 128, "1"), (6, 3, 128, "0"),
-                                                    (5, 3, 256, "1")])
-def test_grouped_wgrads_match_per_layer(layers, group, ch, dstack, monkeypatch):
-    """conv_wgrad_multi (several layers' weight gradients in one launch, fewer pixel splits
-    per layer) gives the per-layer launches' gradients up to fp32 summation order — after
-    the dgrad stack (128 channels) or after the per-layer dgrads run first (256 channels,
-    or DG_DSTACK=0)."""
+@pytest.mark.parametrize("layers,group,ch,dstack,win", [
+    (7, 5, 128, "1", "1"), (9, 3, 128, "1", "1"), (6, 2, 128, "1", "1"), (6, 3, 128, "0", "1"),
+    (5, 3, 256, "1", "1"), (7, 5, 128, "1", "0"), (5, 3, 256, "1", "0")])
+def test_grouped_wgrads_match_per_layer(layers, group, ch, dstack, win, monkeypatch):
+    """Grouped weight gradients (several layers in one launch: the sliding-window kernel
+    conv_wgrad_win, or conv_wgrad_multi with DG_WGRAD_WIN=0) give the per-layer launches'
+    gradients up to fp32 summation order — after the dgrad stack (128 channels) or after
+    the per-layer dgrads run first (256 channels, or DG_DSTACK=0)."""
     monkeypatch.setenv("DG_DSTACK", dstack)
+    monkeypatch.setenv("DG_WGRAD_WIN", win)
     monkeypatch.setenv("DG_WGRAD_GROUP", "1")
     monkeypatch.setenv("DG_DGRAD_FIRST", "0")
     _, n0, _ = _setup(layers, ch, 6, seed=11)
@@ -185,6 +186,7 @@ def test_grouped_wgrads_match_per_layer(layers, group, ch, dstack, monkeypatch):
     monkeypatch.setenv("DG_DGRAD_FIRST", "1")
     _, n1, _ = _setup(layers, ch, 6, seed=11)
     assert not n0.wgroups and n1.wgroups and max(len(g) for g in n1.wgroups) <= group
+    assert bool(n1.win_groups) == (win == "1")
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
