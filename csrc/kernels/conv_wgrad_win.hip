@@ -34,7 +34,6 @@ constexpr int WFF = WF * WF;        // 441 rows per board
 constexpr int STEPS_PER_BOARD = 13; // 13 x 32 = 416 rows from frame row 1
 constexpr int XR = 256;             // X ring rows (128 B each)
 constexpr int XRING = XR * 128;     // 32 KB
-constexpr int DZB = 32 * 256;       // one dZ step: 32 rows x 128 co bf16
 constexpr int MAXL = 16;
 
 struct WinLayers {
@@ -72,9 +71,19 @@ DG_DEV int step_g0(int s) {
 // wave issues exactly 2 per steady-state step (one dZ block, one X block; a wave with no
 // new X block re-loads one that another wave loads, same bytes), so "DMAs of step st+1
 // landed" = vmcnt(2 (PD - 1)).
-template <int ABL, int PD>
-__global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
+//
+// NW: waves per workgroup.  8: 128-co chunks, one workgroup per CU; 4: 64-co chunks, two
+// independent workgroups per CU (their K-step barriers are not in lockstep, so one's LDS
+// reads overlap the other's MFMAs).  Every wave owns 64 co x 9 taps x 16 ci either way.
+template <int ABL, int PD, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
   static_assert(PD >= 1 && PD <= 4, "prefetch distance");
+  static_assert(NW == 4 || NW == 8, "waves");
+  constexpr int COCH = 16 * NW;        // co per workgroup (64 or 128)
+  constexpr int DZR = 2 * COCH;        // dZ LDS row bytes
+  constexpr int DZB = 32 * DZR;        // one dZ step (32 rows); NW 1-KB blocks
+  constexpr int XPW = 8 / (NW / 4) / 4 * 1;  // X blocks per wave per step: NW 8 -> 1, 4 -> 2
+  static_assert(XPW * NW >= 8, "steady-state X blocks");
   __shared__ __attribute__((aligned(16))) char smem[XRING + (PD + 1) * DZB];
   char* xring = smem;
   char* dzbuf = smem + XRING;
@@ -84,22 +93,22 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave >> 2, wn = wave & 3;  // wm = 0 when NW = 4
 
-  const int nci = a.Cx / 64, nco = a.M / 128;
+  const int nci = a.Cx / 64, nco = a.M / COCH;
   const int nwg = a.nl * nco * nci * a.splits;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, xslot = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
-  const int cich = lid % nci;
-  int rest = lid / nci;
-  const int coch = rest % nco;
-  rest /= nco;
+  const int coch = lid % nco;   // co chunks of one (layer, split) adjacent: same XCD / L2
+  int rest = lid / nco;
+  const int cich = rest % nci;
+  rest /= nci;
   const int zsplit = rest % a.splits;
   const int layer = rest / a.splits;
 
-  const char* __restrict__ dZl = Ls.dZ[layer] + coch * 256;
+  const char* __restrict__ dZl = Ls.dZ[layer] + coch * DZR;
   const char* __restrict__ Xl = Ls.X[layer] + cich * 128;
   const int Mb = a.M * 2, Xb = a.Cx * 2;
   const int Gmax = a.B * WFF;
@@ -117,23 +126,40 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
     dma16(Xl + (size_t)gr * Xb + c * 16,
           __builtin_amdgcn_readfirstlane(xring_u + (r0 & (XR - 1)) * 128));
   };
-  // 32 dZ rows of step g0 into buffer buf: one 1-KB block (4 rows) per wave
+  // 32 dZ rows of step g0 into buffer buf: one 1-KB block per wave
   auto dz_block = [&](int buf, int g0) {
     if constexpr (ABL & 4) return;
-    const int r = wave * 4 + (lane >> 4);
-    const int c = (lane & 15) ^ dswz(r);
+    int r, c;
+    if constexpr (NW == 8) {
+      r = wave * 4 + (lane >> 4);
+      c = (lane & 15) ^ dswz(r);
+    } else {
+      r = wave * 8 + (lane >> 3);
+      c = (lane & 7) ^ xswz(r);
+    }
     dma16(dZl + (size_t)(g0 + r) * Mb + c * 16,
           __builtin_amdgcn_readfirstlane(dz_u + buf * DZB + wave * 1024));
   };
   int loaded_hi = 0;
-  // steady-state issue for step sn into dZ buffer buf: exactly 2 DMAs per wave
+  // steady-state issue for step sn into dZ buffer buf: exactly XPW + 1 DMAs per wave
   auto issue = [&](int sn, int buf) {
     const int g0n = step_g0(sn);
     int lo = (g0n - 22) & ~7;
     if (lo < loaded_hi) lo = loaded_hi;
     const int hi = (g0n + 54 + 7) & ~7;
     const int nblk = (hi - lo) >> 3;  // 4 .. 8 (4 inside a board, 7-8 across boards)
-    x_block(lo + 8 * (wave < nblk ? wave : wave - nblk));
+    if constexpr (NW == 4) {
+      // 1 X block per wave inside a board, 2 at a board's first step (7-8 new blocks;
+      // a wave without an 8th block re-loads block 0, same bytes)
+      x_block(lo + 8 * wave);
+      if (nblk > 4) x_block(lo + 8 * (wave + 4 < nblk ? wave + 4 : 0));
+    } else {
+#pragma unroll
+      for (int u = 0; u < XPW; ++u) {
+        const int k = wave + NW * u;
+        x_block(lo + 8 * (k < nblk ? k : k - nblk));
+      }
+    }
     loaded_hi = hi;
     dz_block(buf, g0n);
   };
@@ -153,7 +179,7 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
     const int g0 = step_g0(s0);
     const int lo = (g0 - 22) & ~7;
     loaded_hi = (g0 + 54 + 7) & ~7;
-    for (int k = wave; k < ((loaded_hi - lo) >> 3); k += 8) x_block(lo + 8 * k);
+    for (int k = wave; k < ((loaded_hi - lo) >> 3); k += NW) x_block(lo + 8 * k);
     dz_block(0, g0);
     dma_wait<0>();
     __syncthreads();
@@ -169,9 +195,9 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int rl = 8 * g + 4 * h + q;
-    const int sw = dswz(rl);
+    const int sw = NW == 8 ? dswz(rl) : xswz(rl);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rel_d[h][i] = rl * 256 + (((8 * wm + 2 * i + p1) ^ sw) * 16) + p0;
+    for (int i = 0; i < 4; ++i) rel_d[h][i] = rl * DZR + (((8 * wm + 2 * i + p1) ^ sw) * 16) + p0;
   }
   int rel_x[9][2];
   auto board_rel = [&](int gb) {
@@ -237,10 +263,21 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
         for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
       }
     }
-    if (st + PD < s1)
-      dma_wait<2 * (PD - 1)>();  // this wave's DMAs of step st+1 landed
-    else
+    if (st + PD < s1) {
+      // this wave's DMAs of step st+1 landed: the DMAs of steps st+2 .. st+PD may remain
+      if constexpr (NW == 4) {
+        // 2 per step, 3 at a board's first step (at most one in any 3 consecutive steps)
+        const int r = (st + 2) % STEPS_PER_BOARD;
+        if (r == 0 || r + PD - 2 >= STEPS_PER_BOARD)
+          dma_wait<2 * (PD - 1) + 1>();
+        else
+          dma_wait<2 * (PD - 1)>();
+      } else {
+        dma_wait<(XPW + 1) * (PD - 1)>();
+      }
+    } else {
       dma_wait<0>();
+    }
     __syncthreads();
     buf = buf == PD ? 0 : buf + 1;
     buf_pd = buf_pd == PD ? 0 : buf_pd + 1;
@@ -252,7 +289,7 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = coch * 128 + wm * 64 + i * 16 + g * 4 + r;
+      const int co = coch * COCH + wm * 64 + i * 16 + g * 4 + r;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int k = t * a.Cx + cich * 64 + wn * 16 + li;
@@ -264,19 +301,27 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_win_kernel(WinArgs a, WinLa
 
 int g_win_ablate = 0;
 int g_win_pd = 4;
+int g_win_nw = 4;
+
+template <int ABL, int PD, int NW>
+void launch_win(dim3 grid, const WinArgs& a, const WinLayers& Ls, hipStream_t stream) {
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW>), grid, dim3(64 * NW), 0, stream, a,
+                     Ls);
+}
 
 }  // namespace
 
 extern "C" {
 
 void dg_conv_wgrad_win_set_ablate(int mode) { g_win_ablate = mode; }
-void dg_conv_wgrad_win_set_pd(int pd) { g_win_pd = pd; }
+void dg_conv_wgrad_win_set_pd(int pd) { g_win_pd = pd == 2 ? 2 : 4; }
+void dg_conv_wgrad_win_set_nw(int nw) { g_win_nw = nw == 8 ? 8 : 4; }
 
-// Splits per (layer, chunk pair) that fill num_cus CUs with one workgroup each in one round.
-// At least 8 K-steps per split (the prologue loads a full window).
+// Splits per (layer, chunk pair) that fill num_cus CUs in one round (8 / NW workgroups per
+// CU).  At least 8 K-steps per split (the prologue loads a full window).
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
-  const int pairs = nl * (M / 128) * (Cx / 64);
-  int s = pairs > 0 ? num_cus / pairs : 1;
+  const int pairs = nl * (M / (16 * g_win_nw)) * (Cx / 64);
+  int s = pairs > 0 ? num_cus * (8 / g_win_nw) / pairs : 1;
   const int smax = B * STEPS_PER_BOARD / 8;
   if (s > smax) s = smax;
   return s < 1 ? 1 : s;
@@ -285,7 +330,8 @@ int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
 // table = nl rows of {dZ frame (pad 1, M channels), X frame (pad 1, Cx channels), slab}.
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                              int KP, int splits, hipStream_t stream) {
-  if (nl <= 0 || nl > MAXL || M % 128 != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
+  const int coch = 16 * g_win_nw;
+  if (nl <= 0 || nl > MAXL || M % coch != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || splits <= 0 || splits > B * STEPS_PER_BOARD)
     return hipErrorInvalidValue;
   WinLayers Ls{};
@@ -296,22 +342,21 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
     if (!Ls.dZ[i] || !Ls.X[i] || !Ls.slab[i]) return hipErrorInvalidValue;
   }
   WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
-  const dim3 grid(nl * (M / 128) * (Cx / 64) * splits);
-  if (g_win_ablate & 7) {
-    switch (g_win_ablate & 7) {
-#define WIN_CASE(n) \
-  case n: hipLaunchKernelGGL((conv_wgrad_win_kernel<n, 2>), grid, dim3(512), 0, stream, a, Ls); break;
+  const dim3 grid(nl * (M / coch) * (Cx / 64) * splits);
+  const bool w8 = g_win_nw == 8;
+  switch (g_win_ablate & 7) {
+    case 0:
+      if (g_win_pd == 2)
+        w8 ? launch_win<0, 2, 8>(grid, a, Ls, stream) : launch_win<0, 2, 4>(grid, a, Ls, stream);
+      else
+        w8 ? launch_win<0, 4, 8>(grid, a, Ls, stream) : launch_win<0, 4, 4>(grid, a, Ls, stream);
+      break;
+#define WIN_CASE(n)                                                                     \
+  case n:                                                                               \
+    w8 ? launch_win<n, 4, 8>(grid, a, Ls, stream) : launch_win<n, 4, 4>(grid, a, Ls, stream); \
+    break;
       WIN_CASE(1) WIN_CASE(2) WIN_CASE(3) WIN_CASE(4) WIN_CASE(5) WIN_CASE(6) WIN_CASE(7)
 #undef WIN_CASE
-    }
-  } else if (g_win_pd == 1) {
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 1>), grid, dim3(512), 0, stream, a, Ls);
-  } else if (g_win_pd == 3) {
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 3>), grid, dim3(512), 0, stream, a, Ls);
-  } else if (g_win_pd == 4) {
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 4>), grid, dim3(512), 0, stream, a, Ls);
-  } else {
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<0, 2>), grid, dim3(512), 0, stream, a, Ls);
   }
   return hipGetLastError();
 }

@@ -529,7 +529,7 @@ class HipGoNet:
         for g in groups:
             p = self.plans[g[0]]
             if (win_ok and p.k == 3 and lay[g[0]].pad == 1 and self.dzp[g[0]] == 1
-                    and p.cout % 128 == 0 and p.cinp % 64 == 0 and p.KPw >= 9 * p.cinp):
+                    and p.cout % 64 == 0 and p.cinp % 64 == 0 and p.KPw >= 9 * p.cinp):
                 # sliding-window kernel (conv_wgrad_win.hip): one X window per K-step for
                 # all 9 taps, 43 instead of 171 B of LDS-DMA per MFMA
                 self.win_groups.add(tuple(g))

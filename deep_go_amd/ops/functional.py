@@ -175,8 +175,8 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     _, KPw, _ = LY.conv_dims(k, cinp, cout, 128)
     Mpad = LY.round_up(cout, 128)
     if algo == "win":
-        # sliding-window kernel (conv_wgrad_win.hip): 3x3, pad-1 frames, 128-co / 64-ci chunks
-        assert k == 3 and cout % 128 == 0 and cinp % 64 == 0 and KPw >= 9 * cinp
+        # sliding-window kernel (conv_wgrad_win.hip): 3x3, pad-1 frames, 64-co / 64-ci chunks
+        assert k == 3 and cout % 64 == 0 and cinp % 64 == 0 and KPw >= 9 * cinp
         splits = splits or h.conv_wgrad_win_splits(
             1, cout, cinp, B, torch.cuda.get_device_properties(dev).multi_processor_count)
         dzf = LY.to_frame(dz, 1)

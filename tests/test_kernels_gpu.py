@@ -245,15 +245,24 @@ def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
 
 @pytest.mark.parametrize("B,cin,cout,splits", [
     (3, 128, 128, None), (1, 128, 128, 1), (2, 128, 128, 26), (5, 256, 256, None),
-    (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5)])
-def test_conv_wgrad_win(B, cin, cout, splits):
+    (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5), (3, 128, 64, None)])
+@pytest.mark.parametrize("nw", [4, 8])
+def test_conv_wgrad_win(B, cin, cout, splits, nw):
     """Sliding-window 3x3 wgrad (conv_wgrad_win.hip: frame-linear K, one X window for all 9
-    taps, split ranges that start / end inside a board) vs the fp32 reference."""
+    taps, split ranges that start / end inside a board; 4- and 8-wave workgroups) vs the
+    fp32 reference."""
+    if cout % (16 * nw):
+        pytest.skip("co chunk")
     torch.manual_seed(6)
     from deep_go_amd.ops import functional as Fn
+    from deep_go_amd.ops.native import hip
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
+    hip().conv_wgrad_win_set_nw(nw)
+    try:
+        got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
+    finally:
+        hip().conv_wgrad_win_set_nw(4)
     w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
     (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
     assert rel_err(got, gw) < 1e-3

@@ -35,7 +35,7 @@ def main():
     flops = 2.0 * C * C * 9 * 361 * B * NL
     res, cfg = {}, {}
     Sw = h.conv_wgrad_win_splits(NL, C, C, B, ncu)
-    slab_w = torch.empty(NL * Sw * C * KPw, device=dev)
+    slab_w = torch.empty(NL * 2 * Sw * C * KPw, device=dev)
     per = Sw * C * KPw
     tw = np.array([[dzs[i].data_ptr(), xs[i].data_ptr(), slab_w.data_ptr() + 4 * i * per]
                    for i in range(NL)], dtype=np.int64)
@@ -55,11 +55,19 @@ def main():
     for rnd in range(2):
         for mode in (1, 2, 4, 3, 5, 6, 7):
             h.conv_wgrad_win_set_ablate(mode)
-            res.setdefault(f"win_abl{mode}_pd2", []).append(round(timeit(win), 2))
+            res.setdefault(f"win_nw4_abl{mode}", []).append(round(timeit(win), 2))
         h.conv_wgrad_win_set_ablate(0)
-        for pd in (1, 2, 3, 4):
-            h.conv_wgrad_win_set_pd(pd)
-            res.setdefault(f"win_pd{pd}", []).append(round(timeit(win), 2))
+        for nw in (8, 4):
+            h.conv_wgrad_win_set_nw(nw)
+            for pd in (2, 4):
+                h.conv_wgrad_win_set_pd(pd)
+                Sn = h.conv_wgrad_win_splits(NL, C, C, B, ncu)
+                if Sn * C * KPw * NL > slab_w.numel():
+                    continue
+
+                def winn():
+                    h.conv_wgrad_win(tw.ctypes.data, NL, C, C, C, B, KPw, Sn, s)
+                res.setdefault(f"win_nw{nw}_pd{pd}_S{Sn}", []).append(round(timeit(winn), 2))
         h.conv_wgrad_win_set_pd(4)
         res.setdefault("t3_multi", []).append(round(timeit(t3), 2))
     out = {k: {"us": v, "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
