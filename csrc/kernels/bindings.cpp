@@ -53,6 +53,7 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
 void dg_conv_wgrad_win_set_ablate(int mode);
 void dg_conv_wgrad_win_set_pd(int pd);
 void dg_conv_wgrad_win_set_nw(int nw);
+void dg_conv_wgrad_win_set_swp(int on);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                              int KP, int splits, hipStream_t stream);
@@ -345,6 +346,8 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_wgrad_win_set_ablate", [](int mode) { dg_conv_wgrad_win_set_ablate(mode); });
   m.def("conv_wgrad_win_set_pd", [](int pd) { dg_conv_wgrad_win_set_pd(pd); },
         "LDS-DMA prefetch distance of conv_wgrad_win in K-steps (2 or 4, default 4)");
+  m.def("conv_wgrad_win_set_swp", [](int on) { dg_conv_wgrad_win_set_swp(on); },
+        "software-pipelined conv_wgrad_win K-loop (default 0: measured slower with 4-wave workgroups)");
   m.def("conv_wgrad_win_set_nw", [](int nw) { dg_conv_wgrad_win_set_nw(nw); },
         "waves per conv_wgrad_win workgroup: 4 (64-co chunks, 2 per CU; default) or 8");
   m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });

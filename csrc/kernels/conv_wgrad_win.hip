@@ -64,7 +64,9 @@ DG_DEV int step_g0(int s) {
   return b * WFF + WF + 32 * (s - b * STEPS_PER_BOARD);
 }
 
-// ABL: ablation bits (diagnostics; 0 in production): 1 no MFMA, 2 no LDS reads, 4 no DMA.
+// ABL: ablation bits (diagnostics; 0 in production): 1 no MFMA, 2 no LDS reads, 4 no DMA,
+// 8 X read addresses fixed per board (no per-step address VALU; wrong data), 16 no K-step
+// barrier (races; timing only).
 // PD: LDS-DMA prefetch distance in K-steps (dZ buffers = PD + 1; the X ring holds the
 // current window plus PD steps ahead: <= 22 + 54 + 57 + 32 (PD - 1) + 8 rows < 256 for
 // PD <= 4).  The DMAs are issued from inline asm (dma16) with hand vmcnt accounting: every
@@ -75,7 +77,7 @@ DG_DEV int step_g0(int s) {
 // NW: waves per workgroup.  8: 128-co chunks, one workgroup per CU; 4: 64-co chunks, two
 // independent workgroups per CU (their K-step barriers are not in lockstep, so one's LDS
 // reads overlap the other's MFMAs).  Every wave owns 64 co x 9 taps x 16 ci either way.
-template <int ABL, int PD, int NW>
+template <int ABL, int PD, int NW, bool SWP>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
   static_assert(PD >= 1 && PD <= 4, "prefetch distance");
   static_assert(NW == 4 || NW == 8, "waves");
@@ -215,6 +217,102 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
   board_rel(bsteps * WFF + WF);
   int buf = 0;        // dZ buffer of step st
   int buf_pd = PD;    // dZ buffer of step st + PD
+  // this wave's DMAs of step st+1 landed: the DMAs of steps st+2 .. st+PD may remain
+  auto wait_next = [&](int st) {
+    if (st + PD < s1) {
+      if constexpr (NW == 4) {
+        // 2 per step, 3 at a board's first step (at most one in any 3 consecutive steps)
+        const int r = (st + 2) % STEPS_PER_BOARD;
+        if (r == 0 || r + PD - 2 >= STEPS_PER_BOARD)
+          dma_wait<2 * (PD - 1) + 1>();
+        else
+          dma_wait<2 * (PD - 1)>();
+      } else {
+        dma_wait<(XPW + 1) * (PD - 1)>();
+      }
+    } else {
+      dma_wait<0>();
+    }
+  };
+  if constexpr (SWP) {
+    // Software-pipelined K-steps: the taps run as three kernel-row groups, each group's B
+    // fragments read under the previous group's MFMAs, and the NEXT step's A fragments and
+    // first group read under the last group's MFMAs (after a mid-step barrier that makes
+    // the next step's DMA data visible), so no MFMA waits on a fresh LDS read.
+    // half h = 1 is rows +4: bits 1 and 3 of the row (the swizzle) are unchanged, so its
+    // address is h = 0's + 4 rows (an immediate offset)
+    auto readA = [&](s16x4 (&ta)[2][4], int bf) {
+      const char* sD = dzbuf + bf * DZB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ta[0][i] = lds_read_tr((const LDS_AS char*)(sD + rel_d[0][i]));
+        ta[1][i] = lds_read_tr((const LDS_AS char*)(sD + rel_d[0][i] + 4 * DZR));
+      }
+    };
+    auto readB = [&](s16x4 (&tb)[2][3], int dy, int jo) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          tb[h][u] = lds_read_tr(
+              (const LDS_AS char*)(xring + ((rel_x[3 * dy + u][h] + jo) & (XRING - 1))));
+    };
+    auto mm = [&](const s16x4 (&ta)[2][4], const s16x4 (&tb)[2][3], int dy) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s16x4 lo = ta[0][i], hi = ta[1][i];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const s16x4 lo = tb[0][u], hi = tb[1][u];
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][3 * dy + u] = mfma16(af[i], bfr, acc[i][3 * dy + u]);
+      }
+    };
+    s16x4 ta[2][4], tn[2][4], b0[2][3], b1[2][3], b2[2][3];
+    int jo = j * 4096;
+    if (s0 < s1) {
+      readA(ta, 0);
+      readB(b0, 0, jo);
+    }
+    for (int st = s0; st < s1; ++st) {
+      if (st + PD < s1) issue(st + PD, buf_pd);
+      readB(b1, 1, jo);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(ta, b0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      readB(b2, 2, jo);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(ta, b1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      wait_next(st);
+      __builtin_amdgcn_s_barrier();
+      buf = buf == PD ? 0 : buf + 1;
+      buf_pd = buf_pd == PD ? 0 : buf_pd + 1;
+      if (++j == STEPS_PER_BOARD) {
+        j = 0;
+        ++bsteps;
+        board_rel(bsteps * WFF + WF);
+      }
+      jo = j * 4096;
+      if (st + 1 < s1) {
+        readA(tn, buf);
+        readB(b0, 0, jo);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mm(ta, b2, 2);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ta[h][i] = tn[h][i];
+    }
+  } else {
   for (int st = s0; st < s1; ++st) {
     if (st + PD < s1) issue(st + PD, buf_pd);
     if (j == STEPS_PER_BOARD) {
@@ -242,7 +340,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
       for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          tb[h][t] = lds_read_tr((const LDS_AS char*)(xring + ((rel_x[t][h] + jo) & (XRING - 1))));
+          tb[h][t] = lds_read_tr((const LDS_AS char*)(
+              xring + ((ABL & 8) ? rel_x[t][h] : ((rel_x[t][h] + jo) & (XRING - 1)))));
     }
     bf16x8 af[4];
 #pragma unroll
@@ -263,25 +362,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
         for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
       }
     }
-    if (st + PD < s1) {
-      // this wave's DMAs of step st+1 landed: the DMAs of steps st+2 .. st+PD may remain
-      if constexpr (NW == 4) {
-        // 2 per step, 3 at a board's first step (at most one in any 3 consecutive steps)
-        const int r = (st + 2) % STEPS_PER_BOARD;
-        if (r == 0 || r + PD - 2 >= STEPS_PER_BOARD)
-          dma_wait<2 * (PD - 1) + 1>();
-        else
-          dma_wait<2 * (PD - 1)>();
-      } else {
-        dma_wait<(XPW + 1) * (PD - 1)>();
-      }
-    } else {
-      dma_wait<0>();
-    }
-    __syncthreads();
+    wait_next(st);
+    if constexpr (!(ABL & 16)) __syncthreads();
     buf = buf == PD ? 0 : buf + 1;
     buf_pd = buf_pd == PD ? 0 : buf_pd + 1;
     ++j;
+  }
+
   }
 
   float* slab = Ls.slab[layer] + (size_t)zsplit * a.Mpad * a.KP;
@@ -302,11 +389,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
 int g_win_ablate = 0;
 int g_win_pd = 4;
 int g_win_nw = 4;
+int g_win_swp = 0;
 
-template <int ABL, int PD, int NW>
+template <int ABL, int PD, int NW, bool SWP = false>
 void launch_win(dim3 grid, const WinArgs& a, const WinLayers& Ls, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW>), grid, dim3(64 * NW), 0, stream, a,
-                     Ls);
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW, SWP>), grid, dim3(64 * NW), 0, stream,
+                     a, Ls);
 }
 
 }  // namespace
@@ -316,6 +404,7 @@ extern "C" {
 void dg_conv_wgrad_win_set_ablate(int mode) { g_win_ablate = mode; }
 void dg_conv_wgrad_win_set_pd(int pd) { g_win_pd = pd == 2 ? 2 : 4; }
 void dg_conv_wgrad_win_set_nw(int nw) { g_win_nw = nw == 8 ? 8 : 4; }
+void dg_conv_wgrad_win_set_swp(int on) { g_win_swp = on; }
 
 // Splits per (layer, chunk pair) that fill num_cus CUs in one round (8 / NW workgroups per
 // CU).  At least 8 K-steps per split (the prologue loads a full window).
@@ -344,9 +433,12 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
   WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / coch) * (Cx / 64) * splits);
   const bool w8 = g_win_nw == 8;
-  switch (g_win_ablate & 7) {
+  switch (g_win_ablate & 31) {
     case 0:
-      if (g_win_pd == 2)
+      if (g_win_swp)
+        w8 ? launch_win<0, 4, 8, true>(grid, a, Ls, stream)
+           : launch_win<0, 4, 4, true>(grid, a, Ls, stream);
+      else if (g_win_pd == 2)
         w8 ? launch_win<0, 2, 8>(grid, a, Ls, stream) : launch_win<0, 2, 4>(grid, a, Ls, stream);
       else
         w8 ? launch_win<0, 4, 8>(grid, a, Ls, stream) : launch_win<0, 4, 4>(grid, a, Ls, stream);
@@ -356,6 +448,7 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
     w8 ? launch_win<n, 4, 8>(grid, a, Ls, stream) : launch_win<n, 4, 4>(grid, a, Ls, stream); \
     break;
       WIN_CASE(1) WIN_CASE(2) WIN_CASE(3) WIN_CASE(4) WIN_CASE(5) WIN_CASE(6) WIN_CASE(7)
+      WIN_CASE(8) WIN_CASE(12) WIN_CASE(16) WIN_CASE(20) WIN_CASE(22)
 #undef WIN_CASE
   }
   return hipGetLastError();

@@ -246,11 +246,11 @@ def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
 @pytest.mark.parametrize("B,cin,cout,splits", [
     (3, 128, 128, None), (1, 128, 128, 1), (2, 128, 128, 26), (5, 256, 256, None),
     (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5), (3, 128, 64, None)])
-@pytest.mark.parametrize("nw", [4, 8])
-def test_conv_wgrad_win(B, cin, cout, splits, nw):
+@pytest.mark.parametrize("nw,swp", [(4, 1), (8, 1), (4, 0)])
+def test_conv_wgrad_win(B, cin, cout, splits, nw, swp):
     """Sliding-window 3x3 wgrad (conv_wgrad_win.hip: frame-linear K, one X window for all 9
-    taps, split ranges that start / end inside a board; 4- and 8-wave workgroups) vs the
-    fp32 reference."""
+    taps, split ranges that start / end inside a board; 4- and 8-wave workgroups, pipelined
+    and plain K-loops) vs the fp32 reference."""
     if cout % (16 * nw):
         pytest.skip("co chunk")
     torch.manual_seed(6)
@@ -259,10 +259,12 @@ def test_conv_wgrad_win(B, cin, cout, splits, nw):
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
     hip().conv_wgrad_win_set_nw(nw)
+    hip().conv_wgrad_win_set_swp(swp)
     try:
         got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
     finally:
         hip().conv_wgrad_win_set_nw(4)
+        hip().conv_wgrad_win_set_swp(1)
     w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
     (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
     assert rel_err(got, gw) < 1e-3
