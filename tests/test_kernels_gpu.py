@@ -264,7 +264,7 @@ def test_conv_wgrad_win(B, cin, cout, splits, nw, swp):
         got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
     finally:
         hip().conv_wgrad_win_set_nw(4)
-        hip().conv_wgrad_win_set_swp(1)
+        hip().conv_wgrad_win_set_swp(0)
     w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
     (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
     assert rel_err(got, gw) < 1e-3
