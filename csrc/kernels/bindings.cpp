@@ -312,7 +312,7 @@ PYBIND11_MODULE(_dghip, m) {
         "timing ablations of conv_stack (forward): 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no"
         " copy-out, 16 no barrier");
   m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },
-        "3x3/128-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
+        "3x3/128- and 256-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
   m.def("conv_stack_set_prof", [](uintptr_t p) { dg_conv_stack_set_prof(P<void>(p)); },
         "ablate 32: per-wave phase cycle sums [B][8][8] (s_memtime)");
   m.def("conv_stack_set_stagger", [](int on) { dg_conv_stack_set_stagger(on); },

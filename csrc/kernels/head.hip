@@ -391,7 +391,7 @@ static void allow_lds_once(K kernel, size_t bytes) {
   }
 }
 
-extern "C" hipError_t dg_head_mfma(const void* X, int B, const float* w, const float* bias,
+extern "C" hipError_t dg_head_mfma(int C, const void* X, int B, const float* w, const float* bias,
                                    const float* posb, const int* labels, float* loss, int* pred,
                                    float* logp_out, void* dZ, float* gw_part, float* dzb,
                                    int head_relu, float grad_scale, hipStream_t stream);
@@ -408,9 +408,9 @@ extern "C" hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, co
     const char* e = getenv("DG_HEAD_MFMA");
     g_head_mfma = e ? atoi(e) : 1;
   }
-  // 3x3 head over a 128-channel pad-1 frame: the MFMA kernel (head_mfma.hip)
-  if (g_head_mfma && kw == 3 && C == 128 && x_pad == 1 && (!dZ || dz_pad == 1))
-    return dg_head_mfma(X, B, w, bias, posb, labels, loss, pred, logp_out, dZ, gw_part, dzb,
+  // 3x3 head over a 128/256-channel pad-1 frame: the MFMA kernel (head_mfma.hip)
+  if (g_head_mfma && kw == 3 && (C == 128 || C == 256) && x_pad == 1 && (!dZ || dz_pad == 1))
+    return dg_head_mfma(C, X, B, w, bias, posb, labels, loss, pred, logp_out, dZ, gw_part, dzb,
                         head_relu, grad_scale, stream);
   if (C > CCH && C % CCH != 0) return hipErrorInvalidValue;
   if (C < CCH && (64 % (C / 8)) != 0) return hipErrorInvalidValue;  // lanes per pixel

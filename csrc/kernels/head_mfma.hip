@@ -27,7 +27,6 @@ using namespace dg;
 
 namespace {
 
-constexpr int C = 128;
 constexpr int F = 21;
 constexpr int FF = F * F;          // 441
 constexpr int HROWS = 448;
@@ -68,7 +67,14 @@ DG_DEV bf16x8 pack8(const uint16_t* v) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
+// C = 128: the board's two 64-channel images are resident for the whole kernel.
+// C = 256: the image pair holds one 128-channel half at a time — forward over half 0 then
+// half 1 (z accumulates in registers), the backward on half 1 (still resident), then half 0
+// re-staged: 3 image loads instead of 2, all GEMMs unchanged.
+template <int C>
 __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
+  static_assert(C == 128 || C == 256, "channels");
+  constexpr int NH = C / 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sX = smem;                                      // 2 images
   uint16_t* s_wb = (uint16_t*)(smem + 2 * HB);          // [T*C] bf16 weights
@@ -86,14 +92,18 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
   const int lq = lane >> 4;
   const char* Xb = a.X + (size_t)b * FF * C * 2;
 
-  // ---- stage: image (LDS-DMA, swizzled), weights, zeroed z / dz ----
-  for (int j = wave; j < 2 * (HROWS / 8); j += 8) {
-    const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
-    const int rl = jj * 8 + (lane >> 3);
-    const int r = rl < FF ? rl : FF - 1;  // rows 441.. duplicate the (zero) border row 440
-    const int g = (lane & 7) ^ fsig(rl);
-    glds16(Xb + ((size_t)r * C + c * 64 + g * 8) * 2, (LDS_AS void*)(sX + c * HB + jj * 1024));
-  }
+  // ---- stage: image of channel half hf (LDS-DMA, swizzled), weights, zeroed z / dz ----
+  auto stage = [&](int hf) {
+    for (int j = wave; j < 2 * (HROWS / 8); j += 8) {
+      const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
+      const int rl = jj * 8 + (lane >> 3);
+      const int r = rl < FF ? rl : FF - 1;  // rows 441.. duplicate the (zero) border row 440
+      const int g = (lane & 7) ^ fsig(rl);
+      glds16(Xb + ((size_t)r * C + hf * 128 + c * 64 + g * 8) * 2,
+             (LDS_AS void*)(sX + c * HB + jj * 1024));
+    }
+  };
+  stage(0);
   for (int i = tid; i < T * C; i += HT) {
     const float v = a.w[i];
     s_w[i] = v;
@@ -120,8 +130,14 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
     f32x4 acc[3];
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) acc[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < 2 * T; ++s) {
-      const int c = s / T, t = s - (s / T) * T;
+    for (int s = 0; s < 2 * T * NH; ++s) {
+      const int hs = s / (2 * T), s2 = s - hs * (2 * T);
+      if (NH > 1 && s2 == 0 && hs > 0) {
+        __syncthreads();  // every wave is past its reads of half hs-1
+        stage(hs);
+        __syncthreads();
+      }
+      const int c = s2 / T, t = s2 - (s2 / T) * T;
       const char* sXc = sX + c * HB;
       const int toff = toff_of(t);
       const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
@@ -130,7 +146,7 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
         const int g = kk * 4 + lq;
         bf16x8 af = bf16x8{};
         if (lr == 0)  // A row 0 = the weights, rows 1..15 zero
-          af = *(const bf16x8*)(s_wb + t * C + c * 64 + g * 8);
+          af = *(const bf16x8*)(s_wb + t * C + hs * 128 + c * 64 + g * 8);
 #pragma unroll
         for (int jj = 0; jj < 3; ++jj) {
           const int row = fp[jj] + toff;
@@ -210,6 +226,12 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
   }
   __syncthreads();
 
+  for (int hb = NH - 1; hb >= 0; --hb) {
+  if (hb != NH - 1) {
+    __syncthreads();  // every wave is past its reads of the resident half
+    stage(hb);
+    __syncthreads();
+  }
   // ---- weight-gradient partial: dW[t][c] = sum_f dz[f - off t] X[f][c] ----
   {
     const int ch0 = wave * 16;                  // this wave's 16 channels (N fragment)
@@ -248,7 +270,7 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t = lq * 4 + r;
-      if (t < T) gp[t * C + ch0 + lr] = acc[r];
+      if (t < T) gp[t * C + hb * 128 + ch0 + lr] = acc[r];
     }
   }
 
@@ -269,13 +291,13 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
       bl[jj] = pack8(vl);
     }
     char* dZb = a.dZ + (size_t)b * FF * C * 2;
-    for (int mi = 0; mi < C / 16; ++mi) {
+    for (int mi = 0; mi < 8; ++mi) {
       // A fragment (channels x taps): row c = mi*16 + lr, k = taps lq*8 + e
       uint16_t wh[8], wl[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int t = lq * 8 + e;
-        const float v = t < T ? s_w[t * C + mi * 16 + lr] : 0.f;
+        const float v = t < T ? s_w[t * C + hb * 128 + mi * 16 + lr] : 0.f;
         split_bf(v, wh[e], wl[e]);
       }
       const bf16x8 ah = pack8(wh), al = pack8(wl);
@@ -287,7 +309,7 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
         acc = mfma16(al, bh[jj], acc);
         if (pp3[jj] >= NPTS) continue;
         // lane: channels c .. c+3 (rows lq*4 + r of the fragment) of pixel fp[jj]
-        const int c = mi * 16 + lq * 4;
+        const int c = mi * 16 + lq * 4;  // channel within the resident half
         const int ci = c & 63;
         const uint2 xm = *(const uint2*)(sX + (c / 64) * HB + fp[jj] * 128 +
                                          (((ci >> 3) ^ (fs[jj] & 7)) * 16) + (ci & 4) * 2);
@@ -299,30 +321,36 @@ __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
         uint2 o;
         o.x = pack_bf16x2(v0, v1);
         o.y = pack_bf16x2(v2, v3);
-        *(uint2*)(dZb + ((size_t)fp[jj] * C + c) * 2) = o;
+        *(uint2*)(dZb + ((size_t)fp[jj] * C + hb * 128 + c) * 2) = o;
       }
     }
   }
+  }  // halves
 }
 
 }  // namespace
 
-// 3x3 head over a 128-channel pad-1 frame (the 12-layer configs); see dg_head for the rest.
-extern "C" hipError_t dg_head_mfma(const void* X, int B, const float* w, const float* bias,
+template <int C>
+static hipError_t launch(int B, const HeadMArgs& a, hipStream_t stream) {
+  constexpr size_t lds = 2 * (size_t)HB + T * C * 2 + T * C * 4 + 384 * 4 + DZN * 4 + 32 * 4;
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)head_mfma_kernel<C>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+  hipLaunchKernelGGL(head_mfma_kernel<C>, dim3(B), dim3(HT), lds, stream, a);
+  return hipGetLastError();
+}
+
+// 3x3 head over a 128- or 256-channel pad-1 frame (the 12-layer configs); see dg_head.
+extern "C" hipError_t dg_head_mfma(int C, const void* X, int B, const float* w, const float* bias,
                                    const float* posb, const int* labels, float* loss, int* pred,
                                    float* logp_out, void* dZ, float* gw_part, float* dzb,
                                    int head_relu, float grad_scale, hipStream_t stream) {
   if (B <= 0) return hipErrorInvalidValue;
   HeadMArgs a{(const char*)X, w, bias, posb, labels, loss, pred, logp_out, (char*)dZ, gw_part,
               dzb, head_relu, grad_scale};
-  constexpr size_t lds = 2 * (size_t)HB + T * C * 2 + T * C * 4 + 384 * 4 + DZN * 4 + 32 * 4;
-  static_assert(lds <= 160 * 1024, "LDS");
-  static bool done = false;
-  if (!done) {
-    (void)hipFuncSetAttribute((const void*)head_mfma_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    done = true;
-  }
-  hipLaunchKernelGGL(head_mfma_kernel, dim3(B), dim3(HT), lds, stream, a);
-  return hipGetLastError();
+  return C == 256 ? launch<256>(B, a, stream) : launch<128>(B, a, stream);
 }

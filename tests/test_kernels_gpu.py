@@ -272,9 +272,10 @@ def test_conv_wgrad_win(B, cin, cout, splits, nw, swp):
 
 @pytest.mark.parametrize("B,C,k,relu,mfma", [(3, 64, 3, True, 1), (7, 128, 3, True, 1),
                                              (7, 128, 3, True, 0), (5, 128, 3, False, 1),
-                                             (2, 32, 1, False, 1), (4, 256, 3, True, 1)])
+                                             (2, 32, 1, False, 1), (4, 256, 3, True, 1),
+                                             (4, 256, 3, True, 0), (5, 256, 3, False, 1)])
 def test_head(B, C, k, relu, mfma):
-    """Fused head (3x3/128: MFMA kernel unless mfma=0; other shapes: VALU kernel) vs fp32
+    """Fused head (3x3/128 and /256: MFMA kernel unless mfma=0; other shapes: VALU kernel) vs fp32
     autograd."""
     torch.manual_seed(4)
     from deep_go_amd.ops import functional as Fn
