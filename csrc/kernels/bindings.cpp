@@ -50,6 +50,10 @@ int dg_conv_wgrad_wgs_per_cu_for(int KP);
 hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pad, int M,
                                int Mpad, int x_pad, int x_C, int B, int KP, int splits,
                                hipStream_t stream);
+int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
+hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
+                      int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
+                      hipStream_t stream);
 void dg_conv_wgrad_win_set_ablate(int mode);
 void dg_conv_wgrad_win_set_pd(int pd);
 void dg_conv_wgrad_win_set_nw(int nw);
@@ -335,6 +339,16 @@ PYBIND11_MODULE(_dghip, m) {
                               splits, S(stream)),
           "conv_wgrad_multi");
   }, "weight gradients of several same-shape layers in one three-slice launch");
+  m.def("conv_l1", [](int kw, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
+                      int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
+                      uintptr_t stream) {
+    check(dg_conv_l1(kw, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C, B, P<void>(Y), y_pad,
+                     P<float>(bias), P<float>(posb), S(stream)),
+          "conv_l1");
+  }, "board-resident first-layer forward (conv_l1.hip): bias + position bias + ReLU");
+  m.def("conv_l1_ok", [](int kw, int x_pad, int x_C, int Mpad, int KP) {
+    return dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP);
+  });
   m.def("conv_wgrad_win", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
                              int splits, uintptr_t stream) {
     check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),

@@ -1,0 +1,195 @@
+// Board-resident first layer: the k x k (5 x 5) convolution over the expanded input planes
+// (37 planes padded to 40 channels), bias + untied position bias + ReLU, one board x 128
+// output channels per workgroup.
+//
+// The pixel-tiled im2col kernel (conv_mfma.hip conv_nt_kernel) re-stages every pixel's
+// 5x5x40 patch per tile: 40 KB of LDS-DMA per 192 MFMAs (213 B/MFMA) for a K of only 1000,
+// ~25% of the MFMA rate.  Here the board's whole zero-bordered 23x23x40 input frame (42 KB)
+// is staged ONCE by a linear LDS-DMA copy, and every B fragment is read straight out of it:
+// the K axis is the 125 8-channel chunks (tap, c8) of the layer — a lane's 8 K values are
+// one chunk, so a 32-wide K step may mix taps freely (padded to 128 chunks: K = 1024, 2.4%
+// waste instead of the 60% of a 64-channel image).  The weights [128 co][64 k] stream
+// through a 3-deep LDS ring by inline-asm LDS-DMA two steps ahead (conv_stack's scheme).
+//
+// 8 waves: 2 (64 co) x 4 (96 px, 6 fragments of 16); v_mfma_f32_16x16x32_bf16.
+// Reference: layer 1 of getBasicModel (experiments.lua:137-147: SpatialZeroPadding(2),
+// SpatialConvolutionMM(37 -> d, 5x5), Add (per-position bias), ReLU).
+#include "dg_common.h"
+
+using namespace dg;
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int A_BYTES = BM * 128;  // [128 co][64 k] bf16
+constexpr int NRING = 3;
+constexpr int MF = 4, NF = 6;
+
+struct L1Args {
+  const bf16_t* A;     // [Mpad][KP] weights, k = tap * x_C + c (conv_nt layout)
+  const char* X;       // input frame [B][F][F][x_C] bf16, F = 19 + 2 * pad
+  char* Y;             // output frame [B][19 + 2 y_pad]^2[M] bf16
+  const float* bias;   // [M]
+  const float* posb;   // [361][M]
+  int KP, M, x_C, y_pad, B;
+  int ngroups;         // valid chunks = KW * KW * x_C / 8
+  int img_bytes;       // LDS image bytes (whole KB)
+};
+
+template <int KW>
+__global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
+  constexpr int R = (KW - 1) / 2;
+  constexpr int F = BOARD + 2 * R;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int b = blockIdx.x;
+  const int m_tile = blockIdx.y * BM;
+  char* img = smem;
+  char* ring = smem + a.img_bytes;
+  const uint32_t ring_u = (uint32_t)(uintptr_t)(LDS_AS char*)ring;
+  const int xcb = a.x_C * 2;
+  const int KS = a.KP / 64;
+
+  // weight tile of K-step s -> ring slot s % 3: 2 LDS-DMA instructions per wave
+  const int g_src = (lane & 7) ^ (lane >> 3);
+  const char* a_lane = (const char*)a.A +
+                       ((size_t)(m_tile + wave * 16 + (lane >> 3)) * a.KP + g_src * 8) * 2;
+  auto stage_A = [&](int s) {
+    const char* src = a_lane + s * 128;
+    const uint32_t dst = ring_u + (s % NRING) * A_BYTES + wave * 2048;
+    dma16(src, __builtin_amdgcn_readfirstlane(dst));
+    dma16(src + (size_t)8 * a.KP * 2, __builtin_amdgcn_readfirstlane(dst + 1024));
+  };
+
+  // ---- prologue: the board's input frame, a linear copy (whole 1-KB blocks; the tail
+  // of the last block re-reads the frame's last 16 B into the image padding) ----
+  {
+    const int fbytes = F * F * xcb;
+    const char* Xb = a.X + (size_t)b * fbytes;
+    for (int blk = wave; blk < a.img_bytes / 1024; blk += 8) {
+      int off = blk * 1024 + lane * 16;
+      const int src = off < fbytes ? off : fbytes - 16;
+      glds16(Xb + src, (LDS_AS void*)(img + blk * 1024));
+    }
+    stage_A(0);
+    if (KS > 1) stage_A(1);
+  }
+  dma_wait<0>();
+  __syncthreads();
+
+  const int lr = lane & 15, lq = lane >> 4;
+  int fpb[NF];  // byte offset of this lane's pixel (centre) in the image
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    fpb[j] = ((h + R) * F + (w + R)) * xcb;
+  }
+  const int gpt = a.x_C / 8;
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = 0; s < KS; ++s) {
+    if (s + 2 < KS) stage_A(s + 2);
+    const char* sA = ring + (s % NRING) * A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      // this lane's K chunk: (tap, c8) -> byte offset relative to the pixel centre
+      int kc = s * 8 + kk * 4 + lq;
+      if (kc >= a.ngroups) kc = 0;  // padding chunks: zero weights, any finite image value
+      const int t = kc / gpt, c8 = kc - t * gpt;
+      const int dy = t / KW - R, dx = t - (t / KW) * KW - R;
+      const int koff = (dy * F + dx) * xcb + c8 * 16;
+      const int g = kk * 4 + lq;
+      bf16x8 af[MF], bfr[NF];
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const int row = wm * 64 + i * 16 + lr;
+        af[i] = lds_read_b128((const LDS_AS char*)(sA + row * 128 + ((g ^ (row & 7)) * 16)));
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        bfr[j] = lds_read_b128((const LDS_AS char*)(img + fpb[j] + koff));
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    // tile s+1 landed for this wave (tile s+2 may stay in flight), then for all waves
+    if (s + 2 < KS) dma_wait<2>(); else dma_wait<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: + bias + position bias, ReLU, bf16 -> output frame ----
+  const int yF = BOARD + 2 * a.y_pad;
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int co = m_tile + wm * 64 + i * 16 + lq * 4;
+    if (co >= a.M) continue;
+    const f32x4 bv = *(const f32x4*)(a.bias + co);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = wn * NF * 16 + j * 16 + lr;
+      if (p >= NPTS) continue;
+      const f32x4 pv = *(const f32x4*)(a.posb + (size_t)p * a.M + co);
+      f32x4 v = acc[i][j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bv[r] + pv[r], 0.f);
+      const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+      const size_t yo = (((size_t)b * yF + h + a.y_pad) * yF + (w + a.y_pad)) * a.M + co;
+      uint2 o;
+      o.x = pack_bf16x2(v[0], v[1]);
+      o.y = pack_bf16x2(v[2], v[3]);
+      *(uint2*)(a.Y + yo * 2) = o;
+    }
+  }
+}
+
+template <int KW>
+hipError_t launch_l1(const L1Args& a, int Mpad, hipStream_t stream) {
+  const size_t lds = (size_t)a.img_bytes + NRING * A_BYTES;
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_l1_kernel<KW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+  hipLaunchKernelGGL(conv_l1_kernel<KW>, dim3(a.B, Mpad / BM), dim3(512), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Usable for: 3x3 / 5x5, pad (k-1)/2 input frame with x_C <= 64 channels (multiple of 8),
+// output channels padded to 128, K padded to 64 with zero weights.
+int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP) {
+  if (!(kw == 3 || kw == 5) || x_pad != (kw - 1) / 2 || x_C % 8 != 0 || x_C > 64 ||
+      Mpad % BM != 0 || KP % 64 != 0 || KP < kw * kw * x_C)
+    return 0;
+  const int F = BOARD + 2 * x_pad;
+  const int img = (F * F * x_C * 2 + 1023) / 1024 * 1024;
+  return img + NRING * A_BYTES <= 160 * 1024 ? 1 : 0;
+}
+
+hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
+                      int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
+                      hipStream_t stream) {
+  if (!dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP) || B <= 0 || M % 4 != 0 || M > Mpad)
+    return hipErrorInvalidValue;
+  const int F = BOARD + 2 * x_pad;
+  L1Args a{(const bf16_t*)A, (const char*)X, (char*)Y, bias, posb, KP, M, x_C, y_pad, B,
+           kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024};
+  return kw == 5 ? launch_l1<5>(a, Mpad, stream) : launch_l1<3>(a, Mpad, stream);
+}
+
+}  // extern "C"

@@ -310,6 +310,14 @@ class HipGoNet:
                     self.act[p.index].data_ptr(), y_pad,
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
                     msk.data_ptr() if msk is not None else 0)))
+            elif (self.relu_mask[p.index] is None and os.environ.get("DG_L1_RES", "1") != "0"
+                  and h.conv_l1_ok(p.k, x_pad, p.cinp, p.Mpad, p.KP)):
+                # first layer board-resident (conv_l1.hip): the 23x23x40 input frame staged
+                # once per board instead of a 5x5x40 im2col patch per pixel and tile
+                self._fwd.append((h.conv_l1, (p.k, self.wf[p.index].data_ptr(), p.KP, p.cout,
+                                              p.Mpad, xin.data_ptr(), x_pad, p.cinp, self.B,
+                                              self.act[p.index].data_ptr(), y_pad,
+                                              P + spec.b_off * f4, P + spec.pos_off * f4)))
             else:
                 msk = self.relu_mask[p.index]
                 self._fwd.append((h.conv_nt_ex, (h.EPI_FWD, p.k, p.bm, p.bn,

@@ -46,6 +46,26 @@ def conv_forward(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: st
     return LY.from_frame(yf, 1, cout)
 
 
+def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb) -> torch.Tensor:
+    """Board-resident first-layer forward (conv_l1.hip): relu(conv + bias + posb), fp32 NCHW."""
+    h = hip()
+    dev = w.device
+    B, cin = x.shape[:2]
+    cout, k, _, _ = w.shape
+    pad = (k - 1) // 2
+    cinp = LY.round_up(cin, 8)
+    KP, _, Mpad = LY.conv_dims(k, cinp, cout, 128)
+    assert h.conv_l1_ok(k, pad, cinp, Mpad, KP)
+    xf = LY.to_frame(x.to(dev), pad, cinp)
+    yf = LY.alloc_frame(B, cout, 1, dev)
+    A = LY.fwd_weight(w.float(), cinp, KP, Mpad)
+    bias = bias.float().contiguous().to(dev)
+    posb = posb.float().contiguous().to(dev)
+    h.conv_l1(k, A.data_ptr(), KP, cout, Mpad, xf.data_ptr(), pad, cinp, B, yf.data_ptr(), 1,
+              bias.data_ptr(), posb.data_ptr(), stream_handle())
+    return LY.from_frame(yf, 1, cout)
+
+
 def conv_nt_mask(x: torch.Tensor, w: torch.Tensor, bias, posb):
     """Pixel-tiled forward that also writes the ReLU bitmask [B][361][Cout/8] (bit k of
     byte q = channel 8q + k > 0).  Returns (NCHW output, mask)."""

@@ -243,6 +243,23 @@ def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
         hip().wgrad3_set_variant(1)
 
 
+@pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),
+                                         (4, 64, 128, 3), (5, 16, 128, 5)])
+def test_conv_l1(B, cin, cout, k):
+    """Board-resident first-layer forward (conv_l1.hip: whole input frame in LDS, K over
+    8-channel (tap, chunk) groups) vs the fp32 reference."""
+    torch.manual_seed(8)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, k, k, cin, device=DEV) * 0.1)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y = Fn.conv_l1(x, w, b, pb)
+    ref = torch.relu(conv_ref(x, w, k) + b[None, :, None, None]
+                     + pb.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref) < 1e-2
+
+
 @pytest.mark.parametrize("B,cin,cout,splits", [
     (3, 128, 128, None), (1, 128, 128, 1), (2, 128, 128, 26), (5, 256, 256, None),
     (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5), (3, 128, 64, None)])
