@@ -74,7 +74,7 @@ struct StackArgs {
   int nl, KP;
   StackLayer L[MAXL];
   unsigned long long* prof;  // ABL & 32: per-wave phase cycle sums [B][8 waves][8]
-  int stagger;               // 1: waves 4-7 copy out after their k-half-0 MFMAs
+  int stagger;               // unused (copy-out reads are now pipelined one step ahead)
 };
 
 // NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
@@ -161,20 +161,45 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
     fs[j] = (w + 1) + 3 * (h + 1);  // fsig(fp[j]) before the & 7
   }
 
-  // store one 16-B piece (8 channels of one pixel) of the image held in LDS
-  auto copy_out = [&](int u, const StackLayer& Lo) {
-    const int p = u >> 4, q = u & 15;
-    const int c = q >> 3, g = q & 7;
+  // Copy-out of the previous layer's output (resident in the image) to HBM, one 16-B piece
+  // (8 channels of one pixel) per thread and K-step: the piece of step s is READ from LDS
+  // during step s-1 and STORED in step s, so no wave blocks on that read's latency in front
+  // of its MFMAs (a read+store in one step cost a full LDS round trip per step: ~10% of
+  // the layer).  Thread tid always handles channel piece q = tid & 15 of pixels
+  // p = tid / 16 + 32 s (NT = 512).
+  const int co_q = tid & 15;
+  auto co_addr = [&](int s_, int& f) {
+    const int p = (tid >> 4) + 32 * s_;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    f = (h + 1) * F + (w + 1);
+    return sH + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig(f)) * 16);
+  };
+  auto co_read = [&](int s_) -> uint4 {
+    int f;
+    return *(const uint4*)co_addr(s_, f);
+  };
+  auto co_store = [&](int s_, const uint4& v, const StackLayer& Lo) {
+    const int p = (tid >> 4) + 32 * s_;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    const uint4 v = *(const uint4*)(sH + c * H_BYTES + f * 128 + ((g ^ fsig(f)) * 16));
-    *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C + c * 64 + g * 8) * 2) = v;
+    *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
     if (EPI == EPI_FWD && Lo.mask) {
-      auto nz = [](uint32_t x) { return ((x & 0xFFFFu) ? 1u : 0u) | ((x >> 16) ? 2u : 0u); };
-      Lo.mask[((size_t)b * NPTS + p) * 16 + q] =
-          (uint8_t)(nz(v.x) | (nz(v.y) << 2) | (nz(v.z) << 4) | (nz(v.w) << 6));
+      // bit per nonzero bf16 half (as the gates test it): packed min(x, 1) per half
+      typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+      auto nz2 = [](uint32_t x) {
+        const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
+        const uint32_t t = __builtin_bit_cast(uint32_t, m);
+        return (t | (t >> 15)) & 3u;
+      };
+      Lo.mask[((size_t)b * NPTS + p) * 16 + co_q] =
+          (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
     }
   };
+  auto copy_out = [&](int u, const StackLayer& Lo) {  // exposed (last layer): direct
+    const int s_ = (u - tid) / NT;
+    co_store(s_, co_read(s_), Lo);
+  };
+  constexpr int CO_STEPS = (UNITS + NT - 1) / NT;  // 12
 
 
   auto read_A = [&](const char* sA, int kk, bf16x8 (&af)[MF]) {
@@ -230,6 +255,9 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
       for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if constexpr (BPF) read_B(0, 0, bpre);  // image of this layer is ready (barrier)
+    const bool co_on = !(ABL & 8) && l > 0;
+    uint4 co_v = uint4{0, 0, 0, 0};
+    if (co_on && (tid >> 4) < NPTS) co_v = co_read(0);
     for (int s = 0; s < NSTEP; ++s, ++gs) {
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); tp0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
       // the previous layer's output (already in the image) goes to HBM under this layer's
@@ -238,11 +266,7 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
       // (it cannot prove they do not alias), which would expose the DMA's latency.
       // waves 0-3 copy out before their k-half-0 MFMAs, waves 4-7 (the other wave of each
       // SIMD) after them: one wave of every SIMD always has MFMAs to issue meanwhile
-      const bool co_early = !a.stagger || wave < 4;
-      if (!(ABL & 8) && l > 0 && co_early) {
-        const int u = s * NT + tid;
-        if (u < UNITS) copy_out(u, Lprev);
-      }
+      if (co_on && s < CO_STEPS && (tid >> 4) + 32 * s < NPTS) co_store(s, co_v, Lprev);
       // ring slot (gs+AHEAD)%NRING was last read in step gs-1: every wave passed the
       // barrier after it
       const bool more = gs + AHEAD < total;
@@ -266,10 +290,8 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
       // 16 waves (4 per SIMD, 128 VGPRs): keep k-half 1's reads below these MFMAs (the other
       // waves of the SIMD hide their latency) instead of two live fragment sets
       if constexpr (NW == 16) __builtin_amdgcn_sched_barrier(0);
-      if (!(ABL & 8) && l > 0 && !co_early) {
-        const int u = s * NT + tid;
-        if (u < UNITS) copy_out(u, Lprev);
-      }
+      // next step's copy-out piece, read under this step's k-half-1 MFMAs
+      if (co_on && s + 1 < CO_STEPS && (tid >> 4) + 32 * (s + 1) < NPTS) co_v = co_read(s + 1);
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
       // k-half 1, and the next step's k-half-0 B fragments (the image is resident: no DMA
       // dependency) issued before these MFMAs so their LDS latency hides under them
