@@ -202,10 +202,13 @@ class HipGoNet:
         # 128-channel layer, nothing next to 288 GB) — 1.43 vs 1.37 ms/step: they compete
         # with the wgrad's own L2->LDS traffic (wgrad 42 -> 49 us); "wgrad"
         # (DG_SIDE_STREAM=1) runs the whole weight-gradient chain beside the dgrads
-        side_mode = os.environ.get("DG_SIDE_STREAM", "0")
+        # "bias" runs only the HBM-bound bias-grad partials on the side stream, beside the
+        # MFMA-bound weight-gradient launch of the same layers (everything else as "none")
+        # (default "bias": 262k -> 264k boards/s at 12x128, neutral at 12x256)
+        side_mode = os.environ.get("DG_SIDE_STREAM", "bias")
         self.side_mode = {"1": "wgrad", "0": "none"}.get(side_mode, side_mode)
-        if self.side_mode not in ("none", "wgrad", "light"):
-            raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0, 1 or light")
+        if self.side_mode not in ("none", "wgrad", "light", "bias"):
+            raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0, 1, light or bias")
         self.bchunks = self.h.bias_chunks(batch)
         if self.side_mode == "light":
             self.slabs = [torch.empty(p.splits * p.Mpad_w * p.KPw, dtype=torch.float32,
@@ -473,7 +476,8 @@ class HipGoNet:
         after the head — so every dZ exists before the weight gradients and those can run
         as grouped launches (fewer split-K partials).  DG_DGRAD_FIRST=0 keeps the
         interleaved per-layer order."""
-        if os.environ.get("DG_DGRAD_FIRST", "1") == "0" or self.side_mode != "none":
+        if (os.environ.get("DG_DGRAD_FIRST", "1") == "0"
+                or self.side_mode not in ("none", "bias")):
             return
         moved = []
         for i in range(len(self.plans) - 1, 0, -1):
@@ -505,7 +509,7 @@ class HipGoNet:
         G = int(os.environ.get("DG_WGRAD_GROUP",
                                "5" if self.global_batch != self.B else "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
-        if G < 2 or self.side_mode != "none":
+        if G < 2 or self.side_mode not in ("none", "bias"):
             return
         lay = self.layout.layers
         h = self.h
@@ -656,6 +660,15 @@ class HipGoNet:
         main = torch.cuda.current_stream()
         if self.side_mode == "none":
             self._run(ops[:3], main.cuda_stream)
+            for fn in hooks:
+                fn()
+        elif self.side_mode == "bias":
+            side = self.side
+            side.wait_stream(main)               # dZ of the layer (group) final
+            self._run(ops[:1], side.cuda_stream)
+            self._run(ops[1:2], main.cuda_stream)
+            main.wait_stream(side)               # partials ready for the reduce
+            self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
                 fn()
         elif self.side_mode == "light":

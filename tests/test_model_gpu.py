@@ -92,7 +92,7 @@ def test_graph_replay_matches_eager():
     assert abs(net.lr.item() - lr_eager) < 1e-15
 
 
-@pytest.mark.parametrize("mode", ["1", "light"])
+@pytest.mark.parametrize("mode", ["1", "light", "bias"])
 @pytest.mark.parametrize("layers,ch,B", [(4, 128, 6), (6, 128, 3)])
 def test_side_stream_backward_matches_single_stream(layers, ch, B, mode, monkeypatch):
     """The weight-gradient chain on a side stream (HipGoNet.backward_layer) must give the
