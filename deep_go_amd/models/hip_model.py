@@ -441,6 +441,8 @@ class HipGoNet:
         self.dstack: List[int] = []
         self.wgroups: List[List[int]] = []
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
+        self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
+        self._l0_side_at = None    # group top whose backward also runs layer 0's chain
         if os.environ.get("DG_DSTACK", "1") == "0":
             self._dgrads_first()
             return
@@ -468,6 +470,17 @@ class HipGoNet:
                                                   self.plans[run[0]].KPd, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
             self._bwd[i] = self._bwd[i][:3]
+        # the remaining per-layer dgrads below the stack (layer 1 -> dZ_0) right after it, so
+        # every dZ exists before the weight gradients (the first layer's chain can then run
+        # beside the grouped launch)
+        if (os.environ.get("DG_DGRAD_FIRST", "1") != "0" and self.side_mode in ("none", "bias")
+                and all(len(self._bwd[i]) <= 3 or i == run[-1] - 1
+                        for i in range(1, run[-1]))):
+            for i in range(run[-1] - 1, 0, -1):
+                if len(self._bwd[i]) > 3:
+                    self._bwd_pre.extend(self._bwd[i][3:])
+                    self._bwd[i] = self._bwd[i][:3]
+            self._dgrad_first = True
         self._group_wgrads(set([run[0]] + [i - 1 for i in run]))
 
     def _dgrads_first(self):
@@ -487,6 +500,7 @@ class HipGoNet:
                 self._bwd[i] = ops[:3]
                 moved.append(i)
         if moved:
+            self._dgrad_first = True
             self._group_wgrads(set(range(len(self.plans))))
 
     @staticmethod
@@ -506,6 +520,7 @@ class HipGoNet:
         gpurun_out/ab.txt sweep of 4/5/7/10)."""
         self.wgroups: List[List[int]] = []
         self.win_groups = set()
+        self._l0_side_at = None
         G = int(os.environ.get("DG_WGRAD_GROUP",
                                "5" if self.global_batch != self.B else "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
@@ -534,6 +549,10 @@ class HipGoNet:
         if not groups:
             return
         self.wgroups = groups
+        # with dZ_0 produced up front (dgrad-first), the first layer's bias partial + wgrad +
+        # reduce run on the side stream beside the last group's weight-gradient launch
+        self._l0_side_at = (groups[-1][0] if self.side_mode == "bias" and self._dgrad_first
+                            and all(0 not in g for g in groups) else None)
         wgs = h.conv_wgrad_wgs_per_cu_for(self.plans[groups[0][0]].KPw)
         gslab_elems = 0
         plan_splits = {}
@@ -664,11 +683,17 @@ class HipGoNet:
                 fn()
         elif self.side_mode == "bias":
             side = self.side
-            side.wait_stream(main)               # dZ of the layer (group) final
-            self._run(ops[:1], side.cuda_stream)
-            self._run(ops[1:2], main.cuda_stream)
-            main.wait_stream(side)               # partials ready for the reduce
-            self._run(ops[2:3], main.cuda_stream)
+            l0_side = self._l0_side_at == i
+            if i == 0 and self._l0_side_at is not None:
+                pass                             # done on the side stream with a group
+            else:
+                side.wait_stream(main)           # dZ of the layer (group) final
+                self._run(ops[:1], side.cuda_stream)
+                if l0_side:                      # first layer's whole gradient chain too
+                    self._run(self._bwd[0][:3], side.cuda_stream)
+                self._run(ops[1:2], main.cuda_stream)
+                main.wait_stream(side)           # partials (and layer 0) ready
+                self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
                 fn()
         elif self.side_mode == "light":
