@@ -685,14 +685,15 @@ class HipGoNet:
             side = self.side
             l0_side = self._l0_side_at == i
             if i == 0 and self._l0_side_at is not None:
-                pass                             # done on the side stream with a group
+                main.wait_stream(side)           # layer 0's chain ran on the side stream
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
                 self._run(ops[:1], side.cuda_stream)
-                if l0_side:                      # first layer's whole gradient chain too
-                    self._run(self._bwd[0][:3], side.cuda_stream)
+                ev = side.record_event()         # partials ready for the reduce
+                if l0_side:                      # then the first layer's whole chain,
+                    self._run(self._bwd[0][:3], side.cuda_stream)  # joined at layer 0
                 self._run(ops[1:2], main.cuda_stream)
-                main.wait_stream(side)           # partials (and layer 0) ready
+                main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
                 fn()
