@@ -51,6 +51,7 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
                                int Mpad, int x_pad, int x_C, int B, int KP, int splits,
                                hipStream_t stream);
 int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
+void dg_conv_l1_set_nw(int nw);
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
                       hipStream_t stream);
@@ -346,6 +347,8 @@ PYBIND11_MODULE(_dghip, m) {
                      P<float>(bias), P<float>(posb), S(stream)),
           "conv_l1");
   }, "board-resident first-layer forward (conv_l1.hip): bias + position bias + ReLU");
+  m.def("conv_l1_set_nw", [](int nw) { dg_conv_l1_set_nw(nw); },
+        "conv_l1 workgroup: 4 waves / half a board, 2 per CU (default) or 8 waves / a board");
   m.def("conv_l1_ok", [](int kw, int x_pad, int x_C, int Mpad, int KP) {
     return dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP);
   });

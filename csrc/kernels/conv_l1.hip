@@ -14,6 +14,8 @@
 // 8 waves: 2 (64 co) x 4 (96 px, 6 fragments of 16); v_mfma_f32_16x16x32_bf16.
 // Reference: layer 1 of getBasicModel (experiments.lua:137-147: SpatialZeroPadding(2),
 // SpatialConvolutionMM(37 -> d, 5x5), Add (per-position bias), ReLU).
+#include <stdlib.h>
+
 #include "dg_common.h"
 
 using namespace dg;
@@ -22,7 +24,6 @@ namespace {
 
 constexpr int BM = 128;
 constexpr int A_BYTES = BM * 128;  // [128 co][64 k] bf16
-constexpr int NRING = 3;
 constexpr int MF = 4, NF = 6;
 
 struct L1Args {
@@ -36,16 +37,24 @@ struct L1Args {
   int img_bytes;       // LDS image bytes (whole KB)
 };
 
-template <int KW>
-__global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
+// NW = 8: one workgroup (board x 128 co) per CU, 3-deep weight ring.  NW = 4: a workgroup
+// computes half the board's pixels (the whole input frame is still staged), 2-deep ring,
+// 74 KB of LDS: two independent workgroups per CU, so one's frame load / epilogue overlaps
+// the other's MFMAs.
+template <int KW, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) conv_l1_kernel(L1Args a) {
   constexpr int R = (KW - 1) / 2;
   constexpr int F = BOARD + 2 * R;
+  constexpr int NRING = NW == 8 ? 3 : 2;
+  constexpr int DPW = 16 / NW;          // weight-tile DMA instructions per wave
+  constexpr int WN = NW / 2;            // pixel groups (96 px each) per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int b = blockIdx.x;
+  const int wm = wave / WN, wn = wave % WN;
+  const int b = blockIdx.x / (8 / NW);
+  const int px0 = (blockIdx.x % (8 / NW)) * WN * 96 + wn * 96;
   const int m_tile = blockIdx.y * BM;
   char* img = smem;
   char* ring = smem + a.img_bytes;
@@ -53,15 +62,16 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
   const int xcb = a.x_C * 2;
   const int KS = a.KP / 64;
 
-  // weight tile of K-step s -> ring slot s % 3: 2 LDS-DMA instructions per wave
+  // weight tile of K-step s -> ring slot s % NRING: DPW LDS-DMA instructions per wave
   const int g_src = (lane & 7) ^ (lane >> 3);
   const char* a_lane = (const char*)a.A +
-                       ((size_t)(m_tile + wave * 16 + (lane >> 3)) * a.KP + g_src * 8) * 2;
+                       ((size_t)(m_tile + wave * DPW * 8 + (lane >> 3)) * a.KP + g_src * 8) * 2;
   auto stage_A = [&](int s) {
     const char* src = a_lane + s * 128;
-    const uint32_t dst = ring_u + (s % NRING) * A_BYTES + wave * 2048;
-    dma16(src, __builtin_amdgcn_readfirstlane(dst));
-    dma16(src + (size_t)8 * a.KP * 2, __builtin_amdgcn_readfirstlane(dst + 1024));
+    const uint32_t dst = ring_u + (s % NRING) * A_BYTES + wave * DPW * 1024;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i)
+      dma16(src + (size_t)i * 8 * a.KP * 2, __builtin_amdgcn_readfirstlane(dst + i * 1024));
   };
 
   // ---- prologue: the board's input frame, a linear copy (whole 1-KB blocks; the tail
@@ -69,13 +79,13 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
   {
     const int fbytes = F * F * xcb;
     const char* Xb = a.X + (size_t)b * fbytes;
-    for (int blk = wave; blk < a.img_bytes / 1024; blk += 8) {
+    for (int blk = wave; blk < a.img_bytes / 1024; blk += NW) {
       int off = blk * 1024 + lane * 16;
       const int src = off < fbytes ? off : fbytes - 16;
       glds16(Xb + src, (LDS_AS void*)(img + blk * 1024));
     }
     stage_A(0);
-    if (KS > 1) stage_A(1);
+    if (NRING == 3 && KS > 1) stage_A(1);
   }
   dma_wait<0>();
   __syncthreads();
@@ -84,7 +94,7 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
   int fpb[NF];  // byte offset of this lane's pixel (centre) in the image
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
-    int p = wn * NF * 16 + j * 16 + lr;
+    int p = px0 + j * 16 + lr;
     if (p >= NPTS) p = 0;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     fpb[j] = ((h + R) * F + (w + R)) * xcb;
@@ -98,7 +108,7 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
     for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int s = 0; s < KS; ++s) {
-    if (s + 2 < KS) stage_A(s + 2);
+    if (s + NRING - 1 < KS) stage_A(s + NRING - 1);
     const char* sA = ring + (s % NRING) * A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -123,8 +133,9 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    // tile s+1 landed for this wave (tile s+2 may stay in flight), then for all waves
-    if (s + 2 < KS) dma_wait<2>(); else dma_wait<0>();
+    // tile s+1 landed for this wave (with a 3-deep ring tile s+2 may stay in flight), then
+    // for all waves
+    if (NRING == 3 && s + 2 < KS) dma_wait<DPW>(); else dma_wait<0>();
     __builtin_amdgcn_s_barrier();
   }
 
@@ -137,7 +148,7 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
     const f32x4 bv = *(const f32x4*)(a.bias + co);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-      const int p = wn * NF * 16 + j * 16 + lr;
+      const int p = px0 + j * 16 + lr;
       if (p >= NPTS) continue;
       const f32x4 pv = *(const f32x4*)(a.posb + (size_t)p * a.M + co);
       f32x4 v = acc[i][j];
@@ -153,18 +164,21 @@ __global__ void __launch_bounds__(512, 1) conv_l1_kernel(L1Args a) {
   }
 }
 
-template <int KW>
+template <int KW, int NW>
 hipError_t launch_l1(const L1Args& a, int Mpad, hipStream_t stream) {
-  const size_t lds = (size_t)a.img_bytes + NRING * A_BYTES;
+  const size_t lds = (size_t)a.img_bytes + (NW == 8 ? 3 : 2) * A_BYTES;
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_l1_kernel<KW>,
+    (void)hipFuncSetAttribute((const void*)conv_l1_kernel<KW, NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL(conv_l1_kernel<KW>, dim3(a.B, Mpad / BM), dim3(512), lds, stream, a);
+  hipLaunchKernelGGL((conv_l1_kernel<KW, NW>), dim3(a.B * (8 / NW), Mpad / BM), dim3(64 * NW),
+                     lds, stream, a);
   return hipGetLastError();
 }
+
+int g_l1_nw = 4;
 
 }  // namespace
 
@@ -178,7 +192,7 @@ int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP) {
     return 0;
   const int F = BOARD + 2 * x_pad;
   const int img = (F * F * x_C * 2 + 1023) / 1024 * 1024;
-  return img + NRING * A_BYTES <= 160 * 1024 ? 1 : 0;
+  return img + 3 * A_BYTES <= 160 * 1024 ? 1 : 0;
 }
 
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
@@ -189,7 +203,19 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
   const int F = BOARD + 2 * x_pad;
   L1Args a{(const bf16_t*)A, (const char*)X, (char*)Y, bias, posb, KP, M, x_C, y_pad, B,
            kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024};
-  return kw == 5 ? launch_l1<5>(a, Mpad, stream) : launch_l1<3>(a, Mpad, stream);
+  static bool env_done = false;
+  if (!env_done) {
+    const char* e = getenv("DG_L1_NW");
+    if (e) g_l1_nw = atoi(e) == 8 ? 8 : 4;
+    env_done = true;
+  }
+  // 4-wave half-board workgroups when two fit on a CU
+  const bool w4 = g_l1_nw == 4 && 2 * (a.img_bytes + 2 * A_BYTES) <= 160 * 1024;
+  if (kw == 5) return w4 ? launch_l1<5, 4>(a, Mpad, stream) : launch_l1<5, 8>(a, Mpad, stream);
+  return w4 ? launch_l1<3, 4>(a, Mpad, stream) : launch_l1<3, 8>(a, Mpad, stream);
+}
+
+void dg_conv_l1_set_nw(int nw) { g_l1_nw = nw == 8 ? 8 : 4;
 }
 
 }  // extern "C"

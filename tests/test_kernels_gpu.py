@@ -245,7 +245,8 @@ def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
 
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),
                                          (4, 64, 128, 3), (5, 16, 128, 5)])
-def test_conv_l1(B, cin, cout, k):
+@pytest.mark.parametrize("nw", [4, 8])
+def test_conv_l1(B, cin, cout, k, nw):
     """Board-resident first-layer forward (conv_l1.hip: whole input frame in LDS, K over
     8-channel (tap, chunk) groups) vs the fp32 reference."""
     torch.manual_seed(8)
@@ -254,7 +255,12 @@ def test_conv_l1(B, cin, cout, k):
     w = bf(torch.randn(cout, k, k, cin, device=DEV) * 0.1)
     b = torch.randn(cout, device=DEV) * 0.1
     pb = torch.randn(361, cout, device=DEV) * 0.1
-    y = Fn.conv_l1(x, w, b, pb)
+    from deep_go_amd.ops.native import hip
+    hip().conv_l1_set_nw(nw)
+    try:
+        y = Fn.conv_l1(x, w, b, pb)
+    finally:
+        hip().conv_l1_set_nw(4)
     ref = torch.relu(conv_ref(x, w, k) + b[None, :, None, None]
                      + pb.t().reshape(1, cout, 19, 19))
     assert rel_err(y, ref) < 1e-2

@@ -2,8 +2,8 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "conv_l1" -x -q --timeout 60 --timeout-method thread > gpurun_out/l1_tests.log 2>&1 &&
 timeout -k 10 200 python -u -m pytest tests/test_model_gpu.py -x -q --timeout 60 --timeout-method thread >> gpurun_out/l1_tests.log 2>&1 &&
-timeout -k 10 200 python bench.py --steps 50 --warmup 10 > gpurun_out/l1_b128.log 2>&1 &&
-DG_L1_RES=0 timeout -k 10 200 python bench.py --steps 50 --warmup 10 > gpurun_out/l1_b128_off.log 2>&1 &&
-timeout -k 10 200 python bench.py --steps 20 --warmup 5 --channels 256 > gpurun_out/l1_b256.log 2>&1 &&
-DG_L1_RES=0 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --channels 256 > gpurun_out/l1_b256_off.log 2>&1 &&
+for r in 1 2; do
+timeout -k 10 200 python bench.py --steps 50 --warmup 10 > gpurun_out/l1_b128_$r.log 2>&1 &&
+DG_L1_NW=8 timeout -k 10 200 python bench.py --steps 50 --warmup 10 > gpurun_out/l1_b128_nw8_$r.log 2>&1 || exit 1
+done &&
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/l1t -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 > $GRAFT_REPO_ROOT/gpurun_out/l1_t.log 2>&1
