@@ -443,6 +443,8 @@ class HipGoNet:
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
+        self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
+        self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
         if os.environ.get("DG_DSTACK", "1") == "0":
             self._dgrads_first()
             return
@@ -478,6 +480,7 @@ class HipGoNet:
                         for i in range(1, run[-1]))):
             for i in range(run[-1] - 1, 0, -1):
                 if len(self._bwd[i]) > 3:
+                    self._pre_dgrads[i] = self._bwd[i][3:]
                     self._bwd_pre.extend(self._bwd[i][3:])
                     self._bwd[i] = self._bwd[i][:3]
             self._dgrad_first = True
@@ -496,6 +499,7 @@ class HipGoNet:
         for i in range(len(self.plans) - 1, 0, -1):
             ops = self._bwd[i]
             if len(ops) > 3:
+                self._pre_dgrads[i] = ops[3:]
                 self._bwd_pre.extend(ops[3:])
                 self._bwd[i] = ops[:3]
                 moved.append(i)
@@ -553,6 +557,11 @@ class HipGoNet:
         # reduce run on the side stream beside the last group's weight-gradient launch
         self._l0_side_at = (groups[-1][0] if self.side_mode == "bias" and self._dgrad_first
                             and all(0 not in g for g in groups) else None)
+        if self._l0_side_at is not None and 1 in self._pre_dgrads:
+            # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
+            drop = set(id(op) for op in self._pre_dgrads[1])
+            self._bwd_pre = [op for op in self._bwd_pre if id(op) not in drop]
+            self._l0_dgrad = list(self._pre_dgrads[1])
         wgs = h.conv_wgrad_wgs_per_cu_for(self.plans[groups[0][0]].KPw)
         gslab_elems = 0
         plan_splits = {}
@@ -690,9 +699,10 @@ class HipGoNet:
                 side.wait_stream(main)           # dZ of the layer (group) final
                 self._run(ops[:1], side.cuda_stream)
                 ev = side.record_event()         # partials ready for the reduce
-                if l0_side:                      # then the first layer's whole chain,
-                    self._run(self._bwd[0][:3], side.cuda_stream)  # joined at layer 0
-                self._run(ops[1:2], main.cuda_stream)
+                if l0_side:                      # then dZ_0 and the first layer's whole
+                    self._run(self._l0_dgrad, side.cuda_stream)   # chain, joined at layer 0
+                    self._run(self._bwd[0][:3], side.cuda_stream)  # (measured: the other
+                self._run(ops[1:2], main.cuda_stream)              # order starves the 5x5 wgrad)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
