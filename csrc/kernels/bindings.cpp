@@ -54,7 +54,7 @@ int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
 void dg_conv_l1_set_nw(int nw);
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
-                      hipStream_t stream);
+                      void* mask, hipStream_t stream);
 void dg_conv_wgrad_win_set_ablate(int mode);
 void dg_conv_wgrad_win_set_pd(int pd);
 void dg_conv_wgrad_win_set_nw(int nw);
@@ -342,9 +342,9 @@ PYBIND11_MODULE(_dghip, m) {
   }, "weight gradients of several same-shape layers in one three-slice launch");
   m.def("conv_l1", [](int kw, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
                       int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
-                      uintptr_t stream) {
+                      uintptr_t mask, uintptr_t stream) {
     check(dg_conv_l1(kw, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C, B, P<void>(Y), y_pad,
-                     P<float>(bias), P<float>(posb), S(stream)),
+                     P<float>(bias), P<float>(posb), P<void>(mask), S(stream)),
           "conv_l1");
   }, "board-resident first-layer forward (conv_l1.hip): bias + position bias + ReLU");
   m.def("conv_l1_set_nw", [](int nw) { dg_conv_l1_set_nw(nw); },

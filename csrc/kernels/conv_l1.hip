@@ -35,6 +35,8 @@ struct L1Args {
   int KP, M, x_C, y_pad, B;
   int ngroups;         // valid chunks = KW * KW * x_C / 8
   int img_bytes;       // LDS image bytes (whole KB)
+  uint8_t* mask;       // optional ReLU bitmask [B][361][M/8] (bit k of byte q: channel 8q+k
+                       // nonzero) — lets the backward-data stack reach layer 1
 };
 
 // NW = 8: one workgroup (board x 128 co) per CU, 3-deep weight ring.  NW = 4: a workgroup
@@ -140,26 +142,39 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_l1_kernel(L1Args a) {
   }
 
   // ---- epilogue: + bias + position bias, ReLU, bf16 -> output frame ----
+  // (no divergent exits before the mask shuffle: every lane computes, stores are guarded)
   const int yF = BOARD + 2 * a.y_pad;
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
     const int co = m_tile + wm * 64 + i * 16 + lq * 4;
-    if (co >= a.M) continue;
-    const f32x4 bv = *(const f32x4*)(a.bias + co);
+    const bool co_ok = co < a.M;
+    const int coc = co_ok ? co : 0;
+    const f32x4 bv = *(const f32x4*)(a.bias + coc);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = px0 + j * 16 + lr;
-      if (p >= NPTS) continue;
-      const f32x4 pv = *(const f32x4*)(a.posb + (size_t)p * a.M + co);
+      const bool ok = co_ok && p < NPTS;
+      const int pc = p < NPTS ? p : 0;
+      const f32x4 pv = *(const f32x4*)(a.posb + (size_t)pc * a.M + coc);
       f32x4 v = acc[i][j];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bv[r] + pv[r], 0.f);
-      const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
-      const size_t yo = (((size_t)b * yF + h + a.y_pad) * yF + (w + a.y_pad)) * a.M + co;
       uint2 o;
       o.x = pack_bf16x2(v[0], v[1]);
       o.y = pack_bf16x2(v[2], v[3]);
-      *(uint2*)(a.Y + yo * 2) = o;
+      if (a.mask) {
+        // lanes l and l ^ 16 hold channels co..co+3 and co+4..co+7 of one pixel: one byte
+        const uint32_t nib = ((o.x & 0xFFFFu) ? 1u : 0u) | ((o.x >> 16) ? 2u : 0u) |
+                             ((o.y & 0xFFFFu) ? 4u : 0u) | ((o.y >> 16) ? 8u : 0u);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 16, 64);
+        if (ok && !(lq & 1))
+          a.mask[((size_t)b * NPTS + p) * (a.M >> 3) + (co >> 3)] = (uint8_t)(nib | (hi << 4));
+      }
+      if (ok) {
+        const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+        const size_t yo = (((size_t)b * yF + h + a.y_pad) * yF + (w + a.y_pad)) * a.M + co;
+        *(uint2*)(a.Y + yo * 2) = o;
+      }
     }
   }
 }
@@ -197,12 +212,13 @@ int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP) {
 
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
-                      hipStream_t stream) {
-  if (!dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP) || B <= 0 || M % 4 != 0 || M > Mpad)
+                      void* mask, hipStream_t stream) {
+  if (!dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP) || B <= 0 || M % 4 != 0 || M > Mpad ||
+      (mask && M % 8 != 0))
     return hipErrorInvalidValue;
   const int F = BOARD + 2 * x_pad;
   L1Args a{(const bf16_t*)A, (const char*)X, (char*)Y, bias, posb, KP, M, x_C, y_pad, B,
-           kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024};
+           kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024, (uint8_t*)mask};
   static bool env_done = false;
   if (!env_done) {
     const char* e = getenv("DG_L1_NW");

@@ -184,10 +184,12 @@ class HipGoNet:
         self.relu_mask = [None] * len(self.plans)
         for p in self.plans[:-1]:
             nxt = self.plans[p.index + 1]
-            # board forwards write the bitmask; the pixel-tiled first layer can too
-            # (conv_nt_ex), but its byte stores cost +13 us vs the ~5 us the dgrad stack then
-            # saves on layer 1 (measured): DG_L0_MASK=1 opts in
-            l0 = p.index == 0 and os.environ.get("DG_L0_MASK", "0") == "1"
+            # board forwards write the bitmask; so does the board-resident first layer
+            # (conv_l1), which lets the dgrad stack reach layer 1 (DG_L0_MASK=0: off).  The
+            # pixel-tiled first layer can too (conv_nt_ex), but its byte stores cost +13 us vs
+            # the ~5 us saved (measured): there DG_L0_MASK=1 opts in
+            l0 = p.index == 0 and (os.environ.get("DG_L0_MASK", "") == "1" or (
+                os.environ.get("DG_L0_MASK", "") != "0" and self._l1_res_ok(p)))
             if ((p.board or l0) and nxt.board_d
                     and os.environ.get("DG_RELU_MASK", "1") == "1"):
                 self.relu_mask[p.index] = torch.zeros((B, NUM_POINTS, p.cout // 8),
@@ -313,14 +315,15 @@ class HipGoNet:
                     self.act[p.index].data_ptr(), y_pad,
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
                     msk.data_ptr() if msk is not None else 0)))
-            elif (self.relu_mask[p.index] is None and os.environ.get("DG_L1_RES", "1") != "0"
-                  and h.conv_l1_ok(p.k, x_pad, p.cinp, p.Mpad, p.KP)):
+            elif self._l1_res_ok(p):
                 # first layer board-resident (conv_l1.hip): the 23x23x40 input frame staged
                 # once per board instead of a 5x5x40 im2col patch per pixel and tile
+                msk = self.relu_mask[p.index]
                 self._fwd.append((h.conv_l1, (p.k, self.wf[p.index].data_ptr(), p.KP, p.cout,
                                               p.Mpad, xin.data_ptr(), x_pad, p.cinp, self.B,
                                               self.act[p.index].data_ptr(), y_pad,
-                                              P + spec.b_off * f4, P + spec.pos_off * f4)))
+                                              P + spec.b_off * f4, P + spec.pos_off * f4,
+                                              msk.data_ptr() if msk is not None else 0)))
             else:
                 msk = self.relu_mask[p.index]
                 self._fwd.append((h.conv_nt_ex, (h.EPI_FWD, p.k, p.bm, p.bn,
@@ -506,6 +509,12 @@ class HipGoNet:
         if moved:
             self._dgrad_first = True
             self._group_wgrads(set(range(len(self.plans))))
+
+    def _l1_res_ok(self, p: ConvPlan) -> bool:
+        """First layer on the board-resident kernel (conv_l1.hip; DG_L1_RES=0: pixel-tiled)."""
+        return (p.index == 0 and not p.board and not p.fp8
+                and os.environ.get("DG_L1_RES", "1") != "0"
+                and bool(self.h.conv_l1_ok(p.k, self.layout.layers[0].pad, p.cinp, p.Mpad, p.KP)))
 
     @staticmethod
     def _noop(*_):

@@ -46,8 +46,9 @@ def conv_forward(x: torch.Tensor, w: torch.Tensor, bias=None, posb=None, epi: st
     return LY.from_frame(yf, 1, cout)
 
 
-def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb) -> torch.Tensor:
-    """Board-resident first-layer forward (conv_l1.hip): relu(conv + bias + posb), fp32 NCHW."""
+def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb, with_mask: bool = False):
+    """Board-resident first-layer forward (conv_l1.hip): relu(conv + bias + posb), fp32 NCHW
+    (and the ReLU bitmask [B][361][Cout/8] with with_mask)."""
     h = hip()
     dev = w.device
     B, cin = x.shape[:2]
@@ -61,8 +62,11 @@ def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb) -> torch.Tensor:
     A = LY.fwd_weight(w.float(), cinp, KP, Mpad)
     bias = bias.float().contiguous().to(dev)
     posb = posb.float().contiguous().to(dev)
+    mask = torch.zeros(B, NPTS, cout // 8, dtype=torch.uint8, device=dev) if with_mask else None
     h.conv_l1(k, A.data_ptr(), KP, cout, Mpad, xf.data_ptr(), pad, cinp, B, yf.data_ptr(), 1,
-              bias.data_ptr(), posb.data_ptr(), stream_handle())
+              bias.data_ptr(), posb.data_ptr(), _ptr(mask), stream_handle())
+    if with_mask:
+        return LY.from_frame(yf, 1, cout), mask
     return LY.from_frame(yf, 1, cout)
 
 

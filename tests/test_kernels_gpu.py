@@ -258,12 +258,16 @@ def test_conv_l1(B, cin, cout, k, nw):
     from deep_go_amd.ops.native import hip
     hip().conv_l1_set_nw(nw)
     try:
-        y = Fn.conv_l1(x, w, b, pb)
+        y, mask = Fn.conv_l1(x, w, b, pb, with_mask=cout % 8 == 0)
     finally:
         hip().conv_l1_set_nw(4)
     ref = torch.relu(conv_ref(x, w, k) + b[None, :, None, None]
                      + pb.t().reshape(1, cout, 19, 19))
     assert rel_err(y, ref) < 1e-2
+    # bitmask: bit k of byte q = channel 8q + k of the stored bf16 output is nonzero
+    bits = (mask.unsqueeze(-1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1
+    nz = (y.to(torch.bfloat16) != 0).permute(0, 2, 3, 1).reshape(B, 361, cout)
+    assert torch.equal(bits.reshape(B, 361, cout).bool(), nz)
 
 
 @pytest.mark.parametrize("B,cin,cout,splits", [
