@@ -185,11 +185,12 @@ _preset("cpu-1layer-k16", numLayers=1, first_kernel=5, channelSize=16, batchSize
         useCuda=False, synthetic=True)
 _preset("12x128-bf16", numLayers=12, channelSize=128, batchSize=256, useCuda=True,
         synthetic=True, dtype="bf16")
-_preset("12x256-dp8", numLayers=12, channelSize=256, batchSize=256, useCuda=True,
+# (batchSize is the global batch: 2048 over 8 ranks = 256 boards per GPU)
+_preset("12x256-dp8", numLayers=12, channelSize=256, batchSize=2048, useCuda=True,
         numGPUs=8, synthetic=True, dtype="bf16")
-_preset("full36-d256-dp8", numLayers=12, channelSize=256, batchSize=256, useCuda=True,
+_preset("full36-d256-dp8", numLayers=12, channelSize=256, batchSize=2048, useCuda=True,
         numGPUs=8, synthetic=False, dtype="bf16")
-_preset("fp8-d256-dp8", numLayers=12, channelSize=256, batchSize=256, useCuda=True,
+_preset("fp8-d256-dp8", numLayers=12, channelSize=256, batchSize=2048, useCuda=True,
         numGPUs=8, synthetic=True, dtype="fp8")
 
 
