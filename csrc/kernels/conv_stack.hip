@@ -260,6 +260,12 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
     if (co_on && (tid >> 4) < NPTS) co_v = co_read(0);
     for (int s = 0; s < NSTEP; ++s, ++gs) {
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); tp0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
+      // k-half 0's A fragments first (tile gs landed: barrier above): their LDS latency hides
+      // under the copy-out store and the weight-DMA issue below instead of stalling the
+      // first MFMA (the DMA is inline asm: the compiler inserts no vmcnt wait for it)
+      const char* sA = sA0 + (gs % NRING) * A_BYTES;
+      bf16x8 af[MF], bfr[NF];
+      read_A(sA, 0, af);
       // the previous layer's output (already in the image) goes to HBM under this layer's
       // MFMAs: 512 pieces per step over the first 12 steps.  Issued BEFORE the weight DMA:
       // hipcc puts an s_waitcnt vmcnt(0) in front of an LDS read that follows an LDS-DMA
@@ -276,10 +282,7 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
         else stage_A_at(A_next, s + AHEAD - NSTEP, (gs + AHEAD) % NRING);
       }
       if constexpr ((ABL & 32) != 0) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tp0; tp0 = t; __builtin_amdgcn_sched_barrier(0); }
-      const char* sA = sA0 + (gs % NRING) * A_BYTES;
-      bf16x8 af[MF], bfr[NF];
       // k-half 0: B fragments were prefetched during the previous step (BPF)
-      read_A(sA, 0, af);
       if constexpr (BPF) {
 #pragma unroll
         for (int j = 0; j < NF; ++j) bfr[j] = bpre[j];
