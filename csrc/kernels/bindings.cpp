@@ -27,6 +27,11 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          const float* bias, const float* posb, const void* aux, int aux_pad,
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
+hipError_t dg_conv_stack_fwd_head(const long long* table, int nl, const void* X0, int KP, int B,
+                                  const float* w, const float* bias, const float* posb,
+                                  const int* labels, float* loss, int* pred, void* dZ,
+                                  float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                  hipStream_t stream);
 hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
                              hipStream_t stream);
 void dg_conv_stack_set_ablate(int mode);
@@ -179,6 +184,17 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_conv_stack_fwd(P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
           "conv_stack_fwd");
   }, "fused forward of a run of 128->128 3x3 layers, board resident in LDS");
+  m.def("conv_stack_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                                  uintptr_t w, uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                  uintptr_t loss, uintptr_t pred, uintptr_t dZ, uintptr_t gw_part,
+                                  uintptr_t dzb, int head_relu, float grad_scale,
+                                  uintptr_t stream) {
+    check(dg_conv_stack_fwd_head(P<long long>(table), nl, P<void>(X0), KP, B, P<float>(w),
+                                 P<float>(bias), P<float>(posb), P<int>(labels), P<float>(loss),
+                                 P<int>(pred), P<void>(dZ), P<float>(gw_part), P<float>(dzb),
+                                 head_relu, grad_scale, S(stream)),
+          "conv_stack_fwd_head");
+  }, "forward stack + the 3x3/128 policy head (forward, loss, backward) on the resident image");
   m.def("conv_stack", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
                          uintptr_t stream) {
     check(dg_conv_stack(epi, P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),

@@ -33,6 +33,7 @@
 #include <stdlib.h>
 
 #include "dg_common.h"
+#include "head_body.h"
 
 using namespace dg;
 
@@ -75,6 +76,8 @@ struct StackArgs {
   StackLayer L[MAXL];
   unsigned long long* prof;  // ABL & 32: per-wave phase cycle sums [B][8 waves][8]
   int stagger;               // unused (copy-out reads are now pipelined one step ahead)
+  int fuse_head;             // EPI_FWD, 8 waves: run the policy head on the final image
+  dghead::HeadMArgs head;    // (head_body.h; X unused: the image is resident)
 };
 
 // NRING: weight-tile ring depth (tiles are issued NRING-1 steps ahead).
@@ -366,6 +369,12 @@ __global__ void __launch_bounds__(NW * 64) conv_stack_kernel(StackArgs a) {
   }
   // last layer's output: exposed copy-out
   for (int u = tid; u < UNITS; u += NT) copy_out(u, a.L[a.nl - 1]);
+  // the policy head on the board image that is already in LDS (no re-staging, no launch):
+  // its scratch (weights, logits, frame-shaped dz) goes into the idle weight ring
+  if constexpr (EPI == EPI_FWD && NW == 8 && ABL == 0) {
+    static_assert(dghead::scratch_bytes(C) <= NRING * (size_t)A_BYTES, "head scratch");
+    if (a.fuse_head) dghead::head_body<C>(a.head, b, sH, smem, [](int) {});
+  }
   if constexpr ((ABL & 32) != 0) {
     if (lane == 0 && a.prof) {
       ph[6] = (unsigned long long)a.nl * NSTEP;
@@ -429,11 +438,18 @@ void dg_conv_stack_set_waves(int n) { g_stack_waves = n; }
 // table: nl rows of {A, pbias, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)
 //   epi 2 (dgrad)  : mask required (read; ReLU bits of the layer below), pbias unused
-hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
-                         hipStream_t stream) {
+hipError_t dg_head_mfma(int C, const void* X, int B, const float* w, const float* bias,
+                        const float* posb, const int* labels, float* loss, int* pred,
+                        float* logp_out, void* dZ, float* gw_part, float* dzb, int head_relu,
+                        float grad_scale, hipStream_t stream);
+
+static hipError_t stack_launch(int epi, const long long* table, int nl, const void* X0, int KP,
+                               int B, const dghead::HeadMArgs* head, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || KP < T * C || KP % 64 != 0 || B <= 0) return hipErrorInvalidValue;
   if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
   StackArgs a;
+  a.fuse_head = 0;
+  a.head = dghead::HeadMArgs{};
   a.X0 = (const char*)X0;
   a.nl = nl;
   a.KP = KP;
@@ -453,6 +469,19 @@ hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0
     if (epi == EPI_DGRAD && !a.L[i].mask) return hipErrorInvalidValue;
   }
   const int nring = g_stack_ring ? g_stack_ring : 2;
+  if (head) {
+    if (epi != EPI_FWD) return hipErrorInvalidValue;
+    if (g_stack_ablate || g_stack_waves == 16) {
+      // variants without the fused head: the stack, then the standalone head kernel
+      const hipError_t e = stack_launch(epi, table, nl, X0, KP, B, nullptr, stream);
+      if (e != hipSuccess) return e;
+      const dghead::HeadMArgs& h = *head;
+      return dg_head_mfma(C, a.L[nl - 1].Y, B, h.w, h.bias, h.posb, h.labels, h.loss, h.pred,
+                          h.logp_out, h.dZ, h.gw_part, h.dzb, h.head_relu, h.grad_scale, stream);
+    }
+    a.fuse_head = 1;
+    a.head = *head;
+  }
   if (g_stack_ablate)
     return epi == EPI_FWD ? (nring == 3 ? dispatch_ablate<3>(g_stack_ablate, a, B, stream)
                                         : dispatch_ablate<2>(g_stack_ablate, a, B, stream))
@@ -470,9 +499,27 @@ hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0
                     : launch_stack<EPI_DGRAD, 2, 0>(a, B, stream);
 }
 
+hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
+                         hipStream_t stream) {
+  return stack_launch(epi, table, nl, X0, KP, B, nullptr, stream);
+}
+
 hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
                              hipStream_t stream) {
-  return dg_conv_stack(EPI_FWD, table, nl, X0, KP, B, stream);
+  return stack_launch(EPI_FWD, table, nl, X0, KP, B, nullptr, stream);
+}
+
+// Forward stack + the 3x3 / 128-channel policy head fused after its last layer (training:
+// labels, loss, pred, dZ of the last hidden layer, per-board weight partials, dz for the
+// bias reduce — the head_mfma arguments, minus the activation frame).
+hipError_t dg_conv_stack_fwd_head(const long long* table, int nl, const void* X0, int KP, int B,
+                                  const float* w, const float* bias, const float* posb,
+                                  const int* labels, float* loss, int* pred, void* dZ,
+                                  float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                  hipStream_t stream) {
+  const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
+                            gw_part, dzb, head_relu, grad_scale};
+  return stack_launch(EPI_FWD, table, nl, X0, KP, B, &h, stream);
 }
 
 }  // extern "C"

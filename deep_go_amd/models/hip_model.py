@@ -357,6 +357,25 @@ class HipGoNet:
                                     self.labels.data_ptr(), self.eval_loss.data_ptr(),
                                     self.eval_pred.data_ptr(), 0, 0, 0, 0, 0, 0,
                                     int(self.cfg.head_relu), 1.0 / self.global_batch))
+        # training: the head runs inside the forward stack's launch when the stack ends at the
+        # last hidden layer (its image is already in LDS; conv_stack.hip + head_body.h);
+        # evaluation keeps the standalone head.  DG_FUSE_HEAD=0 keeps the separate launch.
+        self._fwd_train = self._fwd
+        if (self.stack and self.stack[-1] == len(self.plans) - 1 and hd.k == 3
+                and hd.cin == 128 and hd.pad == 1 and self.dzp[-1] == 1
+                and os.environ.get("DG_FUSE_HEAD", "1") != "0"
+                and os.environ.get("DG_HEAD_MFMA", "1") != "0"):
+            first = self.stack[0]
+            fused = (h.conv_stack_fwd_head, (
+                self._stack_table.ctypes.data, len(self.stack), self.act[first - 1].data_ptr(),
+                self.plans[first].KP, self.B, P + hd.w_off * f4, P + hd.b_off * f4,
+                P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
+                self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
+                self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
+            self._fwd_train = [fused if f is h.conv_stack_fwd else (f, a)
+                               for f, a in self._fwd]
+            if any(f is h.conv_stack_fwd_head for f, _ in self._fwd_train):
+                self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
             i = p.index
@@ -672,7 +691,7 @@ class HipGoNet:
         # (no gradient zeroing: every gradient entry is written — not accumulated — by the
         # slab reduces and the deterministic head reduce)
         self._run(self._pre, s)
-        self._run(self._fwd, s)
+        self._run(self._fwd_train, s)
         f, a = self._head_train
         f(*a, s)
         f, a = self._head_red
@@ -868,7 +887,7 @@ class SegmentedStep:
             cur.append(fn)
 
         emit(lambda: net._run(net._pre, stream_handle()))
-        emit(lambda: net._run(net._fwd, stream_handle()))
+        emit(lambda: net._run(net._fwd_train, stream_handle()))
         emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
         emit(lambda: net._head_red[0](*net._head_red[1], stream_handle()))
         emit(lambda: net._run(net._bwd_pre, stream_handle()))

@@ -148,6 +148,28 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.parametrize("layers", [4, 7])
+def test_head_fused_into_forward_stack(layers, monkeypatch):
+    """The policy head run inside the forward stack's launch (on the resident board image)
+    gives the standalone MFMA head's loss, predictions, dZ and gradients bit for bit."""
+    monkeypatch.setenv("DG_FUSE_HEAD", "0")
+    _, n0, _ = _setup(layers, 128, 5, seed=12)
+    monkeypatch.setenv("DG_FUSE_HEAD", "1")
+    _, n1, _ = _setup(layers, 128, 5, seed=12)
+    assert n0._fwd_train is n0._fwd
+    assert any(f is n1.h.conv_stack_fwd_head for f, _ in n1._fwd_train)
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(n0.loss, n1.loss) and torch.equal(n0.pred, n1.pred)
+    assert torch.equal(n0.dz[-1], n1.dz[-1])
+    assert torch.equal(n0.grads, n1.grads)
+    # evaluation still runs the standalone head
+    n1.evaluate()
+    torch.cuda.synchronize()
+    assert torch.equal(n1.eval_loss, n1.loss)
+
+
 @pytest.mark.parametrize("l0_mask", ["0", "1"])
 @pytest.mark.parametrize("layers", [5, 7])
 def test_fused_dgrad_stack_matches_per_layer(layers, l0_mask, monkeypatch):
