@@ -68,9 +68,12 @@ def test_every_gradient_is_written_each_step():
     assert torch.allclose(net.grads, g0, rtol=1e-5, atol=1e-8)
 
 
-def test_graph_replay_matches_eager():
+@pytest.mark.parametrize("layers,ch,B", [(4, 64, 6), (6, 128, 4), (12, 128, 3)])
+def test_graph_replay_matches_eager(layers, ch, B):
+    """SegmentedStep.__call__ without buckets replays backward + optimizer as ONE graph
+    (full_graph); parameters and the decayed LR match the eager train_step."""
     from deep_go_amd.models.hip_model import SegmentedStep
-    cfg, net, data = _setup(4, 64, 6)
+    cfg, net, data = _setup(layers, ch, B)
     p0 = net.params.clone()
     net.train_step()
     torch.cuda.synchronize()
@@ -81,6 +84,7 @@ def test_graph_replay_matches_eager():
     net.lr.fill_(cfg.rate)
     net.refresh_weights()
     step = SegmentedStep(net, None, use_graphs=True)
+    assert step.full_graph is not None
     net.params.copy_(p0)
     net.lr.fill_(cfg.rate)
     net.refresh_weights()
