@@ -95,6 +95,11 @@ class CPUBackend:
             for w in works:
                 w.wait()
 
+    def train_step(self):
+        """forward_backward + optimizer_step with nothing in between."""
+        self.forward_backward()
+        self.optimizer_step()
+
     def optimizer_step(self):
         if self.cfg.nan_policy == "skip" and not np.isfinite(self._loss_sum):
             self.nan_skipped += 1
@@ -188,6 +193,12 @@ class HIPBackend:
 
     def forward_backward(self):
         self._step.forward_backward()
+        self._last = "train"
+
+    def train_step(self):
+        """forward_backward + optimizer_step with nothing in between: without DP buckets
+        SegmentedStep replays both as ONE hipGraph (no graph boundary before the update)."""
+        self._step()
         self._last = "train"
 
     def optimizer_step(self):

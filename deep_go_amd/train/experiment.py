@@ -168,9 +168,16 @@ class Experiment:
             with trace.range("load_batch"):
                 batch = be.load_next(loader)
             self.loader_seq = loader.consumed
-            with trace.range("fwd_bwd"):
-                be.forward_backward()
             step = self.iterations + 1
+            # nothing reads the pre-update state this iteration (no validation, no host NaN
+            # check before the update): forward/backward + update as one fused step
+            fused = (step % cfg.validation_interval != 0 and cfg.nan_policy != "raise"
+                     and not fault)
+            with trace.range("fwd_bwd"):
+                if fused:
+                    be.train_step()
+                else:
+                    be.forward_backward()
             inj = maybe_inject(info.rank, step, fault) if fault else None
             need_cost = (step % cfg.log_interval == 0) or (step % cfg.validation_interval == 0) \
                 or ema is None or cfg.nan_policy == "raise"
@@ -207,8 +214,9 @@ class Experiment:
                 self.metrics.record(kind="train", step=step, loss_ema=ema, boards_per_sec=bps,
                                     lr=be.rate)
                 t_log, n_log = now, 0
-            with trace.range("optimizer"):
-                be.optimizer_step()
+            if not fused:
+                with trace.range("optimizer"):
+                    be.optimizer_step()
             if save_now:
                 with trace.range("checkpoint"):
                     self.save()
