@@ -113,7 +113,8 @@ hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gs
                   const float* gate, hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
                       float decay, float gscale, const float* gate, hipStream_t s);
-hipError_t dg_finite_gate(const float* loss, int n, float* gate, int* bad_count, hipStream_t s);
+hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t ng, float* gate,
+                          int* bad_count, hipStream_t s);
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s);
@@ -309,9 +310,11 @@ PYBIND11_MODULE(_dghip, m) {
                      P<float>(gate), S(stream)),
           "rmsprop");
   });
-  m.def("finite_gate", [](uintptr_t loss, int n, uintptr_t gate, uintptr_t bad,
-                          uintptr_t stream) {
-    check(dg_finite_gate(P<float>(loss), n, P<float>(gate), P<int>(bad), S(stream)),
+  // loss (or 0) rank-local; grads (or 0) the flat (all-reduced) gradient: gate = all finite
+  m.def("finite_gate", [](uintptr_t loss, int n, uintptr_t grads, size_t ng, uintptr_t gate,
+                          uintptr_t bad, uintptr_t stream) {
+    check(dg_finite_gate(P<float>(loss), n, P<float>(grads), ng, P<float>(gate), P<int>(bad),
+                         S(stream)),
           "finite_gate");
   });
   m.def("lr_decay", [](uintptr_t lr, double decay, uintptr_t step, uintptr_t stream) {

@@ -145,8 +145,10 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n,
                            const double* __restrict__ lr, float gscale,
                            const float* __restrict__ gate) {
-  // gate (optional, device): 0 skips the update (non-finite loss policy, graph-friendly)
-  const float l = (float)(*lr) * gscale * (gate ? *gate : 1.f);
+  // gate (optional, device): 0 skips the update (non-finite loss/gradient policy, graph-
+  // friendly).  Return, do not scale by it: 0 * NaN gradient is still NaN.
+  if (gate && *gate == 0.f) return;
+  const float l = (float)(*lr) * gscale;
   const size_t n4 = n / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -165,8 +167,8 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, s
 __global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
                                float* __restrict__ ms, size_t n, const double* __restrict__ lr,
                                float decay, float gscale, const float* __restrict__ gate) {
-  const float l = (float)(*lr) * (gate ? *gate : 1.f);
   if (gate && *gate == 0.f) return;
+  const float l = (float)(*lr);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
@@ -174,6 +176,10 @@ __global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ 
     ms[i] = m;
     p[i] -= l * gi * rsqrtf(m);
   }
+}
+
+__global__ void set_gate_kernel(float* gate) {
+  if (threadIdx.x == 0) *gate = 1.f;
 }
 
 // gate = isfinite(sum(loss[0..n))) ? 1 : 0 — one workgroup; feeds the optimizer gate.
@@ -189,6 +195,28 @@ __global__ void finite_gate_kernel(const float* __restrict__ loss, int n, float*
   if (threadIdx.x == 0) {
     *gate = s_bad ? 0.f : 1.f;
     if (s_bad && bad_count) *bad_count += 1;
+  }
+}
+
+// gate &= all-finite(g[0..n)): run after finite_gate_kernel on the (all-reduced) flat gradient.
+// Under data parallelism every rank sees the same reduced gradient, so every rank takes the
+// same decision (a rank-local loss check would let one rank's NaN reach ranks that still
+// step).  The first lane that finds a bad value flips the gate and counts the step once.
+__global__ void grad_gate_kernel(const float* __restrict__ g, size_t n, float* __restrict__ gate,
+                                 int* __restrict__ bad_count) {
+  const size_t n4 = n / 4;
+  bool bad = false;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const f32x4 v = ((const f32x4*)g)[i];
+    bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(g[i]);
+  if (bad) {
+    const int old = atomicExch((int*)gate, 0);
+    if (old != 0 && bad_count) atomicAdd(bad_count, 1);
   }
 }
 
@@ -362,9 +390,21 @@ hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const doubl
   return hipGetLastError();
 }
 
-hipError_t dg_finite_gate(const float* loss, int n, float* gate, int* bad_count,
-                          hipStream_t s) {
-  hipLaunchKernelGGL(finite_gate_kernel, dim3(1), dim3(256), 0, s, loss, n, gate, bad_count);
+// loss (optional, rank-local) and grads (optional, flat, all-reduced) -> gate in {0, 1}
+hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t ng, float* gate,
+                          int* bad_count, hipStream_t s) {
+  if (loss) {
+    hipLaunchKernelGGL(finite_gate_kernel, dim3(1), dim3(256), 0, s, loss, n, gate, bad_count);
+  } else {
+    hipLaunchKernelGGL(set_gate_kernel, dim3(1), dim3(64), 0, s, gate);
+  }
+  if (grads && ng) {
+    int blocks = (int)((ng / 4 + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(grad_gate_kernel, dim3(blocks), dim3(256), 0, s, grads, ng, gate,
+                       bad_count);
+  }
   return hipGetLastError();
 }
 

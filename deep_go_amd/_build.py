@@ -22,6 +22,7 @@ OUT = PKG / "_native"
 BUILD = ROOT / "build"
 KDIR = ROOT / "csrc" / "kernels"
 EDIR = ROOT / "csrc" / "engine"
+CDIR = ROOT / "csrc" / "comm"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
@@ -105,22 +106,39 @@ def build_cpu(force: bool = False, jobs: int = 8, sanitize: str | None = None) -
     return target
 
 
+def build_comm(force: bool = False) -> Path:
+    """_dgcomm: native RCCL communicator (host code; links librccl.so.1 — at run time the copy
+    torch already mapped, same SONAME)."""
+    BUILD.mkdir(exist_ok=True)
+    OUT.mkdir(exist_ok=True)
+    target = OUT / f"_dgcomm{EXT}"
+    src = CDIR / "comm.cpp"
+    if force or _newer(src, target):
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", *(_pybind_includes()),
+              "-I/opt/rocm/include", str(src), "-o", str(target), "-L/opt/rocm/lib", "-lrccl",
+              "-lamdhip64"])
+    return target
+
+
 def build_all(force: bool = False) -> None:
     build_cpu(force)
     build_hip(force)
+    build_comm(force)
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--only", choices=["hip", "cpu"])
+    ap.add_argument("--only", choices=["hip", "cpu", "comm"])
     ap.add_argument("--sanitize", choices=["thread", "address", "address,undefined"])
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     a = ap.parse_args(argv)
-    if a.only != "hip":
+    if a.only in (None, "cpu"):
         print(build_cpu(a.force, a.j, a.sanitize))
-    if a.only != "cpu" and not a.sanitize:
+    if a.only in (None, "hip") and not a.sanitize:
         print(build_hip(a.force, a.j))
+    if a.only in (None, "comm") and not a.sanitize:
+        print(build_comm(a.force))
 
 
 if __name__ == "__main__":

@@ -181,7 +181,11 @@ _preset("default-experiment", numLayers=6, channelSize=64, batchSize=64, rate=0.
 # notebook cell 1 (Run Experiment.ipynb:10-33)
 _preset("notebook", numLayers=3, channelSize=64, batchSize=64, validationSize=200, useCuda=True)
 # BASELINE.json configs
-_preset("cpu-1layer-k16", numLayers=1, first_kernel=5, channelSize=16, batchSize=16,
+# "1-layer 19x19 conv k=16, batch=16 on CPU": ONE 5x5 conv layer of 16 filters (37 -> 16,
+# + bias + ReLU) under the 3x3 output head (16 -> 1, log-softmax) — numLayers counts the head
+# (experiments.lua:133-153), so a single conv of 16 filters is numLayers=2 (numLayers=1 would
+# be the bare 37 -> 1 head, where channelSize has no effect)
+_preset("cpu-1layer-k16", numLayers=2, first_kernel=5, channelSize=16, batchSize=16,
         useCuda=False, synthetic=True)
 _preset("12x128-bf16", numLayers=12, channelSize=128, batchSize=256, useCuda=True,
         synthetic=True, dtype="bf16")

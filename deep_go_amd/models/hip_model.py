@@ -583,8 +583,15 @@ class HipGoNet:
         self.wgroups = groups
         # with dZ_0 produced up front (dgrad-first), the first layer's bias partial + wgrad +
         # reduce run on the side stream beside the last group's weight-gradient launch
+        # Only when every layer from 1 up to the lowest group is itself grouped: an ungrouped
+        # layer j below the group would run its per-layer wgrad on the main stream into the
+        # shared slab / bias-partial buffers while layer 0's chain still uses them on the
+        # side stream (e.g. 8 layers under DP: groups [6..2] and [1] -> [1] is dropped).
+        grouped = set(i for g in groups for i in g)
         self._l0_side_at = (groups[-1][0] if self.side_mode == "bias" and self._dgrad_first
-                            and all(0 not in g for g in groups) else None)
+                            and 0 not in grouped
+                            and all(i in grouped for i in range(1, groups[-1][0] + 1))
+                            else None)
         if self._l0_side_at is not None and 1 in self._pre_dgrads:
             # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
             drop = set(id(op) for op in self._pre_dgrads[1])
@@ -772,7 +779,11 @@ class HipGoNet:
         n = self.layout.numel
         gate = 0
         if self.cfg.nan_policy == "skip":
-            self.h.finite_gate(self.loss.data_ptr(), self.B, self.gate.data_ptr(),
+            # gate = finite(gradients) [and finite(local loss) on one rank]: under DP every
+            # rank sees the same all-reduced gradient, so all ranks skip together
+            dp = self.global_batch != self.B
+            self.h.finite_gate(0 if dp else self.loss.data_ptr(), self.B,
+                               self.grads.data_ptr(), n, self.gate.data_ptr(),
                                self.bad_steps.data_ptr(), s)
             gate = self.gate.data_ptr()
         if self.ms is not None:
@@ -840,38 +851,22 @@ class HipGoNet:
         return sum(t.numel() * t.element_size() for t in ts)
 
 
-class GraphedStep:
-    """Capture HipGoNet.train_step (fwd+bwd+optimizer) into one hipGraph and replay it.
-
-    Inputs must be written into ``net.planes/player/rank/labels`` before ``replay()``."""
-
-    def __init__(self, net: HipGoNet, warmup: int = 2, with_optimizer: bool = True):
-        self.net = net
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                net.forward_backward()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            net.forward_backward()
-            if with_optimizer:
-                net.optimizer_step()
-        torch.cuda.synchronize()
-
-    def replay(self):
-        self.graph.replay()
-
-
 class SegmentedStep:
-    """Training step as hipGraph segments with gradient-bucket collectives between them.
+    """The training step (forward, backward, [gradient all-reduce], optimizer) as hipGraphs.
 
+    Modes (``self.mode``):
+      graph      no collectives: the whole step is ONE graph (a graph-to-graph boundary costs
+                 ~10 us of idle GPU per step);
+      dp-graph   native RCCL communicator (parallel/dp.py NativeComm): still ONE graph.  After
+                 the backward of the lowest layer of each gradient bucket, the comm stream is
+                 forked from the compute stream by an event and the bucket's ncclAllReduce is
+                 captured there, so it overlaps the remaining backward; the compute stream
+                 joins the comm stream before the optimizer.  No host work per bucket;
+      dp-segments torch.distributed communicator: graph segments between buckets, the
+                 all-reduces issued from the host between segment replays (the fallback);
+      eager      no graphs (debugging, ``--no-graph``).
     Segment boundaries sit right after the wgrad of the lowest layer of each DP bucket
-    (see ``parallel.dp.make_buckets``); the bucket's all-reduce is issued between two
-    segment replays so RCCL (own stream) overlaps the next segment's backward.  With no
-    bucketer the whole step is one graph (same as ``GraphedStep``)."""
+    (``parallel.dp.make_buckets``)."""
 
     def __init__(self, net: HipGoNet, bucketer=None, use_graphs: bool = True, warmup: int = 1):
         self.net = net
@@ -905,9 +900,17 @@ class SegmentedStep:
             segs.append((cur, []))
         self.segments = segs
         self.use_graphs = use_graphs
+        self.in_graph_comm = bucketer is not None and getattr(bucketer, "in_graph", False)
+        if not use_graphs:
+            self.mode = "eager"
+        elif bucketer is None:
+            self.mode = "graph" if os.environ.get("DG_ONE_GRAPH", "1") != "0" else "segments"
+        else:
+            self.mode = "dp-graph" if self.in_graph_comm else "dp-segments"
         self.graphs = []
         self.opt_graph = None
         self.full_graph = None
+        self.fb_graph = None
         if use_graphs:
             self._capture(warmup)
 
@@ -916,39 +919,65 @@ class SegmentedStep:
         for f in fns:
             f()
 
+    def _fb_in_stream(self):
+        """forward + backward with the in-graph (stream-ordered) collectives."""
+        for fns, fire in self.segments:
+            self._call_all(fns)
+            for b in fire:
+                self.bucketer.enqueue(b)
+        self.bucketer.join()
+
     def _capture(self, warmup: int):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                for fns, _ in self.segments:
-                    self._call_all(fns)
+                if self.in_graph_comm:
+                    self._fb_in_stream()       # also connects the communicator eagerly
+                else:
+                    for fns, _ in self.segments:
+                        self._call_all(fns)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        for fns, _ in self.segments:
+        if self.mode == "dp-graph":
+            # thread-local capture: RCCL's own threads may call HIP while we capture
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._call_all(fns)
-            self.graphs.append(g)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._fb_in_stream()
+            self.fb_graph = g
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._fb_in_stream()
+                self.net.optimizer_step()
+            self.full_graph = g
+        else:
+            for fns, _ in self.segments:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._call_all(fns)
+                self.graphs.append(g)
+            if self.mode == "graph":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for fns, _ in self.segments:
+                        self._call_all(fns)
+                    self.net.optimizer_step()
+                self.full_graph = g
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.net.optimizer_step()
         self.opt_graph = g
-        # no collectives between the segments: the whole step (backward + optimizer) is ONE
-        # graph for __call__ — a graph-to-graph boundary costs ~10 us of idle GPU per step
-        # (kernel trace: gap between the last backward kernel and sgd_kernel)
-        self.full_graph = None
-        if self.bucketer is None and os.environ.get("DG_ONE_GRAPH", "1") != "0":
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for fns, _ in self.segments:
-                    self._call_all(fns)
-                self.net.optimizer_step()
-            self.full_graph = g
         torch.cuda.synchronize()
 
     def forward_backward(self):
         """Gradients (all-reduced across ranks when DP) of the batch in the input buffers."""
+        if self.fb_graph is not None:
+            with trace.range("fwd_bwd_graph"):
+                self.fb_graph.replay()
+            return
+        if self.in_graph_comm:          # eager with the native communicator
+            self._fb_in_stream()
+            return
         for si, (fns, fire) in enumerate(self.segments):
             with trace.range(f"segment{si}"):
                 if self.use_graphs:
@@ -971,7 +1000,7 @@ class SegmentedStep:
                 self.net.optimizer_step()
 
     def __call__(self):
-        if self.use_graphs and self.full_graph is not None:
+        if self.full_graph is not None:
             with trace.range("step_graph"):
                 self.full_graph.replay()
             return

@@ -33,7 +33,8 @@ def _load(name: str):
     except ImportError as e:
         if os.environ.get("DG_AUTOBUILD", "0") == "1":
             from .. import _build
-            (_build.build_hip if name == "_dghip" else _build.build_cpu)()
+            {"_dghip": _build.build_hip, "_dgcomm": _build.build_comm}.get(
+                name, _build.build_cpu)()
             mod = importlib.import_module(name)
         else:
             raise NativeExtensionMissing(
@@ -49,6 +50,11 @@ def hip():
 
 def cpu():
     return _load("_dgcpu")
+
+
+def comm():
+    """_dgcomm: native RCCL communicator (csrc/comm/comm.cpp)."""
+    return _load("_dgcomm")
 
 
 def hip_available() -> bool:

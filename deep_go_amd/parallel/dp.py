@@ -108,13 +108,163 @@ def make_buckets(layer_ranges: Sequence[Tuple[int, int]], bucket_bytes: int,
     return buckets
 
 
+class TorchComm:
+    """Collectives through torch.distributed (ProcessGroupNCCL = RCCL on ROCm, or gloo).
+    Issued from the host between graph segments (they cannot sit inside our step graph)."""
+    kind = "torch"
+    in_graph = False
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+
+    def all_reduce_async(self, t: torch.Tensor):
+        return dist.all_reduce(t, group=self.group, async_op=True)
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0):
+        if self.world > 1:
+            dist.broadcast(t, root, group=self.group)
+        return t
+
+    def async_error(self) -> str:
+        return ""
+
+    def close(self):
+        pass
+
+
+class NativeComm:
+    """The native RCCL communicator (csrc/comm/comm.cpp, ``_dgcomm``) on its own HIP stream.
+
+    Its collectives are plain stream-ordered ncclAllReduce calls, so the training step can
+    capture them INSIDE its hipGraph: forked from the compute stream by an event once a
+    bucket's gradients are final, joined back before the optimizer (``SegmentedStep`` mode
+    "dp-graph").  Rendezvous: rank 0's unique id travels through torch.distributed's store;
+    world 1 (``bench.py --force-dp``) needs no process group."""
+    kind = "native"
+    in_graph = True
+    _seq = 0
+
+    def __init__(self, device):
+        from ..ops.native import comm as _comm_mod
+        mod = _comm_mod()
+        device = torch.device(device)
+        self.device = device
+        if dist.is_initialized():
+            self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        else:
+            self.world, self.rank = 1, 0
+        if self.world > 1:
+            store = dist.distributed_c10d._get_default_store()
+            key = f"dg_rccl_uid_{NativeComm._seq}"
+            if self.rank == 0:
+                store.set(key, mod.unique_id().hex())
+            uid = bytes.fromhex(store.get(key).decode())
+        else:
+            uid = mod.unique_id()
+        NativeComm._seq += 1
+        self.c = mod.Comm(uid, self.world, self.rank, device.index or 0)
+        self.stream = torch.cuda.Stream(device=device)
+
+    @staticmethod
+    def _dt(t: torch.Tensor) -> str:
+        return {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float64: "fp64",
+                torch.int32: "i32", torch.int64: "i64", torch.float16: "fp16"}[t.dtype]
+
+    def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
+        """In-place all-reduce of a contiguous tensor on ``stream`` (default: comm stream)."""
+        s = stream if stream is not None else self.stream
+        self.c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), op,
+                          int(s.cuda_stream))
+        return t
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0):
+        """Blocking (w.r.t. the current stream) broadcast, e.g. the initial parameters."""
+        if self.world > 1:
+            cur = torch.cuda.current_stream(self.device)
+            self.stream.wait_stream(cur)
+            self.c.broadcast(t.data_ptr(), t.numel(), self._dt(t), root,
+                             int(self.stream.cuda_stream))
+            cur.wait_stream(self.stream)
+        return t
+
+    def async_error(self) -> str:
+        return self.c.async_error()
+
+    def abort(self):
+        self.c.abort()
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        self.c.destroy()
+
+
+def make_communicator(kind: str, device):
+    """``native`` | ``torch`` | ``auto``.  ``auto`` takes the native in-graph communicator and
+    falls back to torch.distributed if the native module is missing or its self-test (a
+    graph-captured all-reduce whose result is checked) fails — the fallback is reported by
+    ``comm.kind`` (bench JSON "comm")."""
+    if kind == "torch":
+        return TorchComm()
+    try:
+        c = NativeComm(device)
+        if kind == "auto":
+            selftest_in_graph(c)
+        return c
+    except Exception as e:  # noqa: BLE001
+        if kind == "native":
+            raise
+        import sys
+        print(f"[dp] native communicator unavailable ({e}); using torch.distributed",
+              file=sys.stderr, flush=True)
+        return TorchComm()
+
+
+def selftest_in_graph(c: NativeComm, n: int = 4096):
+    """Capture ONE all-reduce on the comm stream into a hipGraph forked from / joined to the
+    capturing stream (the step graph's structure), replay it twice, check the sums."""
+    dev = c.device
+    x = torch.empty(n, dtype=torch.float32, device=dev)
+    x.fill_(float(c.rank + 1))
+    c.all_reduce_(x, stream=torch.cuda.current_stream(dev))   # eager: connects the comm
+    torch.cuda.synchronize(dev)
+    want = float(c.world * (c.world + 1) // 2)
+    if not bool((x == want).all()):
+        raise RuntimeError("native all-reduce self-test: wrong eager sum")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        cur = torch.cuda.current_stream(dev)
+        x.fill_(float(c.rank + 1))
+        c.stream.wait_stream(cur)
+        c.all_reduce_(x)
+        cur.wait_stream(c.stream)
+        x.mul_(2.0)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    if not bool((x == 2 * want).all()):
+        raise RuntimeError("native all-reduce self-test: wrong in-graph sum")
+    del g
+
+
 class GradBucketer:
-    """Issues async all-reduces of flat-gradient buckets; ``wait()`` joins them all."""
+    """All-reduces flat-gradient buckets.
+
+    torch communicator: ``fire(b)`` issues an async all-reduce from the host (between graph
+    segments); ``wait()`` joins them all.
+    native communicator: ``enqueue(b)`` forks the comm stream from the current (compute)
+    stream and queues the bucket's all-reduce there — graph-capturable; ``join()`` makes the
+    current stream wait for every queued bucket.
+
+    ``grad_dtype="bf16"``: the wire format is bf16 (half the bytes); the bucket is rounded
+    into a bf16 shadow on the comm stream and the sum written back to the fp32 gradients."""
 
     def __init__(self, grads: torch.Tensor, buckets: List[Tuple[int, int, int]],
-                 group=None, grad_dtype: str = "fp32"):
+                 group=None, grad_dtype: str = "fp32", comm=None):
         self.grads = grads
         self.buckets = buckets
+        self.comm = comm if comm is not None else TorchComm(group)
         self.group = group
         self.grad_dtype = grad_dtype
         self.works = []
@@ -122,23 +272,48 @@ class GradBucketer:
         if grad_dtype == "bf16":
             self._shadow = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device)
 
+    @property
+    def in_graph(self) -> bool:
+        return self.comm.in_graph
+
+    # -- torch.distributed path (host-issued between segments)
     def fire(self, b: int):
+        if self.in_graph:
+            return self.enqueue(b)
         s, e, _ = self.buckets[b]
         if self._shadow is not None:
             sh = self._shadow[s:e]
             sh.copy_(self.grads[s:e])
-            self.works.append((dist.all_reduce(sh, group=self.group, async_op=True), b))
+            self.works.append((self.comm.all_reduce_async(sh), b))
         else:
-            self.works.append((dist.all_reduce(self.grads[s:e], group=self.group,
-                                               async_op=True), b))
+            self.works.append((self.comm.all_reduce_async(self.grads[s:e]), b))
 
     def wait(self):
+        if self.in_graph:
+            return self.join()
         for w, b in self.works:
             w.wait()
             if self._shadow is not None:
                 s, e, _ = self.buckets[b]
                 self.grads[s:e].copy_(self._shadow[s:e])
         self.works = []
+
+    # -- native path (stream-ordered; capturable)
+    def enqueue(self, b: int):
+        s, e, _ = self.buckets[b]
+        cs = self.comm.stream
+        cs.wait_stream(torch.cuda.current_stream())     # bucket's gradients final
+        with torch.cuda.stream(cs):
+            if self._shadow is not None:
+                sh = self._shadow[s:e]
+                sh.copy_(self.grads[s:e])
+                self.comm.all_reduce_(sh)
+                self.grads[s:e].copy_(sh)
+            else:
+                self.comm.all_reduce_(self.grads[s:e])
+
+    def join(self):
+        torch.cuda.current_stream().wait_stream(self.comm.stream)
 
 
 def all_reduce_scalars(vals: Sequence[float], device=None, op=None) -> List[float]:

@@ -101,7 +101,11 @@ class CPUBackend:
         self.optimizer_step()
 
     def optimizer_step(self):
-        if self.cfg.nan_policy == "skip" and not np.isfinite(self._loss_sum):
+        # skip on non-finite (all-reduced) gradients: every rank sees the same reduced
+        # gradient, so all ranks skip together (a rank-local loss check would not)
+        if self.cfg.nan_policy == "skip" and not (
+                np.isfinite(self._loss_sum) if self.world == 1
+                else bool(torch.isfinite(self.params.grad).all())):
             self.nan_skipped += 1
             self.opt.rate = self.opt.rate * (1.0 - getattr(self.opt, "rate_decay", 0.0))
             return
@@ -142,7 +146,7 @@ class CPUBackend:
 class HIPBackend:
     def __init__(self, cfg: ExperimentConfig, batch: int, flat: Optional[torch.Tensor] = None,
                  world: int = 1, device=None, use_graphs: bool = True, bucket_mb: float = 4.0,
-                 grad_dtype: str = "fp32"):
+                 grad_dtype: str = "fp32", comm: str = "auto"):
         from ..models.hip_model import HipGoNet, SegmentedStep
         self.cfg = cfg
         self.B = batch
@@ -155,12 +159,17 @@ class HIPBackend:
             dp.broadcast_(self.net.params, 0)
             self.net.refresh_weights()
         self.bucketer = None
+        self.comm = None
         if world > 1:
+            # RCCL needs one GPU per rank: a gloo process group (e.g. several ranks sharing
+            # one GPU in tests) keeps torch.distributed collectives
+            kind = comm if torch.distributed.get_backend() == "nccl" else "torch"
+            self.comm = dp.make_communicator(kind, self.device)
             ranges = [self.layout.layer_range(i) for i in range(len(self.layout.layers))]
             self.bucketer = dp.GradBucketer(self.net.grads,
                                             dp.make_buckets(ranges, int(bucket_mb * 2 ** 20),
                                                             groups=self.net.wgroups),
-                                            grad_dtype=grad_dtype)
+                                            grad_dtype=grad_dtype, comm=self.comm)
         self._step = SegmentedStep(self.net, self.bucketer, use_graphs=use_graphs)
         self._eval_n = batch
         self._last = "train"

@@ -156,8 +156,12 @@ class Experiment:
         val = self.draw_validation(cfg.validationSize)
         loader = self._train_loader()
         fault = parse_fault()
-        watchdog = StepWatchdog(float(os.environ.get("DG_STEP_TIMEOUT", "0"))) \
-            if os.environ.get("DG_STEP_TIMEOUT") else None
+        # step timeout (DG_STEP_TIMEOUT seconds) and, with the native RCCL communicator,
+        # ncclCommGetAsyncError polling (always on under DP)
+        comm = getattr(be, "comm", None)
+        comm = comm if comm is not None and comm.kind == "native" else None
+        watchdog = (StepWatchdog(float(os.environ.get("DG_STEP_TIMEOUT", "0")), comm=comm)
+                    if os.environ.get("DG_STEP_TIMEOUT") or comm is not None else None)
         ema = self.train_costs[-1] if self.train_costs else None
         t_start = time.perf_counter()
         t_log = t_start
@@ -173,6 +177,10 @@ class Experiment:
             # check before the update): forward/backward + update as one fused step
             fused = (step % cfg.validation_interval != 0 and cfg.nan_policy != "raise"
                      and not fault)
+            # the rate this iteration's update uses, read before the step so fused and unfused
+            # iterations log the same thing (only on logging iterations: it syncs the device)
+            lr_now = (be.rate if step % cfg.log_interval == 0
+                      or step % cfg.validation_interval == 0 else None)
             with trace.range("fwd_bwd"):
                 if fused:
                     be.train_step()
@@ -200,7 +208,7 @@ class Experiment:
                 self.validation_accuracies.append(va)
                 self.metrics.line(f"validation at iteration {step}: cost={vc}, accuracy={va}")
                 self.metrics.record(kind="validation", step=step, val_cost=vc, val_acc=va,
-                                    lr=be.rate)
+                                    lr=lr_now)
                 # the reference saves here, BEFORE this iteration's update (train.lua:124):
                 # that checkpoint pairs iteration N with N-1 updates.  We save after the
                 # update below so a resumed run continues bit-exactly (auto-resume).
@@ -212,7 +220,7 @@ class Experiment:
                 if step % cfg.validation_interval != 0:
                     self.metrics.line(f"training {ema} (samples per second {bps:.1f})")
                 self.metrics.record(kind="train", step=step, loss_ema=ema, boards_per_sec=bps,
-                                    lr=be.rate)
+                                    lr=lr_now)
                 t_log, n_log = now, 0
             if not fused:
                 with trace.range("optimizer"):

@@ -9,7 +9,10 @@ Here:
   optimizer gate so the step is skipped but the LR still decays).
 * ``StepWatchdog`` — a thread that aborts the process (``os._exit``) when a training step
   does not finish within a timeout, so a hung collective cannot wedge a node forever;
-  torch.distributed's own collective timeout also applies.
+  torch.distributed's own collective timeout also applies.  Given the native RCCL
+  communicator (``parallel/dp.py`` NativeComm) it also polls ``ncclCommGetAsyncError``
+  every tick and, on an error (dead peer, transport failure), aborts the communicator —
+  which unblocks any collective stuck in the step graph — and exits with code 43.
 * ``DG_FAULT=rank:step:kind`` fault injection for tests: kinds ``nan`` (poison the loss),
   ``raise`` (exception), ``hang`` (sleep past the watchdog), ``exit`` (hard exit code 17).
 """
@@ -63,9 +66,14 @@ def check_finite(loss_sum: float, step: int, policy: str, batch=None, dump_dir: 
 
 
 class StepWatchdog:
-    def __init__(self, timeout_s: float, on_timeout=None):
+    def __init__(self, timeout_s: float, on_timeout=None, comm=None, on_comm_error=None,
+                 poll_s: float = 1.0):
         self.timeout = timeout_s
         self.on_timeout = on_timeout
+        self.comm = comm
+        self.on_comm_error = on_comm_error
+        self.poll = poll_s
+        self.comm_error = ""
         self._beat = time.monotonic()
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
@@ -75,8 +83,19 @@ class StepWatchdog:
         self._beat = time.monotonic()
 
     def _run(self):
-        while not self._stop.wait(min(1.0, self.timeout / 4)):
-            if time.monotonic() - self._beat > self.timeout:
+        tick = min(self.poll, self.timeout / 4) if self.timeout > 0 else self.poll
+        while not self._stop.wait(tick):
+            if self.comm is not None:
+                err = self.comm.async_error()
+                if err:
+                    self.comm_error = err
+                    if self.on_comm_error:
+                        self.on_comm_error(err)
+                        return
+                    print(f"[watchdog] communicator error: {err}: aborting", flush=True)
+                    self.comm.abort()
+                    os._exit(43)
+            if self.timeout > 0 and time.monotonic() - self._beat > self.timeout:
                 if self.on_timeout:
                     self.on_timeout()
                 else:

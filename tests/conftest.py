@@ -8,6 +8,10 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 REFERENCE_DATA = "/root/reference/data"
+# the reference's bundled fixture (/root/reference/data), decoded by our own t7 reader and
+# committed as packed .npz (tools/pack_fixture.py): present wherever the repo is, including
+# the GPU box, where the reference tree is not mounted
+PACKED_FIXTURE = os.path.join(ROOT, "tests", "fixtures")
 
 
 def pytest_configure(config):
@@ -40,3 +44,8 @@ def ref_data():
     if not os.path.isdir(REFERENCE_DATA):
         pytest.skip("reference fixture data not mounted")
     return REFERENCE_DATA
+
+
+@pytest.fixture(scope="session")
+def packed_fixture():
+    return PACKED_FIXTURE

@@ -1,0 +1,51 @@
+"""bench.py driver contract on the CPU: ``--gpus N`` spawns N ranks (torch.distributed.run as
+a child process), rank 0 prints ONE JSON line with n_gpus == N, the parent relays it and
+fails loudly when a rank fails (``--cpu-dry-run``: gloo + the fp32 oracle, no GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env=None, timeout=300):
+    e = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                          capture_output=True, text=True, timeout=timeout, env=e, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_launcher_spawns_n_ranks_one_json_line(n):
+    r = _bench("--cpu-dry-run", "--gpus", str(n), "--steps", "3", "--warmup", "1",
+               "--batch", "4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["steps"] == 3 and rec["warmup"] == 1
+    assert rec["config"]["global_batch"] == 4 * n
+    assert rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["rank_ms_per_step_max"] >= rec["rank_ms_per_step_min"] > 0
+    assert rec["value"] > 0 and rec["dry_run"] == "cpu-gloo"
+    for k in ("metric", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+              "dtype", "data"):
+        assert k in rec
+
+
+def test_launcher_fails_loudly_when_a_rank_fails():
+    # rank 1 exits non-zero (DG_BENCH_FAIL_RANK hook): no JSON line, non-zero exit
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "2", "--warmup", "1",
+               env={"DG_BENCH_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "1", "--warmup", "0",
+               env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1 != --gpus 2" in r.stderr

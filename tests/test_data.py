@@ -1,4 +1,6 @@
 """Dataset index, packed dataset and threaded loader."""
+import os
+
 import numpy as np
 import pytest
 
@@ -109,12 +111,12 @@ def test_pack_batch_roundtrip(B):
 
 
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
-def test_packed_slot_copy_matches_numpy(train_index, device):
+def test_packed_slot_copy_matches_numpy(packed_fixture, device):
     """next_packed_to (one copy of the pinned packed slot) carries the same batches as
     next_numpy, and many more batches than slots go through without a stall."""
     import torch
     from deep_go_amd.data.batch import packed_batch_bytes, unpack_views
-    pk = PackedDataset.from_index(train_index)
+    pk = PackedDataset.load(os.path.join(packed_fixture, "train.dgpack.npz"))
     B = 24
     la = BatchLoader(pk, B, threads=2, prefetch=3, seed=11, pin=(device == "cuda"))
     lb = BatchLoader(pk, B, threads=2, prefetch=3, seed=11, pin=False)
@@ -128,3 +130,14 @@ def test_packed_slot_copy_matches_numpy(train_index, device):
             assert np.array_equal(g.numpy(), w)
     la.close()
     lb.close()
+
+
+@pytest.mark.parametrize("split", ["train", "validation", "test"])
+def test_committed_packed_fixture_matches_reference(ref_data, packed_fixture, split):
+    """tests/fixtures/<split>.dgpack.npz is exactly what our t7 reader makes of the
+    reference's bundled data (so GPU-box tests on it test the real fixture)."""
+    a = PackedDataset.from_index(load_index(ref_data, split, build_missing=False))
+    b = PackedDataset.load(os.path.join(packed_fixture, f"{split}.dgpack.npz"))
+    assert len(a) == len(b) and a.num_games == b.num_games
+    for f in ("planes", "player", "rank", "label", "game_start", "game_count"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f

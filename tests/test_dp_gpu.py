@@ -123,3 +123,46 @@ def test_multirank_dp_step_matches_single_process(world, tmp_path):
     g = res["grads"].cuda()
     err = (g - ref.grads).norm() / ref.grads.norm()
     assert err < 1e-5, err.item()
+
+
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_native_comm_one_graph_dp_step(grad_dtype):
+    """Native RCCL communicator (csrc/comm/comm.cpp) at world 1: its all-reduces captured
+    INSIDE the one-graph DP step (mode dp-graph) give the plain step's gradients; the
+    optimizer runs after the join; async_error() reports a healthy communicator."""
+    from deep_go_amd.config import ExperimentConfig
+    from deep_go_amd.data.synthetic import random_planes
+    from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep
+    from deep_go_amd.parallel import dp
+    comm = dp.make_communicator("native", "cuda:0")
+    assert comm.kind == "native" and comm.world == 1
+    dp.selftest_in_graph(comm)
+    cfg = ExperimentConfig(numLayers=8, channelSize=128, batchSize=8, seed=2)
+    data = [torch.from_numpy(a).cuda() for a in random_planes(8, seed=3)]
+    ref = HipGoNet(cfg, 8, device="cuda")
+    ref.set_batch(*data)
+    ref.forward_backward()
+    ref_opt = HipGoNet(cfg, 8, device="cuda")
+    ref_opt.set_batch(*data)
+    ref_opt.train_step()
+    net = HipGoNet(cfg, 8, device="cuda")
+    net.set_batch(*data)
+    lay = net.layout
+    ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
+    bk = dp.GradBucketer(net.grads, dp.make_buckets(ranges, 256 * 1024, groups=net.wgroups),
+                         grad_dtype=grad_dtype, comm=comm)
+    step = SegmentedStep(net, bk, use_graphs=True)
+    assert step.mode == "dp-graph" and len(bk.buckets) >= 2
+    p0 = net.params.clone()
+    step.forward_backward()
+    torch.cuda.synchronize()
+    tol = dict(rtol=1e-5, atol=1e-8) if grad_dtype == "fp32" else dict(rtol=1e-2, atol=1e-5)
+    assert torch.allclose(net.grads, ref.grads, **tol)
+    net.params.copy_(p0)
+    net.lr.fill_(cfg.rate)
+    step()                               # full graph: fwd/bwd + collectives + optimizer
+    torch.cuda.synchronize()
+    ptol = dict(rtol=1e-6, atol=1e-7) if grad_dtype == "fp32" else dict(rtol=1e-4, atol=1e-6)
+    assert torch.allclose(net.params, ref_opt.params, **ptol)
+    assert comm.async_error() == ""
+    comm.close()

@@ -326,3 +326,52 @@ def test_head_relu_dead_logits_quirk():
     torch.cuda.synchronize()
     assert abs(net.mean_loss().item() - np.log(361)) < 1e-5
     assert net.grads.abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("layers,group", [(8, "5"), (9, "3")])
+def test_side_stream_with_ungrouped_layers_matches(layers, group, monkeypatch):
+    """8 layers with 5- or 3-layer weight-gradient groups leave hidden layer(s) ungrouped
+    below the lowest group; layer 0's side-stream chain must not then share the scratch
+    slab with their main-stream wgrads (data race).  Gradients must equal the
+    single-stream order."""
+    monkeypatch.setenv("DG_WGRAD_GROUP", group)
+    monkeypatch.setenv("DG_SIDE_STREAM", "0")
+    _, net0, _ = _setup(layers, 128, 4, seed=3)
+    net0.forward_backward()
+    torch.cuda.synchronize()
+    monkeypatch.setenv("DG_SIDE_STREAM", "bias")
+    _, net1, _ = _setup(layers, 128, 4, seed=3)
+    grouped = set(i for g in net1.wgroups for i in g)
+    assert any(i not in grouped for i in range(1, layers - 1))
+    for _ in range(3):
+        net1.forward_backward()
+        torch.cuda.synchronize()
+        assert torch.allclose(net1.grads, net0.grads, rtol=1e-5, atol=1e-7)
+
+
+def test_nan_skip_policy_leaves_parameters_unchanged():
+    """nan_policy='skip': a non-finite gradient or loss ON THE DEVICE skips the SGD update
+    (0 * NaN must not reach the weights), counts the step, and still decays the rate."""
+    cfg, net, _ = _setup(4, 128, 4, seed=1, nan_policy="skip")
+    net.forward_backward()
+    torch.cuda.synchronize()
+    p0 = net.params.clone()
+    wf0 = [w.clone() for w in net.wf]
+    lr0 = net.lr.item()
+    net.grads[17] = float("nan")            # poisoned gradient, finite loss
+    net.optimizer_step()
+    torch.cuda.synchronize()
+    assert torch.equal(net.params, p0)
+    assert all(torch.equal(a, b) for a, b in zip(net.wf, wf0))
+    assert net.bad_steps.item() == 1 and net.gate.item() == 0.0
+    assert net.lr.item() < lr0
+    net.forward_backward()
+    net.loss[0] = float("inf")              # poisoned loss, finite gradients
+    net.optimizer_step()
+    torch.cuda.synchronize()
+    assert torch.equal(net.params, p0) and net.bad_steps.item() == 2
+    net.forward_backward()                  # healthy step: updates again
+    net.optimizer_step()
+    torch.cuda.synchronize()
+    assert net.gate.item() == 1.0 and not torch.equal(net.params, p0)
+    assert torch.isfinite(net.params).all()

@@ -9,8 +9,9 @@ from deep_go_amd.config import ExperimentConfig
 
 pytestmark = pytest.mark.gpu
 
+# the reference's bundled data, packed by our t7 reader and committed (tests/fixtures)
 FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                       "data_cache", "fixture")
+                       "tests", "fixtures")
 
 
 def _cfg(tmp_path, **kw):
@@ -55,7 +56,6 @@ def test_gpu_step_matches_cpu_step(tmp_path):
     assert gpu_be.rate == pytest.approx(cpu_be.rate, rel=1e-12)
 
 
-@pytest.mark.skipif(not os.path.isdir(FIXTURE), reason="packed fixture not built")
 def test_real_data_training_reduces_loss(tmp_path):
     from deep_go_amd.train.experiment import Experiment
     cfg = _cfg(tmp_path, synthetic=False, data_root=FIXTURE, numLayers=6, channelSize=64,
