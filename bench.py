@@ -288,11 +288,23 @@ def run_gpu(args) -> int:
         phases = {k: round(1e3 * v / args.profile, 4) for k, v in trace.totals(True).items()}
         trace.enable(False)
     loss = net.mean_loss().item()  # sanity: finite
+    consistent = None
+    if world > 1:
+        # every rank must hold bit-identical parameters after the run (same init, same
+        # all-reduced gradients): a silent collective bug fails the bench here
+        sig = torch.stack([net.params.double().sum(), (net.params.double() ** 2).sum()])
+        sigs = [torch.zeros_like(sig) for _ in range(world)]
+        torch.distributed.all_gather(sigs, sig)
+        consistent = all(torch.equal(x, sigs[0]) for x in sigs)
+        if not consistent:
+            raise SystemExit(f"rank {info.rank}: parameters diverged across ranks: "
+                             f"{[x.tolist() for x in sigs]}")
     if info.rank == 0:
         extra = {"last_loss": round(loss, 4), "graphs": not args.no_graph,
                  "step_mode": step.mode, "spinup_steps": args.spinup_steps}
         if use_dp:
             extra["comm"] = comm.kind
+            extra["ranks_params_identical"] = consistent
             extra["grad_dtype"] = args.grad_dtype
         if phases:
             extra["profile_host_ms_per_step"] = phases

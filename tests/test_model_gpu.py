@@ -37,6 +37,131 @@ def _oracle(net, data):
     return loss.item(), logp.argmax(1), g
 
 
+class _RoundBF16(torch.autograd.Function):
+    """bf16 rounding of a stored tensor: the activation frame in the forward AND the dZ frame
+    flowing back through it (the kernels store both in bf16)."""
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _oracle_bf16(net, data):
+    """fp32 oracle that stores what the kernels store in bf16: hidden weights, activations
+    and dZ frames in bf16, and bias + position bias as ONE bf16 table where the layer's
+    epilogue reads that table (net.pbias).  What remains is accumulation order (fp32 MFMA
+    sums), so the error should not grow with depth."""
+    from deep_go_amd.config import NUM_POINTS
+    from deep_go_amd.data.features import expand_batch
+    planes, player, rank, labels = data
+    lay = net.layout
+    x = torch.from_numpy(expand_batch(planes, player, rank)).to(torch.bfloat16).float()
+    flat = net.params.detach().cpu().clone().requires_grad_(True)
+    n = len(lay.layers)
+    h = x
+    for L in lay.layers:
+        head = L.index == n - 1
+        w = lay.weight(flat, L.index).permute(0, 3, 1, 2)
+        if not head:
+            w = w + (w.detach().to(torch.bfloat16).float() - w.detach())
+        z = F.conv2d(h, w, padding=L.pad)
+        bias = lay.bias(flat, L.index).reshape(1, L.cout, 1, 1) + \
+            lay.pos_bias(flat, L.index).t().reshape(1, L.cout, 19, 19)
+        if not head and net.pbias[L.index] is not None:
+            bias = bias + (bias.detach().to(torch.bfloat16).float() - bias.detach())
+        z = z + bias
+        if not head or net.cfg.head_relu:
+            z = F.relu(z)
+        h = z if head else _RoundBF16.apply(z)
+    logp = F.log_softmax(h.reshape(h.shape[0], NUM_POINTS), dim=1)
+    loss = F.nll_loss(logp, torch.from_numpy(labels).long())
+    (g,) = torch.autograd.grad(loss, flat)
+    return loss.item(), logp.argmax(1), g
+
+
+@pytest.mark.parametrize("layers,ch,B", [(4, 128, 3), (12, 128, 2), (12, 256, 2)])
+def test_model_matches_bf16_storage_oracle(layers, ch, B):
+    """Flagship shapes (12x128, 12x256) end to end against the bf16-storage oracle.  The
+    oracle rounds where the kernels round but cannot round the SAME values (its fp32 sums
+    differ in order), so a few ReLU gates near zero flip and the difference compounds down the
+    backward: measured max per-tensor gradient error 3.6% (12x128) / 4.7% (12x256), 0.17% at
+    4 layers.  The per-layer, depth-independent bound is test_layerwise_teacher_forced."""
+    cfg, net, data = _setup(layers, ch, B, seed=4)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, pred_ref, g_ref = _oracle_bf16(net, data)
+    assert abs(net.mean_loss().item() - loss_ref) < 2e-3 * max(1.0, abs(loss_ref))
+    g = net.grads.cpu()
+    errs = {}
+    for name, off, n in net.layout.tensor_ranges():
+        a, b = g[off:off + n], g_ref[off:off + n]
+        errs[name] = ((a - b).norm() / (b.norm() + 1e-12)).item()
+    worst = max(errs, key=errs.get)
+    print("max per-tensor grad rel err", worst, errs[worst])
+    import json
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/oracle_errs_{layers}x{ch}.json", "w") as f:
+        json.dump(errs, f, indent=0)
+    assert errs[worst] < 6e-2, errs
+
+
+def _interior(frame, pad):
+    return frame[:, pad:pad + 19, pad:pad + 19, :].float().permute(0, 3, 1, 2).cpu()
+
+
+@pytest.mark.parametrize("layers,ch,B", [(12, 128, 4), (12, 256, 2), (6, 64, 4)])
+def test_layerwise_teacher_forced(layers, ch, B):
+    """Every layer's kernels against an fp32 oracle fed with the kernels' OWN stored inputs
+    (activation, dZ and mask frames), so nothing compounds: forward output, weight / bias /
+    position-bias gradients and the dgrad of each layer of the flagship shapes within a
+    depth-independent bound (bf16 output rounding: 2^-8 relative per element)."""
+    from deep_go_amd.data.features import expand_batch
+    cfg, net, data = _setup(layers, ch, B, seed=9)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    planes, player, rank, labels = data
+    lay = net.layout
+    flat = net.params.detach().cpu()
+    g = net.grads.cpu()
+    x0 = torch.from_numpy(expand_batch(planes, player, rank)).to(torch.bfloat16).float()
+    n = len(lay.layers)
+
+    def rel(a, b):
+        return ((a - b).norm() / (b.norm() + 1e-20)).item()
+    worst = {}
+    for L in lay.layers[:-1]:
+        i = L.index
+        xin = (x0 if i == 0 else _interior(net.act[i - 1], lay.layers[i].pad)).requires_grad_(True)
+        w = lay.weight(flat, i).permute(0, 3, 1, 2).to(torch.bfloat16).float().requires_grad_(True)
+        bias = lay.bias(flat, i).reshape(1, -1, 1, 1) + lay.pos_bias(flat, i).t().reshape(1, -1, 19, 19)
+        if net.pbias[i] is not None:
+            bias = bias.to(torch.bfloat16).float()
+        bias.requires_grad_(True)
+        z = F.conv2d(xin, w, padding=L.pad) + bias
+        y = F.relu(z)
+        y_gpu = _interior(net.act[i], lay.layers[i + 1].pad)
+        e_fwd = rel(y_gpu, y.detach())
+        dz = _interior(net.dz[i], net.dzp[i])
+        gx, gw, gb = torch.autograd.grad(z, (xin, w, bias), dz)
+        e_w = rel(g[L.w_off:L.w_off + L.w_numel].view(L.cout, L.k, L.k, L.cin).permute(0, 3, 1, 2), gw)
+        e_b = rel(g[L.b_off:L.b_off + L.cout], gb.sum((0, 2, 3)))
+        e_pb = rel(g[L.pos_off:L.pos_off + 361 * L.cout].view(361, L.cout).t().reshape(L.cout, 19, 19), gb.sum(0))
+        e_dx = 0.0
+        if i > 0:
+            mask = (_interior(net.act[i - 1], lay.layers[i].pad) > 0).float()
+            e_dx = rel(_interior(net.dz[i - 1], net.dzp[i - 1]), gx * mask)
+        worst[i] = (e_fwd, e_w, e_b, e_pb, e_dx)
+    print({i: tuple(round(v, 5) for v in e) for i, e in worst.items()})
+    for i, (e_fwd, e_w, e_b, e_pb, e_dx) in worst.items():
+        assert e_fwd < 4e-3, (i, "fwd", e_fwd)
+        assert max(e_w, e_b, e_pb) < 2e-3, (i, "wgrad", e_w, e_b, e_pb)
+        assert e_dx < 4e-3, (i, "dgrad", e_dx)
+
+
 @pytest.mark.parametrize("layers,ch,B", [(3, 64, 5), (4, 128, 3), (6, 64, 8)])
 def test_model_matches_oracle(layers, ch, B):
     cfg, net, data = _setup(layers, ch, B)

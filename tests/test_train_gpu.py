@@ -70,3 +70,48 @@ def test_real_data_training_reduces_loss(tmp_path):
     assert e.validation_costs[-1] < 5.0, e.validation_costs
     cost, acc = e.evaluate_split("test", 125)
     assert np.isfinite(cost) and acc > 0.0
+
+
+def test_200_step_training_curve_matches_fp32_oracle(tmp_path):
+    """200 SGD steps on the real fixture from the same init and the same batch stream: the
+    HIP trainer (bf16 operands, fp32 master weights, one-graph step) against the fp32
+    PyTorch oracle (CPUBackend), rate 0.05.  Stated tolerances: per-step loss within 0.01
+    nats at every step (measured max 4.7e-4), the mean loss of each 50-step window within
+    0.1% of the oracle's, and the parameter update (p_200 - p_0) within 10% relative norm.
+    (At rate 0.1 this tiny fixture's SGD is chaotic — a 1e-5 difference at step 1 grew to
+    0.77 nats by step 200 — so the rate is kept in the stable regime.)  The reference's
+    semantics: train.lua:4-12, optimizer.lua:16-27."""
+    from deep_go_amd.data.dataset import PackedDataset
+    from deep_go_amd.data.loader import BatchLoader
+    from deep_go_amd.train.backends import CPUBackend, HIPBackend
+    torch.set_num_threads(min(16, os.cpu_count() or 4))
+    cfg = _cfg(tmp_path, numLayers=6, channelSize=64, batchSize=32, rate=0.05, rateDecay=1e-4,
+               head_relu=False, synthetic=False, data_root=FIXTURE)
+    pk = PackedDataset.load(os.path.join(FIXTURE, "train.dgpack.npz"))
+    ld = BatchLoader(pk, 32, threads=2, prefetch=3, seed=5, pin=False)
+    cpu_be = CPUBackend(cfg, 32)
+    p0 = cpu_be.flat_params().clone()
+    gpu_be = HIPBackend(cfg, 32, flat=p0.clone())
+    lc, lg = [], []
+    for _ in range(200):
+        batch = ld.next_numpy()
+        for be, out in ((cpu_be, lc), (gpu_be, lg)):
+            be.set_batch(*batch)
+            be.train_step()
+            out.append(be.loss_sum() / 32)
+    ld.close()
+    lc, lg = np.array(lc), np.array(lg)
+    import json
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/curve_200.json", "w") as f:
+        json.dump({"cpu_fp32": lc.tolist(), "hip_bf16": lg.tolist()}, f)
+    assert np.isfinite(lg).all()
+    assert np.abs(lc - lg).max() < 0.01, np.abs(lc - lg).max()
+    for w in range(4):
+        a, b = lc[50 * w:50 * (w + 1)].mean(), lg[50 * w:50 * (w + 1)].mean()
+        assert abs(a - b) < 1e-3 * a, (w, a, b)
+    assert lc[-50:].mean() < lc[:50].mean() - 0.02     # it is learning
+    da = cpu_be.flat_params() - p0
+    db = gpu_be.flat_params() - p0
+    assert ((da - db).norm() / da.norm()).item() < 0.10
+    assert gpu_be.rate == pytest.approx(cpu_be.rate, rel=1e-9)

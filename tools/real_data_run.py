@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--ch", type=int, default=64)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--head-relu", type=int, default=0)
-    ap.add_argument("--data", default="data_cache/fixture")
+    ap.add_argument("--data", default="tests/fixtures")
     a = ap.parse_args()
     from deep_go_amd.config import ExperimentConfig
     from deep_go_amd.train.experiment import Experiment
