@@ -32,6 +32,14 @@ hipError_t dg_conv_stack_fwd_head(const long long* table, int nl, const void* X0
                                   const int* labels, float* loss, int* pred, void* dZ,
                                   float* gw_part, float* dzb, int head_relu, float grad_scale,
                                   hipStream_t stream);
+void dg_conv_stack2_set_bdb(int on);
+hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
+                          hipStream_t stream);
+hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
+                                   const float* w, const float* bias, const float* posb,
+                                   const int* labels, float* loss, int* pred, void* dZ,
+                                   float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                   hipStream_t stream);
 hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
                              hipStream_t stream);
 void dg_conv_stack_set_ablate(int mode);
@@ -202,6 +210,34 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_stack");
   }, "fused run of 128->128 3x3 layers, board resident in LDS: EPI_FWD forward (+bias, ReLU,"
      " writes masks) or EPI_DGRAD backward-data chain (ReLU masks of the layers below)");
+  // conv_stack2.hip: weights streamed into VGPRs (fragment-ordered), no per-K-step barrier.
+  // Same signatures as conv_stack* (KP unused: the fragment layout is fixed for C = 128).
+  m.def("conv_stack2_fwd", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                              uintptr_t stream) {
+    (void)KP;
+    check(dg_conv_stack2(1, P<long long>(table), nl, P<void>(X0), B, S(stream)),
+          "conv_stack2_fwd");
+  }, "conv_stack2 forward: table rows {A_frag, pbias_frag, Y, mask}");
+  m.def("conv_stack2_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                                   uintptr_t w, uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                   uintptr_t loss, uintptr_t pred, uintptr_t dZ, uintptr_t gw_part,
+                                   uintptr_t dzb, int head_relu, float grad_scale,
+                                   uintptr_t stream) {
+    (void)KP;
+    check(dg_conv_stack2_fwd_head(P<long long>(table), nl, P<void>(X0), B, P<float>(w),
+                                  P<float>(bias), P<float>(posb), P<int>(labels), P<float>(loss),
+                                  P<int>(pred), P<void>(dZ), P<float>(gw_part), P<float>(dzb),
+                                  head_relu, grad_scale, S(stream)),
+          "conv_stack2_fwd_head");
+  }, "conv_stack2 forward + the fused 3x3/128 policy head");
+  m.def("conv_stack2_set_bdb", [](int on) { dg_conv_stack2_set_bdb(on); },
+        "conv_stack2 B-fragment double buffering across k-halves (default 1)");
+  m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+                          uintptr_t stream) {
+    (void)KP;
+    check(dg_conv_stack2(epi, P<long long>(table), nl, P<void>(X0), B, S(stream)),
+          "conv_stack2");
+  }, "conv_stack2: EPI_FWD forward or EPI_DGRAD backward-data chain (fragment-ordered A)");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
                          int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {

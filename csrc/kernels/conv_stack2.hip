@@ -1,0 +1,378 @@
+// Fused run of hidden 3x3 layers (C -> C, C = 128, pad 1), board-resident in LDS, with the
+// weights streamed straight into VGPRs: no LDS weight ring, no barrier inside a layer.
+//
+// One workgroup (8 waves) owns one board for ALL layers of the run (forward stack, or the
+// backward-data chain in EPI_DGRAD mode):
+//   * the board's zero-bordered 21x21x128 frame lives in LDS (two 64-channel images of 448
+//     XOR-swizzled 128-B rows, 112 KB; the head_body.h layout);
+//   * wave (wm, wn) computes output channels wm*64 .. +64 x pixels wn*96 .. +96 as 4 x 6
+//     v_mfma_f32_16x16x32_bf16 fragments; a layer is 18 K-steps (2 chunks of 64 input
+//     channels x 9 taps) of 2 MFMA k-halves;
+//   * the A operand (weights) of a K-step comes from global memory (L2 / L1: every board
+//     reads the same 288 KB per layer) in FRAGMENT ORDER (weight_refresh writes it:
+//     [step 18][wm 2][kk 2][i 4][lane 64][8 bf16]), so one global_load_dwordx4 per
+//     fragment moves one contiguous KB per wave, straight into the registers the MFMA
+//     reads.  Each k-half's fragments for the next K-step are loaded as soon as that
+//     k-half's MFMAs have issued (half a step ahead, across layer boundaries); the
+//     compiler's own vmcnt waits cover them.
+//
+// Why: the previous design (conv_stack.hip) staged each [128 co][64 k] weight tile through
+// an LDS ring by LDS-DMA, which needs one workgroup barrier per K-step (the tile is written
+// by all waves and read by all).  With two waves per SIMD both hit that barrier together,
+// and the phase timer put the idle barrier + DMA-issue + wait at ~900 of ~2700 cycles per
+// K-step (profiles/r1_kbench_stack_final.json).  Here the image is the only shared LDS
+// state, and it is read-only for the whole layer, so waves only meet at the layer's
+// epilogue (2 barriers per layer instead of 18).  10 layers x 256 boards on one MI355X:
+// forward 250 -> 233 us, dgrad 242 -> 224 us, bit-identical outputs
+// (profiles/r2_kbench_stack2.json).
+//
+// The epilogue writes the layer's bf16 output straight back INTO the LDS image (the next
+// layer's input):
+//   EPI_FWD   : + (bias + pos-bias) table, ReLU          (forward; writes ReLU bitmask)
+//   EPI_DGRAD : * ReLU bitmask of the layer below       (dZ_{i-1} = mask * W_i^T dZ_i)
+// and the global store of that output (activation / gradient frame for the wgrads, plus
+// the forward's bitmask) is spread over the next layer's first 12 K-steps, under its MFMAs.
+//
+// LDS: 12 KB head scratch + 112 KB image = 124 KB: one 8-wave workgroup per CU.
+//
+// Reference ops: nn.SpatialZeroPadding + SpatialConvolutionMM + Add + ReLU per layer
+// (experiments.lua:137-147) and their backward through the stack (train.lua:10).
+#include <stdlib.h>
+
+#include "dg_common.h"
+#include "head_body.h"
+
+using namespace dg;
+
+namespace {
+
+constexpr int EPI_FWD = 1;
+constexpr int EPI_DGRAD = 2;
+constexpr int C = 128;
+constexpr int F = 21;                     // 19 + 2 * pad(1)
+constexpr int FF = F * F;                 // 441
+constexpr int HROWS = 448;                // halo rows padded to whole 8-wave DMA rounds
+constexpr int H_BYTES = HROWS * 128;      // one 64-channel image
+constexpr int T = 9;
+constexpr int NSTEP = 2 * T;              // chunks x taps
+constexpr int UNITS = NPTS * 16;          // 16-B output pieces of one board (5776)
+constexpr int MAXL = 24;
+constexpr int MF = 4;                     // 64 co per wave (4 fragments of 16)
+constexpr int NF = 6;                     // 96 px per wave (6 fragments of 16)
+constexpr int NW = 8;
+constexpr int NT = NW * 64;
+constexpr int SCRATCH = 12 * 1024;        // head_body scratch (fused head)
+constexpr int STEP_BYTES = 2 * 2 * MF * 64 * 16;   // one K-step of one layer: 16 KB
+constexpr int WM_BYTES = STEP_BYTES / 2;           // one co-half: 8 KB
+constexpr int CO_STEPS = (UNITS + NT - 1) / NT;    // 12
+
+static_assert(dghead::scratch_bytes(C) <= SCRATCH, "head scratch");
+
+struct StackLayer {
+  const char* A;        // fragment-ordered weights (18 x 16 KB; dgrad: flipped, transposed)
+  const bf16_t* pbias;  // EPI_FWD: bf16 bias + pos-bias in fragment order ([24][2][4][64] x 4)
+  char* Y;              // output frame [B][21][21][128] bf16
+  uint8_t* mask;        // [B][361][16] ReLU bits: EPI_FWD writes (optional), EPI_DGRAD reads
+};
+struct StackArgs {
+  const char* X0;       // input frame [B][21][21][128] bf16 of the first layer
+  int nl;
+  int fuse_head;        // EPI_FWD: run the policy head on the final image
+  StackLayer L[MAXL];
+  dghead::HeadMArgs head;  // (head_body.h; X unused: the image is resident)
+};
+
+DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+
+// s_waitcnt lgkmcnt(0) (LDS writes of this wave done), vmcnt/expcnt untouched, then barrier:
+// unlike __syncthreads() this does not drain the weight loads already in flight
+DG_DEV void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+
+// MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
+// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop
+template <int EPI, int MODE>
+__global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int b = blockIdx.x;
+  char* sH = smem + SCRATCH;  // image c at sH + c * H_BYTES
+
+  // ---- prologue: the first layer's input frame (both 64-channel images) by LDS-DMA ----
+  {
+    const char* Xb = a.X0 + (size_t)b * FF * C * 2;
+    for (int j = wave; j < 2 * (HROWS / 8); j += NW) {
+      const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
+      int r = jj * 8 + (lane >> 3);
+      r = r < FF ? r : FF - 1;
+      const int rl = jj * 8 + (lane >> 3);  // LDS row this lane fills (slot lane & 7)
+      const int gs_ = (lane & 7) ^ fsig(rl);
+      glds16(Xb + ((size_t)r * C + c * 64 + gs_ * 8) * 2,
+             (LDS_AS void*)(sH + c * H_BYTES + jj * 1024));
+    }
+  }
+
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  // this lane's B-fragment rows: pixel p = wn*96 + j*16 + lr (clamped), frame row fp,
+  // swizzle signature fs (before & 7)
+  // packed per fragment: row byte offset fp*128 (16 bits) | (fs & 7) << 16 (one VGPR each)
+  uint32_t pk[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    pk[j] = (uint32_t)(((h + 1) * F + (w + 1)) * 128) | ((uint32_t)(((w + 1) + 3 * (h + 1)) & 7) << 16);
+  }
+  const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
+
+  // A fragments of one k-half of a K-step (A = the step's 16 KB): 4 x 1 KB pieces, one
+  // global_load_dwordx4 each.  Plain loads (the compiler counts them and waits for them);
+  // the sched_barriers in the step pin where they issue — left alone the scheduler sinks
+  // them next to their consumer, a half step later.
+  auto load_A = [&](const char* A, int kk, bf16x8 (&r)[MF]) {
+    const char* p = A + a_lane + kk * MF * 1024;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) r[i] = *(const bf16x8*)(p + i * 1024);
+  };
+  // B fragments (pixels x 32 channels of k-half kk) of K-step s from the resident image:
+  // slot (kk*4 + lq) ^ sig, and kk = 1 is kk = 0 with bit 2 of the slot flipped
+  auto read_B = [&](int s, int kk, bf16x8 (&bfr)[NF]) {
+    const int c = s / T, t = s % T;
+    const LDS_AS char* sHc = (const LDS_AS char*)(sH + c * H_BYTES);
+    const int toff = (t / 3 - 1) * F + (t % 3 - 1);
+    const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int off = (int)(pk[j] & 0xFFFFu) + toff * 128 +
+                      ((lq ^ (((int)(pk[j] >> 16) + tsig) & 7)) * 16);
+      bfr[j] = lds_read_b128(sHc + (off ^ (kk * 64)));
+    }
+  };
+  auto mma = [&](const bf16x8 (&af)[MF], const bf16x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+  };
+
+  // Copy-out of the previous layer's output (resident in the image) to HBM, one 16-B piece
+  // (8 channels of one pixel) per thread and K-step over the first 12 K-steps: the piece
+  // of step s is READ from LDS during step s-1 and STORED in step s.  Thread tid always
+  // handles channel piece q = tid & 15 of pixels p = tid / 16 + 32 s.
+  const int co_q = tid & 15;
+  auto co_read = [&](int s_) -> uint4 {
+    const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    const int f = (h + 1) * F + (w + 1);
+    return *(const uint4*)(sH + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig(f)) * 16));
+  };
+  auto co_store = [&](int s_, const uint4& v, const StackLayer& Lo) {
+    // lanes past the board re-store pixel 360 (same value): every wave issues the stores
+    const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    const int f = (h + 1) * F + (w + 1);
+    *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
+    if (EPI == EPI_FWD && Lo.mask) {
+      // bit per nonzero bf16 half (as the gates test it): packed min(x, 1) per half
+      typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+      auto nz2 = [](uint32_t x) {
+        const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
+        const uint32_t t = __builtin_bit_cast(uint32_t, m);
+        return (t | (t >> 15)) & 3u;
+      };
+      Lo.mask[((size_t)b * NPTS + p) * 16 + co_q] =
+          (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
+    }
+  };
+
+  __syncthreads();  // image landed (the compiler waits for the LDS-DMA before the barrier)
+
+  bf16x8 Ak[2][MF];
+  load_A(a.L[0].A, 0, Ak[0]);
+  load_A(a.L[0].A, 1, Ak[1]);  // (first waits: nothing newer in flight)
+
+  for (int l = 0; l < a.nl; ++l) {
+    const StackLayer L = a.L[l];
+    const char* A_next = l + 1 < a.nl ? a.L[l + 1].A : L.A;
+    const StackLayer Lprev = a.L[l > 0 ? l - 1 : 0];
+    const bool co_on = l > 0;
+    f32x4 acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 co_v;
+
+    // One K-step.  A k-half's fragments (the next step's) are re-loaded right after that
+    // k-half's MFMAs are issued: one register set, half a step of prefetch distance.  Plain
+    // loads the compiler counts; the sched_barriers pin where they issue (left alone, the
+    // scheduler sinks them next to their consumer).  The copy-out store goes last, after
+    // the loads, so waiting for a load never waits for a store issued after it.
+    // Rolled on purpose: the compiler's wait at the loop head is then vmcnt(0) (the k-half-1
+    // loads and the copy-out stores of the previous step drain there), and unrolled by 2 or
+    // 3 every wait names exactly the loads it needs, yet measured 267 / 279 us vs 233 us
+    // for the 10-layer forward (profiles/r2_kbench_stack2.json: with precise waits the
+    // copy-out stores pile up behind the loads, 60 vs 20 us of copy-out cost)
+#pragma unroll 1
+    for (int s = 0; s < NSTEP; ++s) {
+      // (past the last step of the last layer: a harmless re-load of step 0)
+      const char* An = s + 1 < NSTEP ? L.A + (s + 1) * STEP_BYTES : A_next;
+      bf16x8 bfr[NF];
+      if constexpr (!(MODE & 8)) read_B(s, 0, bfr);
+      mma(Ak[0], bfr, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(MODE & 2)) load_A(An, 0, Ak[0]);
+      if (!(MODE & 4) && co_on && s < CO_STEPS) co_v = co_read(s);
+      if constexpr (!(MODE & 8)) read_B(s, 1, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(Ak[1], bfr, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(MODE & 2)) load_A(An, 1, Ak[1]);
+      if (!(MODE & 4) && co_on && s < CO_STEPS) co_store(s, co_v, Lprev);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: write the layer's output back into the LDS image ----
+    // every global load of the epilogue is issued before the first use
+    uint2 eu[NF][EPI == EPI_FWD ? MF : 1];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
+      if constexpr (EPI == EPI_FWD) {
+        const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+      } else {  // 64 channel bits of this wave's image half
+        eu[j][0] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8);
+      }
+    }
+    lds_barrier();  // every wave is past its last read of this layer's image
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = wn * NF * 16 + j * 16 + lr;
+      const int f = (int)(pk[j] & 0xFFFFu) >> 7;
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
+        f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_FWD) {
+          const uint2 u = eu[j][i];
+          v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
+          v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+          v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
+          v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+        } else {
+          const uint32_t word = (cl < 32) ? eu[j][0].x : eu[j][0].y;
+          const uint32_t bits = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] : 0.f;
+        }
+        uint2 o;
+        o.x = pack_bf16x2(v[0], v[1]);
+        o.y = pack_bf16x2(v[2], v[3]);
+        const int slot = (cl >> 3) ^ (int)(pk[j] >> 16);
+        if (p < NPTS) *(uint2*)(sH + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
+      }
+    }
+    lds_barrier();  // the next layer's input is complete
+  }
+  // last layer's output: exposed copy-out
+  {
+    const StackLayer Ll = a.L[a.nl - 1];
+    for (int s_ = 0; s_ < CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
+  }
+  // the policy head on the board image that is already in LDS (no re-staging, no launch)
+  if constexpr (EPI == EPI_FWD) {
+    if (a.fuse_head) dghead::head_body<C>(a.head, b, sH, smem, [](int) {});
+  }
+}
+
+template <int EPI, int MODE>
+hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
+  constexpr size_t lds = SCRATCH + 2 * (size_t)H_BYTES;
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_stack2_kernel<EPI, MODE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+  hipLaunchKernelGGL((conv_stack2_kernel<EPI, MODE>), dim3(B), dim3(NT), lds, stream, a);
+  return hipGetLastError();
+}
+
+int g_stack2_bdb = -1;  // ablation MODE of the forward (0 = production)
+
+hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int B,
+                         const dghead::HeadMArgs* head, hipStream_t stream) {
+  if (nl <= 0 || nl > MAXL || B <= 0) return hipErrorInvalidValue;
+  if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
+  StackArgs a;
+  a.fuse_head = 0;
+  a.head = dghead::HeadMArgs{};
+  a.X0 = (const char*)X0;
+  a.nl = nl;
+  for (int i = 0; i < nl; ++i) {
+    a.L[i].A = (const char*)table[4 * i];
+    a.L[i].pbias = (const bf16_t*)table[4 * i + 1];
+    a.L[i].Y = (char*)table[4 * i + 2];
+    a.L[i].mask = (uint8_t*)table[4 * i + 3];
+    if (!a.L[i].A || !a.L[i].Y) return hipErrorInvalidValue;
+    if (epi == EPI_FWD && !a.L[i].pbias) return hipErrorInvalidValue;
+    if (epi == EPI_DGRAD && !a.L[i].mask) return hipErrorInvalidValue;
+  }
+  if (head) {
+    if (epi != EPI_FWD) return hipErrorInvalidValue;
+    a.fuse_head = 1;
+    a.head = *head;
+  }
+  if (g_stack2_bdb < 0) {
+    g_stack2_bdb = 0;
+  }
+  if (epi == EPI_DGRAD) {
+    return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
+  }
+  switch (g_stack2_bdb) {  // forward: the MODE ablations too (kbench_stack.py)
+    case 2: return launch_stack2<EPI_FWD, 2>(a, B, stream);
+    case 6: return launch_stack2<EPI_FWD, 6>(a, B, stream);
+    case 14: return launch_stack2<EPI_FWD, 14>(a, B, stream);
+    case 4: return launch_stack2<EPI_FWD, 4>(a, B, stream);
+    case 10: return launch_stack2<EPI_FWD, 10>(a, B, stream);
+    default: return launch_stack2<EPI_FWD, 0>(a, B, stream);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void dg_conv_stack2_set_bdb(int on) { g_stack2_bdb = on; }
+
+// table: nl rows of {A (fragment-ordered weights), pbias_frag, Y, mask} (int64 pointers)
+//   epi 1 (forward): pbias required, mask optional (written)
+//   epi 2 (dgrad)  : mask required (read; ReLU bits of the layer below), pbias unused
+hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
+                          hipStream_t stream) {
+  return stack2_launch(epi, table, nl, X0, B, nullptr, stream);
+}
+
+// Forward stack + the 3x3 / 128-channel policy head fused after its last layer.
+hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
+                                   const float* w, const float* bias, const float* posb,
+                                   const int* labels, float* loss, int* pred, void* dZ,
+                                   float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                   hipStream_t stream) {
+  const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
+                            gw_part, dzb, head_relu, grad_scale};
+  return stack2_launch(EPI_FWD, table, nl, X0, B, &h, stream);
+}
+
+}  // extern "C"

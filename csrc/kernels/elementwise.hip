@@ -243,6 +243,8 @@ struct WRefreshLayer {
   bf16_t* pbias;       // [361][cout] or null
   uint2* pbias_frag;   // the same table in the board-resident stack's accumulator-fragment
                        // order (cout == 128): [24 px frags][2 co halves][4][64 lanes] x 4 bf16
+  uint4* wf_frag;      // conv_stack2 A operands (3x3, 128 -> 128 only), MFMA fragment order:
+  uint4* wd_frag;      //   [step 18][wm 2][kk 2][i 4][lane 64] x 8 bf16 (forward / dgrad)
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -290,13 +292,32 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       }
       tileS[rr][cc] = v;
     }
+    if (L.wd || L.wf_frag) __syncthreads();
     if (L.wd) {
-      __syncthreads();
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
         const int ci = cit * 64 + rr, co = cot * 64 + cc;
         if (co < L.cout && ci < L.cin)
           L.wd[(size_t)ci * L.kpd + (L.taps - 1 - t) * L.cout + co] = f2bf(tileS[cc][rr]);
+      }
+    }
+    if (L.wf_frag) {
+      // this tile is exactly one 8 KB (step, co-half) chunk of each fragment layout:
+      //   forward: rows co (wm = cot), k = ci of chunk cit at tap t -> step cit * 9 + t
+      //   dgrad  : rows ci (wm = cit), k = co of chunk cot at flipped tap 8 - t
+      // 16-B unit u = (kk * 4 + i) * 64 + lane holds rows i*16 + (lane & 15), k = kk*32 +
+      // (lane >> 4)*8 .. +7: one coalesced 16-B store per thread and unit
+      for (int u = threadIdx.x; u < 512; u += 256) {
+        const int kk = u >> 8, i = (u >> 6) & 3, ln = u & 63;
+        const int r = i * 16 + (ln & 15), k0 = kk * 32 + (ln >> 4) * 8;
+        uint32_t f[4], d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          f[e] = pack_bf16x2(tileS[r][k0 + 2 * e], tileS[r][k0 + 2 * e + 1]);
+          d[e] = pack_bf16x2(tileS[k0 + 2 * e][r], tileS[k0 + 2 * e + 1][r]);
+        }
+        L.wf_frag[((size_t)(cit * 9 + t) * 2 + cot) * 512 + u] = uint4{f[0], f[1], f[2], f[3]};
+        L.wd_frag[((size_t)(cot * 9 + (8 - t)) * 2 + cit) * 512 + u] = uint4{d[0], d[1], d[2], d[3]};
       }
     }
     __syncthreads();
@@ -413,9 +434,9 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
   return hipGetLastError();
 }
 
-// layers: n entries of 16 int64 words
+// layers: n entries of 18 int64 words
 //   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, pbias_frag, wf8, s_w, amax_w, bias, posb,
-//    pbias}  (pbias_frag: stack-order table, cout 128 only, or 0)
+//    pbias, wf_frag, wd_frag}  (pbias_frag / *_frag: stack-order tables, 128 -> 128 only, or 0)
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -424,7 +445,7 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 16 * i;
+    const long long* t = table + 18 * i;
     a.L[i].w = (const float*)t[0];
     a.L[i].wf = (bf16_t*)t[1];
     a.L[i].wd = (bf16_t*)t[2];
@@ -442,6 +463,11 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].pbias = (bf16_t*)t[15];
     a.L[i].pbias_frag = (uint2*)t[9];
     if (a.L[i].pbias_frag && a.L[i].cout != 128) return hipErrorInvalidValue;
+    a.L[i].wf_frag = (uint4*)t[16];
+    a.L[i].wd_frag = (uint4*)t[17];
+    if ((a.L[i].wf_frag != nullptr) != (a.L[i].wd_frag != nullptr)) return hipErrorInvalidValue;
+    if (a.L[i].wf_frag && (a.L[i].cout != 128 || a.L[i].cin != 128 || a.L[i].taps != 9))
+      return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;
   }

@@ -35,6 +35,10 @@ from .gocnn import ParamLayout, init_params
 INPUT_CP = 40  # 37 planes padded to 5 x 8-channel groups
 
 
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
 @dataclass
 class ConvPlan:
     index: int
@@ -149,6 +153,18 @@ class HipGoNet:
                             if p.fp8 else None)
             self.plans.append(p)
         self.head = L[-1]
+        # conv_stack2 (csrc/kernels/conv_stack2.hip): fragment-ordered forward / dgrad operands
+        # of every hidden 3x3 128 -> 128 layer, written by weight_refresh beside wf / wd.
+        # DG_STACK_V=1 keeps the LDS-ring stack kernel (conv_stack.hip).
+        self.stack_v = int(os.environ.get("DG_STACK_V", "2"))
+        self.wfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        self.wdfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        if self.stack_v == 2:
+            for p in self.plans:
+                if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
+                    self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
+                                                      device=dev)
+                    self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
 
         # ---- activation / gradient frames ----
         B = batch
@@ -268,7 +284,8 @@ class HipGoNet:
                          self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0,
                          self.params.data_ptr() + 4 * spec.b_off,
                          self.params.data_ptr() + 4 * spec.pos_off,
-                         self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0])
+                         self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0,
+                         _ptr(self.wfrag[p.index]), _ptr(self.wdfrag[p.index])])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
     def _build_plans(self):
@@ -372,9 +389,12 @@ class HipGoNet:
                 P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
                 self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
                 self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
-            self._fwd_train = [fused if f is h.conv_stack_fwd else (f, a)
+            fused = ((h.conv_stack2_fwd_head if self.stack_v == 2 else h.conv_stack_fwd_head),
+                     fused[1])
+            self._fwd_train = [fused if f in (h.conv_stack_fwd, h.conv_stack2_fwd) else (f, a)
                                for f, a in self._fwd]
-            if any(f is h.conv_stack_fwd_head for f, _ in self._fwd_train):
+            if any(f in (h.conv_stack_fwd_head, h.conv_stack2_fwd_head)
+                   for f, _ in self._fwd_train):
                 self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -429,7 +449,8 @@ class HipGoNet:
 
         def ok(p):
             return (p.index > 0 and p.board and not p.fp8 and p.k == 3 and p.cinp == 128
-                    and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1)
+                    and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1
+                    and (self.stack_v != 2 or self.wfrag[p.index] is not None))
         best, cur = [], []
         for p in self.plans:
             cur = cur + [p.index] if ok(p) else []
@@ -441,11 +462,13 @@ class HipGoNet:
         rows = []
         for i in best:
             m = self.relu_mask[i]
-            rows.append([self.wf[i].data_ptr(), self.pbias_frag[i].data_ptr(),
+            A = self.wfrag[i] if self.stack_v == 2 else self.wf[i]
+            rows.append([A.data_ptr(), self.pbias_frag[i].data_ptr(),
                          self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
         self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
-        op = (self.h.conv_stack_fwd, (self._stack_table.ctypes.data, len(best),
+        fn = self.h.conv_stack2_fwd if self.stack_v == 2 else self.h.conv_stack_fwd
+        op = (fn, (self._stack_table.ctypes.data, len(best),
                                       self.act[first - 1].data_ptr(), self.plans[first].KP,
                                       self.B))
         if len(self._fwd) != len(self.plans):  # fp8 quantize ops interleaved: keep per-layer
@@ -476,7 +499,8 @@ class HipGoNet:
             p = self.plans[i]
             return (i > 0 and p.board_d and p.k == 3 and p.cin == 128 and p.cout == 128
                     and L[i].pad == 1 and self.dzp[i - 1] == 1 and p.KPd == p.KP
-                    and self.relu_mask[i - 1] is not None)
+                    and self.relu_mask[i - 1] is not None
+                    and (self.stack_v != 2 or self.wdfrag[i] is not None))
         run = []
         for i in range(len(self.plans) - 1, 0, -1):   # must start at the top hidden layer
             if not ok(i):
@@ -486,10 +510,12 @@ class HipGoNet:
             self._dgrads_first()
             return
         self.dstack = run
-        rows = [[self.wd[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
+        wd = self.wdfrag if self.stack_v == 2 else self.wd
+        rows = [[wd[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
                  self.relu_mask[i - 1].data_ptr()] for i in run]
         self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-        self._bwd_pre.append((self.h.conv_stack, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+        fn = self.h.conv_stack2 if self.stack_v == 2 else self.h.conv_stack
+        self._bwd_pre.append((fn, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
                                                   len(run), self.dz[run[0]].data_ptr(),
                                                   self.plans[run[0]].KPd, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]

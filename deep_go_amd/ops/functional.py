@@ -322,14 +322,23 @@ def sgd_(p: torch.Tensor, g: torch.Tensor, lr: float, decay: float, steps: int =
     return lrt
 
 
-def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0, Mpad_d: int = 0):
+def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0, Mpad_d: int = 0,
+                   frag: bool = False):
+    """bf16 operand layouts of OHWI weights w (weight_refresh_kernel).  frag=True (3x3,
+    128 -> 128 only) also returns the conv_stack2 fragment-ordered forward / dgrad operands."""
     h = hip()
     cout, k, _, cin = w.shape
     wf = torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=w.device)
     wd = torch.zeros((Mpad_d, KPd), dtype=torch.bfloat16, device=w.device) if KPd else None
+    ff = fd = None
+    if frag:
+        ff = torch.zeros(cout * k * k * cin, dtype=torch.bfloat16, device=w.device)
+        fd = torch.zeros_like(ff)
     tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0,
-                     0, 0, 0, 0, 0, 0]],
+                     0, 0, 0, 0, 0, 0, _ptr(ff), _ptr(fd)]],
                    dtype=np.int64)
     h.weight_refresh(tbl.ctypes.data, 1, stream_handle())
     torch.cuda.synchronize()
+    if frag:
+        return wf, wd, ff, fd
     return wf, wd

@@ -65,6 +65,17 @@ def dgrad_weight(w_ohwi: torch.Tensor, KPd: int, Mpad: int) -> torch.Tensor:
     return out
 
 
+def stack_frag(A: torch.Tensor) -> torch.Tensor:
+    """conv_stack2 A-operand order of a [128][1152] operand matrix (fwd_weight / dgrad_weight
+    of a 3x3 128 -> 128 layer, k = tap*128 + channel): K-step s = chunk*9 + tap covers columns
+    tap*128 + chunk*64 .. +64; flat [s 18][wm 2][kk 2][i 4][lane 64][e 8] with row
+    wm*64 + i*16 + (lane & 15), column base + kk*32 + (lane >> 4)*8 + e."""
+    assert A.shape[0] >= 128 and A.shape[1] >= 1152
+    a = A[:128, :1152].reshape(2, 4, 16, 9, 2, 2, 4, 8)   # wm i lr | tap chunk kk lq e
+    # -> chunk tap | wm | kk | i | lq lr | e
+    return a.permute(4, 3, 0, 5, 1, 6, 2, 7).reshape(-1).contiguous()
+
+
 def conv_dims(k: int, cin_frame: int, cout: int, bm: int):
     """K/M padding for a conv whose input frame has ``cin_frame`` channels."""
     ngroups = k * k * cin_frame // 8

@@ -165,3 +165,20 @@ def test_concurrent_rank_loaders_are_deterministic(packed_fixture):
         want = _rank_stream((r, path, 6))
         assert all(np.array_equal(a, b) for a, b in zip(got[r], want))
     assert not np.array_equal(got[0][0], got[1][0])
+
+
+def test_stack_frag_layout_indexing():
+    """layouts.stack_frag puts A[row][col] at the conv_stack2 fragment index (CPU check of the
+    permutation the kernel and weight_refresh assume)."""
+    import torch
+    from deep_go_amd.ops import layouts as LY
+    A = torch.arange(128 * 1152, dtype=torch.float64).reshape(128, 1152)
+    f = LY.stack_frag(A)
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        s, wm, kk, i, lane, e = (int(rng.integers(n)) for n in (18, 2, 2, 4, 64, 8))
+        chunk, tap = divmod(s, 9)
+        row = wm * 64 + i * 16 + (lane & 15)
+        col = tap * 128 + chunk * 64 + kk * 32 + (lane >> 4) * 8 + e
+        idx = ((((s * 2 + wm) * 2 + kk) * 4 + i) * 64 + lane) * 8 + e
+        assert f[idx].item() == A[row, col].item()

@@ -384,3 +384,16 @@ def test_weight_refresh():
     wf, wd = Fn.weight_refresh(w, 32, KP, Mpad, KPd, Mpad_d)
     assert torch.equal(wf, LY.fwd_weight(w, 32, KP, Mpad))
     assert torch.equal(wd, LY.dgrad_weight(w, KPd, Mpad_d))
+
+
+def test_weight_refresh_stack_fragments():
+    """conv_stack2's fragment-ordered A operands (written by weight_refresh from the fp32
+    master) are the plain forward / dgrad operand matrices permuted by layouts.stack_frag."""
+    from deep_go_amd.ops import functional as Fn
+    from deep_go_amd.ops import layouts as LY
+    w = torch.randn(128, 3, 3, 128, device=DEV)
+    KP, _, Mpad = LY.conv_dims(3, 128, 128, 128)
+    wf, wd, ff, fd = Fn.weight_refresh(w, 128, KP, Mpad, KP, Mpad, frag=True)
+    assert torch.equal(ff, LY.stack_frag(wf))
+    assert torch.equal(fd, LY.stack_frag(wd))
+    assert torch.equal(ff, LY.stack_frag(LY.fwd_weight(w, 128, KP, Mpad)))

@@ -1,0 +1,76 @@
+"""Board-resident layer stacks (csrc/kernels/conv_stack.hip, conv_stack2.hip) against a plain
+PyTorch fp32 oracle, layer by layer (teacher-forced: each layer's oracle input is the
+kernel's own bf16 output of the layer below, so errors do not compound).
+
+The stack computes, per layer l with operand matrix A_l [128][9*128] (k = tap*128 + c):
+  out[r][p] = sum_{tap, c} A_l[r][tap*128 + c] * X[p + off(tap)][c]   (zero padded 19x19)
+  EPI_FWD  : Y = relu(out + pbias)          (pbias = 0 here) and the ReLU bitmask
+  EPI_DGRAD: Y = out * mask bit(r)          (mask = the random bitmask supplied)
+Both epilogues see the same A, so one oracle covers the forward and the dgrad stack (for the
+dgrad A holds the flipped, transposed weights).  Reference ops: experiments.lua:137-147.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+C = 128
+
+
+def _oracle(A, x_frame, mask, epi):
+    """A [128][1152] bf16, x_frame [B][21][21][128] bf16 -> fp32 [B][19][19][128]."""
+    from deep_go_amd.ops import layouts as LY
+    x = LY.frame_interior(x_frame, 1).float().permute(0, 3, 1, 2)          # B C 19 19
+    w = A[:C, :9 * C].float().reshape(C, 3, 3, C).permute(0, 3, 1, 2)    # r c kh kw
+    out = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)                   # B 19 19 r
+    if epi == "fwd":
+        return out.relu()
+    bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1)  # B 361 16 8
+    return out * bits.reshape(out.shape[0], 19, 19, C).float()
+
+
+@pytest.mark.parametrize("impl", ["v1", "v2", "v2nodb"])
+@pytest.mark.parametrize("epi", ["fwd", "dgrad"])
+def test_stack_layers_match_fp32_oracle(impl, epi):
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    torch.manual_seed(3)
+    B, NL = 6, 3
+    KP = 9 * C
+    x = LY.alloc_frame(B, C, 1, DEV)
+    LY.frame_interior(x, 1).copy_(torch.randn(B, 19, 19, C, device=DEV).relu())
+    As, ys, ms = [], [], []
+    for _ in range(NL):
+        As.append((torch.randn(C, KP, device=DEV) / (3 * C ** 0.5)).to(torch.bfloat16))
+        ys.append(LY.alloc_frame(B, C, 1, DEV))
+        ms.append(torch.randint(0, 256, (B, 361, 16), dtype=torch.uint8, device=DEV))
+    pb = torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=DEV)
+    ops = [LY.stack_frag(a) for a in As] if impl != "v1" else As
+    tab = np.array([[ops[i].data_ptr(), pb.data_ptr() if epi == "fwd" else 0, ys[i].data_ptr(),
+                     ms[i].data_ptr()] for i in range(NL)], dtype=np.int64)
+    masks_in = [m.clone() for m in ms]
+    e = h.EPI_FWD if epi == "fwd" else h.EPI_DGRAD
+    if impl == "v1":
+        h.conv_stack(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
+    else:
+        h.conv_stack2_set_bdb(1 if impl == "v2" else 0)
+        h.conv_stack2(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
+        h.conv_stack2_set_bdb(1)  # back to the default
+    torch.cuda.synchronize()
+    xin = x
+    for l in range(NL):
+        ref = _oracle(As[l], xin, masks_in[l], epi)
+        got = LY.frame_interior(ys[l], 1).float()
+        err = ((got - ref).abs().max() / (ref.abs().max() + 1e-6)).item()
+        assert err < 1e-2, f"{impl} {epi} layer {l}: rel err {err:.3g}"
+        # zero border untouched
+        assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
+        if epi == "fwd":  # bitmask written = nonzero of the bf16 output
+            nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, 16, 8).long()
+            packed = (nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8)
+            assert torch.equal(packed, ms[l]), f"{impl} fwd layer {l}: mask"
+        xin = ys[l]

@@ -13,6 +13,8 @@
 #   pmc[:ARGS]       rocprofv3 --kernel-trace --pmc (MFMA busy, waits, LDS conflicts, clock) of
 #                    bench.py --steps 3 --warmup 1 --no-graph ARGS -> gpurun_out/pmc_<n>/ and
 #                    a per-kernel summary (tools/pmc_summary.py)
+#   pmcpy:SCRIPT     the pmc counters (+ LDS wait / LDS-active) over python SCRIPT (a kernel
+#                    micro-benchmark) -> gpurun_out/pmcpy_<n>/ and a per-kernel summary
 #   py:SCRIPT ARGS   python SCRIPT ARGS (a tools/ script), stdout -> gpurun_out/py_<n>.log
 #   ab:R:A|B|...     R interleaved rounds of bench.py under env settings A, B, ... ("-" = none)
 set -o pipefail
@@ -55,6 +57,16 @@ for step in "$@"; do
       if [ $rc = 0 ]; then
         f=$(find gpurun_out/pmc_$n -name '*counter_collection.csv' | head -1)
         python tools/pmc_summary.py "$f" > gpurun_out/pmc_$n.txt && cat gpurun_out/pmc_$n.txt
+      fi ;;
+    pmcpy)
+      C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $C \
+        --output-format csv -d $R/gpurun_out/pmcpy_$n -o run -- \
+        python3 $R/$arg > $R/gpurun_out/pmcpy_$n.log 2>&1)
+      rc=$?
+      if [ $rc = 0 ]; then
+        f=$(find gpurun_out/pmcpy_$n -name '*counter_collection.csv' | head -1)
+        python tools/pmc_summary.py "$f" > gpurun_out/pmcpy_$n.txt && cat gpurun_out/pmcpy_$n.txt
       fi ;;
     py)
       timeout -k 10 600 python $arg > gpurun_out/py_$n.log 2>&1
