@@ -27,12 +27,7 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          const float* bias, const float* posb, const void* aux, int aux_pad,
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
-hipError_t dg_conv_stack_fwd_head(const long long* table, int nl, const void* X0, int KP, int B,
-                                  const float* w, const float* bias, const float* posb,
-                                  const int* labels, float* loss, int* pred, void* dZ,
-                                  float* gw_part, float* dzb, int head_relu, float grad_scale,
-                                  hipStream_t stream);
-void dg_conv_stack2_set_bdb(int on);
+void dg_conv_stack2_set_mode(int on);
 hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
                           hipStream_t stream);
 hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
@@ -40,22 +35,11 @@ hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X
                                    const int* labels, float* loss, int* pred, void* dZ,
                                    float* gw_part, float* dzb, int head_relu, float grad_scale,
                                    hipStream_t stream);
-hipError_t dg_conv_stack_fwd(const long long* table, int nl, const void* X0, int KP, int B,
-                             hipStream_t stream);
-void dg_conv_stack_set_ablate(int mode);
-void dg_conv_stack_set_prof(void* p);
-void dg_conv_stack_set_stagger(int on);
-void dg_conv_stack_set_ring(int n);
-void dg_conv_stack_set_bpf(int on);
-void dg_conv_stack_set_waves(int n);
-hipError_t dg_conv_stack(int epi, const long long* table, int nl, const void* X0, int KP, int B,
-                         hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
                             const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
                             const float* bias, const float* posb, const void* pbias,
                             const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
-void dg_conv_wgrad_set_ring(int on);
 int dg_conv_wgrad_wgs_per_cu();
 void dg_conv_wgrad_set_t3(int on);
 int dg_conv_wgrad_ktile(int KP);
@@ -86,12 +70,6 @@ hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps,
                          const float* s_w, hipStream_t s);
 hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
                            unsigned* amax, hipStream_t s);
-void dg_conv_wgrad3_set_ablate(int mode);
-int dg_wgrad3_tiles(int Mpad, int x_C);
-int dg_wgrad3_wgs_per_cu(int x_C);
-void dg_wgrad3_set_variant(int v);
-hipError_t dg_conv_wgrad3(const void* dZ, int dz_pad, int M, int Mpad, const void* X, int x_pad,
-                          int x_C, int B, int KP, int splits, float* slab, hipStream_t stream);
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
@@ -188,28 +166,6 @@ PYBIND11_MODULE(_dghip, m) {
                 "conv_board_ex");
         },
         "conv_board + optional bf16 bias table (fwd) and ReLU bitmask (fwd writes, dgrad reads)");
-  m.def("conv_stack_fwd", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
-                             uintptr_t stream) {
-    check(dg_conv_stack_fwd(P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
-          "conv_stack_fwd");
-  }, "fused forward of a run of 128->128 3x3 layers, board resident in LDS");
-  m.def("conv_stack_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
-                                  uintptr_t w, uintptr_t bias, uintptr_t posb, uintptr_t labels,
-                                  uintptr_t loss, uintptr_t pred, uintptr_t dZ, uintptr_t gw_part,
-                                  uintptr_t dzb, int head_relu, float grad_scale,
-                                  uintptr_t stream) {
-    check(dg_conv_stack_fwd_head(P<long long>(table), nl, P<void>(X0), KP, B, P<float>(w),
-                                 P<float>(bias), P<float>(posb), P<int>(labels), P<float>(loss),
-                                 P<int>(pred), P<void>(dZ), P<float>(gw_part), P<float>(dzb),
-                                 head_relu, grad_scale, S(stream)),
-          "conv_stack_fwd_head");
-  }, "forward stack + the 3x3/128 policy head (forward, loss, backward) on the resident image");
-  m.def("conv_stack", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
-                         uintptr_t stream) {
-    check(dg_conv_stack(epi, P<long long>(table), nl, P<void>(X0), KP, B, S(stream)),
-          "conv_stack");
-  }, "fused run of 128->128 3x3 layers, board resident in LDS: EPI_FWD forward (+bias, ReLU,"
-     " writes masks) or EPI_DGRAD backward-data chain (ReLU masks of the layers below)");
   // conv_stack2.hip: weights streamed into VGPRs (fragment-ordered), no per-K-step barrier.
   // Same signatures as conv_stack* (KP unused: the fragment layout is fixed for C = 128).
   m.def("conv_stack2_fwd", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
@@ -230,8 +186,8 @@ PYBIND11_MODULE(_dghip, m) {
                                   head_relu, grad_scale, S(stream)),
           "conv_stack2_fwd_head");
   }, "conv_stack2 forward + the fused 3x3/128 policy head");
-  m.def("conv_stack2_set_bdb", [](int on) { dg_conv_stack2_set_bdb(on); },
-        "conv_stack2 B-fragment double buffering across k-halves (default 1)");
+  m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
+        "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
   m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
                           uintptr_t stream) {
     (void)KP;
@@ -245,16 +201,6 @@ PYBIND11_MODULE(_dghip, m) {
                         splits, P<float>(slab), S(stream)),
           "conv_wgrad");
   });
-  m.def("conv_wgrad3", [](uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X, int x_pad,
-                          int x_C, int B, int KP, int splits, uintptr_t slab, uintptr_t stream) {
-    check(dg_conv_wgrad3(P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, B, KP, splits,
-                         P<float>(slab), S(stream)),
-          "conv_wgrad3");
-  });
-  m.def("wgrad3_tiles", [](int Mpad, int x_C) { return dg_wgrad3_tiles(Mpad, x_C); });
-  m.def("wgrad3_wgs_per_cu", [](int x_C) { return dg_wgrad3_wgs_per_cu(x_C); });
-  m.def("wgrad3_set_variant", [](int v) { dg_wgrad3_set_variant(v); },
-        "0: 128-ch chunks / 8 waves; 1: 64-ch / 4 waves (2 WGs per CU); 2: 64-ch / 8 waves");
   m.def("conv_board_fp8", [](int kw, int bm, uintptr_t A8, int KP, int M, int Mpad, uintptr_t X8,
                              int x_pad, int x_C, int B, uintptr_t Y, uintptr_t Y8, int y_pad,
                              uintptr_t bias, uintptr_t posb, uintptr_t s_x, uintptr_t s_w,
@@ -323,12 +269,6 @@ PYBIND11_MODULE(_dghip, m) {
                              P<void>(out), B, pad, CP, nullptr, 0, S(stream)),
           "expand_features");
   });
-  m.def("expand_features2", [](uintptr_t planes, uintptr_t player, uintptr_t rank, uintptr_t out,
-                               int B, int pad, int CP, uintptr_t out2, int CP2, uintptr_t stream) {
-    check(dg_expand_features(P<uint8_t>(planes), P<uint8_t>(player), P<uint8_t>(rank),
-                             P<void>(out), B, pad, CP, P<void>(out2), CP2, S(stream)),
-          "expand_features2");
-  }, "expand into the CP-channel frame and a second CP2-channel copy (board-tiled layer 1)");
   m.def("bias_grad_partial", [](uintptr_t dZ, int B, int C, int pad, uintptr_t part,
                                 uintptr_t stream) {
     check(dg_bias_grad_partial(P<void>(dZ), B, C, pad, P<float>(part), S(stream)),
@@ -368,24 +308,9 @@ PYBIND11_MODULE(_dghip, m) {
   });
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
-  m.def("conv_stack_set_ablate", [](int mode) { dg_conv_stack_set_ablate(mode); },
-        "timing ablations of conv_stack (forward): 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no"
-        " copy-out, 16 no barrier");
   m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },
         "3x3/128- and 256-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
-  m.def("conv_stack_set_prof", [](uintptr_t p) { dg_conv_stack_set_prof(P<void>(p)); },
-        "ablate 32: per-wave phase cycle sums [B][8][8] (s_memtime)");
-  m.def("conv_stack_set_stagger", [](int on) { dg_conv_stack_set_stagger(on); },
-        "1: half the waves copy the previous layer out after their first MFMAs");
-  m.def("conv_stack_set_waves", [](int n) { dg_conv_stack_set_waves(n); },
-        "conv_stack waves per workgroup: 8 (64x96 per wave) or 16 (64x48 per wave)");
-  m.def("conv_stack_set_bpf", [](int on) { dg_conv_stack_set_bpf(on); },
-        "B-fragment prefetch across K-steps in conv_stack (default on)");
-  m.def("conv_stack_set_ring", [](int n) { dg_conv_stack_set_ring(n); },
-        "weight-tile ring depth of conv_stack (2 or 3; 0 = default)");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
-  m.def("conv_wgrad_set_ring", [](int on) { dg_conv_wgrad_set_ring(on); },
-        "1: 32-pixel 3-stage ring wgrad for 3x3/5x5 (3 workgroups per CU); 0: 64-pixel 2-stage");
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
   m.def("conv_wgrad_set_t3", [](int on) { dg_conv_wgrad_set_t3(on); },
         "three-slice (128 x 384) wgrad tiles on/off (default on; env DG_WGRAD_T3)");
@@ -424,7 +349,6 @@ PYBIND11_MODULE(_dghip, m) {
         "waves per conv_wgrad_win workgroup: 4 (64-co chunks, 2 per CU; default) or 8");
   m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });
   m.def("conv_wgrad_wgs_per_cu_for", [](int KP) { return dg_conv_wgrad_wgs_per_cu_for(KP); });
-  m.def("conv_wgrad3_set_ablate", [](int mode) { dg_conv_wgrad3_set_ablate(mode); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
 }

@@ -453,152 +453,6 @@ conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// Ring variant of conv_wgrad_kernel: 32-pixel K-steps through an NST-stage LDS ring (16 KB
-// per stage: 3 stages = 48 KB -> three independent workgroups per CU instead of two), the
-// next-but-one stage's LDS-DMA issued from inline asm at the top of each step (invisible to
-// the compiler's waitcnt pass; counted by hand: 4 DMA instructions per wave per stage,
-// s_waitcnt vmcnt(4) keeps the newest stage in flight).  Same tiles, XCD remap, fragment
-// reads and slab layout as conv_wgrad_kernel.
-template <int KW, int NST>
-__global__ void __launch_bounds__(256, 3)
-conv_wgrad_ring_kernel(WgradArgs a) {
-  constexpr int BM = 128, BN = 128, BKN = 32;
-  constexpr int T_BYTES = BKN * 256;           // 32 rows x 256 B
-  constexpr int STAGE = 2 * T_BYTES;
-  constexpr int DPS = 4;                       // DMA instructions per wave per stage
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = a.ktiles * a.mtiles * a.splits;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, xslot = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
-  const int kt = lid % a.ktiles;
-  const int rest = lid / a.ktiles;
-  const int mt = rest % a.mtiles;
-  const int zsplit = rest / a.mtiles;
-  const int k_tile = kt * BN;
-  const int m_tile = mt * BM;
-  const int n_begin = zsplit * a.px_per_split;
-  int n_end = n_begin + a.px_per_split;
-  if (n_end > a.Npix) n_end = a.Npix;
-  const int nsteps = n_end > n_begin ? (n_end - n_begin + BKN - 1) / BKN : 0;
-
-  const int r_in = lane >> 4;
-  const int slot = lane & 15;
-  int koffs[2], dz_chunk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = (wave * 2 + i) * 4 + r_in;
-    const int c = slot ^ wg_swz(r);
-    dz_chunk[i] = (m_tile * 2) + c * 16;
-    koffs[i] = koff_wg<KW>(k_tile / 8 + c, a);
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
-  auto stage = [&](int buf, int step) {
-    const uint32_t sA = lds0 + buf * STAGE;
-    const uint32_t sB = sA + T_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (wave * 2 + i) * 4 + r_in;
-      int n = n_begin + step * BKN + r;
-      const bool ok = n < n_end;
-      if (!ok) n = n_begin;
-      const int b = n / NPTS;
-      const int p = n - b * NPTS;
-      const int h = p / BOARD;
-      const int w = p - h * BOARD;
-      const uint32_t dzo = frame_off(b, h, w, a.dz_pad, a.M);
-      const uint32_t xo = frame_off(b, h, w, a.x_pad, a.x_C);
-      const char* src_dz = ok ? (a.dZ + dzo + dz_chunk[i]) : (a.dZ + (slot * 16));
-      dma16(src_dz, __builtin_amdgcn_readfirstlane(sA + (wave * 2 + i) * 1024));
-      dma16(a.X + xo + koffs[i], __builtin_amdgcn_readfirstlane(sB + (wave * 2 + i) * 1024));
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: stages 0 .. NST-2 in flight, wait for stage 0
-#pragma unroll
-  for (int q0 = 0; q0 < NST - 1; ++q0)
-    if (q0 < nsteps) stage(q0, q0);
-  if (nsteps >= NST - 1) dma_wait<DPS * (NST - 2)>(); else dma_wait<0>();
-  __builtin_amdgcn_s_barrier();
-
-  const int li = lane & 15;
-  const int g = lane >> 4;
-  const int q = li >> 2, pp = li & 3;
-  for (int st = 0; st < nsteps; ++st) {
-    const bool more = st + NST - 1 < nsteps;
-    if (more) stage((st + NST - 1) % NST, st + NST - 1);  // into the stage read at st - 1
-    const int buf = st % NST;
-    const char* sA = smem + buf * STAGE;
-    const char* sB = sA + T_BYTES;
-    s16x4 ta[2][4], tb[2][4];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int row = 8 * g + 4 * half + q;
-      const int sw = wg_swz(row);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = (wm * 64 + i * 16) / 8 + (pp >> 1);
-        ta[half][i] =
-            lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = (wn * 64 + j * 16) / 8 + (pp >> 1);
-        tb[half][j] =
-            lds_read_tr((const LDS_AS char*)(sB + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
-      }
-    }
-    bf16x8 af[4], bfr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const s16x4 lo = ta[0][i], hi = ta[1][i];
-      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = __builtin_bit_cast(bf16x8, v);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const s16x4 lo = tb[0][j], hi = tb[1][j];
-      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      bfr[j] = __builtin_bit_cast(bf16x8, v);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-    __builtin_amdgcn_sched_barrier(0);
-    // stage st+1 must have landed for every wave; stage st+NST-1 (issued above) may fly
-    if (more && NST > 2) dma_wait<DPS * (NST - 2)>(); else dma_wait<0>();
-    __builtin_amdgcn_s_barrier();
-  }
-
-  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = m_tile + wm * 64 + i * 16 + g * 4 + r;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k_tile + wn * 64 + j * 16 + li;
-        slab[(size_t)co * a.KP + k] = acc[i][j][r];
-      }
-    }
-  }
-}
-
-
 // Three-tap variant of conv_wgrad_kernel: one workgroup (8 waves) owns a 128 co x 384 k
 // tile — three consecutive 128-k slices (e.g. the three dw taps of one kernel row) — so the
 // dZ rows staged for a 64-pixel step serve three slices instead of one: 64 KB of LDS-DMA
@@ -972,16 +826,7 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
 
 static int g_wgrad_ablate = 0;
 void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
-static int g_wgrad_ring = -1;
-static bool wgrad_ring_enabled() {
-  if (g_wgrad_ring < 0) {
-    const char* e = getenv("DG_WGRAD_RING");
-    g_wgrad_ring = e ? atoi(e) : 0;
-  }
-  return g_wgrad_ring != 0;
-}
-void dg_conv_wgrad_set_ring(int on) { g_wgrad_ring = on; }
-int dg_conv_wgrad_wgs_per_cu() { return wgrad_ring_enabled() ? 3 : 2; }
+int dg_conv_wgrad_wgs_per_cu() { return 2; }
 static int g_wgrad_t3 = -1;
 static bool wgrad_t3_enabled() {
   if (g_wgrad_t3 < 0) {
@@ -993,7 +838,7 @@ static bool wgrad_t3_enabled() {
 void dg_conv_wgrad_set_t3(int on) { g_wgrad_t3 = on; }
 // k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K
 int dg_conv_wgrad_ktile(int KP) {
-  return (wgrad_t3_enabled() && !wgrad_ring_enabled() && KP % 384 == 0) ? 384 : 128;
+  return (wgrad_t3_enabled() && KP % 384 == 0) ? 384 : 128;
 }
 int dg_conv_wgrad_wgs_per_cu_for(int KP) {
   return dg_conv_wgrad_ktile(KP) == 384 ? 1 : dg_conv_wgrad_wgs_per_cu();
@@ -1038,12 +883,6 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
     return launch_t3(kw, a, Ls, stream);
   }
   dim3 grid(a.ktiles * a.mtiles * splits);
-  if (wgrad_ring_enabled() && (kw == 3 || kw == 5)) {
-    constexpr size_t lds_r = 3 * 2 * 32 * 256;
-    if (kw == 3) hipLaunchKernelGGL((conv_wgrad_ring_kernel<3, 3>), grid, dim3(256), lds_r, stream, a);
-    else hipLaunchKernelGGL((conv_wgrad_ring_kernel<5, 3>), grid, dim3(256), lds_r, stream, a);
-    return hipGetLastError();
-  }
   const size_t lds = 2 * 2 * 64 * 256;
   switch (kw) {
     case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), lds, stream, a); break;

@@ -309,7 +309,7 @@ hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
   return hipGetLastError();
 }
 
-int g_stack2_bdb = -1;  // ablation MODE of the forward (0 = production)
+int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
 
 hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int B,
                          const dghead::HeadMArgs* head, hipStream_t stream) {
@@ -334,13 +334,10 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     a.fuse_head = 1;
     a.head = *head;
   }
-  if (g_stack2_bdb < 0) {
-    g_stack2_bdb = 0;
-  }
   if (epi == EPI_DGRAD) {
     return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
   }
-  switch (g_stack2_bdb) {  // forward: the MODE ablations too (kbench_stack.py)
+  switch (g_stack2_mode) {  // forward: the MODE ablations too (kbench_stack.py)
     case 2: return launch_stack2<EPI_FWD, 2>(a, B, stream);
     case 6: return launch_stack2<EPI_FWD, 6>(a, B, stream);
     case 14: return launch_stack2<EPI_FWD, 14>(a, B, stream);
@@ -354,7 +351,7 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
 
 extern "C" {
 
-void dg_conv_stack2_set_bdb(int on) { g_stack2_bdb = on; }
+void dg_conv_stack2_set_mode(int m) { g_stack2_mode = m; }
 
 // table: nl rows of {A (fragment-ordered weights), pbias_frag, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)

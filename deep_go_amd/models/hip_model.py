@@ -60,9 +60,7 @@ class ConvPlan:
     bn_d: int = 128
     board: bool = False    # fwd uses the board-tiled kernel
     board_d: bool = False  # dgrad uses the board-tiled kernel
-    wgrad3: bool = False   # wgrad uses the row-stripe kernel (conv_wgrad3.hip)
     fp8: bool = False      # forward on the e4m3 MX-MFMA kernel (conv_fp8.hip)
-    cinp_f: int = 0        # forward input-frame channels if != cinp (board-tiled layer 1: 64)
 
 
 class HipGoNet:
@@ -114,29 +112,15 @@ class HipGoNet:
             cinp = INPUT_CP if spec.index == 0 else spec.cin
             board = LY.board_ok(spec.k, cinp)
             bm, bn = LY.pick_tiles(npix, spec.cout, num_cus)
-            cinp_f = 0
             if board:
                 bm = LY.board_bm(spec.cout)
-            elif (spec.index == 0 and spec.k in (1, 3, 5) and spec.pad <= 2
-                  and os.environ.get("DG_L1_BOARD", "0") == "1"):
-                # first layer on the board kernel: the expansion kernel also writes a
-                # 64-channel copy of the input frame (channels >= 37 zero); the wgrad keeps
-                # the 40-channel frame (60% less K).  BM 128: one 1-round grid of 256 boards.
-                board, cinp_f, bm = True, 64, 128
-            KP, KPw, Mpad = LY.conv_dims(spec.k, cinp_f or cinp, spec.cout, bm)
-            if cinp_f:
-                _, KPw, _ = LY.conv_dims(spec.k, cinp, spec.cout, bm)
+            KP, KPw, Mpad = LY.conv_dims(spec.k, cinp, spec.cout, bm)
             Mpad_w = LY.round_up(spec.cout, 128)
-            w3 = LY.wgrad3_ok(spec.k, cinp, spec.pad) and os.environ.get("DG_WGRAD3", "0") == "1"
-            if w3:
-                splits = LY.pick_wgrad3_splits(batch, self.h.wgrad3_tiles(Mpad_w, cinp),
-                                                self.h.wgrad3_wgs_per_cu(cinp), num_cus)
-            else:
-                splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
-                                               self.h.conv_wgrad_wgs_per_cu_for(KPw),
-                                               self.h.conv_wgrad_ktile(KPw))
+            splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
+                                           self.h.conv_wgrad_wgs_per_cu_for(KPw),
+                                           self.h.conv_wgrad_ktile(KPw))
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
-                         Mpad, KPw, Mpad_w, splits, board=board, wgrad3=w3, cinp_f=cinp_f)
+                         Mpad, KPw, Mpad_w, splits, board=board)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
             if spec.index > 0:
                 bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
@@ -154,24 +138,19 @@ class HipGoNet:
             self.plans.append(p)
         self.head = L[-1]
         # conv_stack2 (csrc/kernels/conv_stack2.hip): fragment-ordered forward / dgrad operands
-        # of every hidden 3x3 128 -> 128 layer, written by weight_refresh beside wf / wd.
-        # DG_STACK_V=1 keeps the LDS-ring stack kernel (conv_stack.hip).
-        self.stack_v = int(os.environ.get("DG_STACK_V", "2"))
+        # of every hidden 3x3 128 -> 128 layer, written by weight_refresh beside wf / wd
         self.wfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wdfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
-        if self.stack_v == 2:
-            for p in self.plans:
-                if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
-                    self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
-                                                      device=dev)
-                    self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
+        for p in self.plans:
+            if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
+                self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
+                                                  device=dev)
+                self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
 
         # ---- activation / gradient frames ----
         B = batch
         pads = [s.pad for s in L]
         self.x0 = LY.alloc_frame(B, INPUT_CP, pads[0], dev)
-        self.x0b = (LY.alloc_frame(B, self.plans[0].cinp_f, pads[0], dev)
-                    if self.plans[0].cinp_f else None)
         # act[i]: output of layer i, framed with the pad of layer i+1
         self.act = [LY.alloc_frame(B, L[i].cout, pads[i + 1], dev) for i in range(self.L - 1)]
         # dz[i]: d loss / d pre-activation of layer i, framed with layer i's pad (>=1)
@@ -214,34 +193,25 @@ class HipGoNet:
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self._fp8_calibrated = not self.fp8
-        # backward side stream (off by default: both measured slower, profiles/README.md):
-        # "light" runs the bandwidth-bound bias-grad partials and split-K slab reduces beside
-        # the wgrads (each layer then needs its own slab / partial buffers: ~34 MB per
-        # 128-channel layer, nothing next to 288 GB) — 1.43 vs 1.37 ms/step: they compete
-        # with the wgrad's own L2->LDS traffic (wgrad 42 -> 49 us); "wgrad"
-        # (DG_SIDE_STREAM=1) runs the whole weight-gradient chain beside the dgrads
-        # "bias" runs only the HBM-bound bias-grad partials on the side stream, beside the
-        # MFMA-bound weight-gradient launch of the same layers (everything else as "none")
-        # (default "bias": 262k -> 264k boards/s at 12x128, neutral at 12x256)
+        # backward side stream ("bias", the default): the HBM-bound bias-grad partials run on
+        # it beside the MFMA-bound weight-gradient launch of the same layers, and the first
+        # layer's whole weight-gradient chain beside the last wgrad group (262k -> 264k
+        # boards/s at 12x128 when introduced, neutral at 12x256).  DG_SIDE_STREAM=0: one
+        # stream.  (Two other modes — the whole wgrad chain, or partials + slab reduces,
+        # on the side stream — measured slower and were removed in round 2.)
         side_mode = os.environ.get("DG_SIDE_STREAM", "bias")
-        self.side_mode = {"1": "wgrad", "0": "none"}.get(side_mode, side_mode)
-        if self.side_mode not in ("none", "wgrad", "light", "bias"):
-            raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0, 1, light or bias")
+        self.side_mode = {"0": "none"}.get(side_mode, side_mode)
+        if self.side_mode not in ("none", "bias"):
+            raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0 or bias")
         self.bchunks = self.h.bias_chunks(batch)
-        if self.side_mode == "light":
-            self.slabs = [torch.empty(p.splits * p.Mpad_w * p.KPw, dtype=torch.float32,
-                                      device=dev) for p in self.plans]
-            self.bparts = [torch.empty(self.bchunks * (NUM_POINTS + 19) * p.cout,
-                                       dtype=torch.float32, device=dev) for p in self.plans]
-        else:
-            slab = torch.empty(max(p.splits * p.Mpad_w * p.KPw for p in self.plans),
-                               dtype=torch.float32, device=dev)
-            cmax = max(p.cout for p in self.plans)
-            bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
-                                device=dev)
-            self.slabs = [slab] * len(self.plans)
-            self.bparts = [bpart] * len(self.plans)
-        self.slab = self.slabs[0]
+        slab = torch.empty(max(p.splits * p.Mpad_w * p.KPw for p in self.plans),
+                           dtype=torch.float32, device=dev)
+        cmax = max(p.cout for p in self.plans)
+        bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
+                            device=dev)
+        self.slabs = [slab] * len(self.plans)
+        self.bparts = [bpart] * len(self.plans)
+        self.slab = slab
 
         # ---- step I/O ----
         # one packed uint8 input buffer (planes | player | rank | labels as int32), so a step's
@@ -276,7 +246,7 @@ class HipGoNet:
             w = self.params[spec.w_off:spec.w_off + spec.w_numel]
             w8 = self.wf8[p.index]
             rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0,
-                         p.cout, p.cin, p.k * p.k, p.cinp_f or p.cinp, p.KP, p.KPd,
+                         p.cout, p.cin, p.k * p.k, p.cinp, p.KP, p.KPd,
                          self.pbias_frag[p.index].data_ptr()
                          if self.pbias_frag[p.index] is not None else 0,
                          w8.data_ptr() if w8 is not None else 0,
@@ -296,15 +266,9 @@ class HipGoNet:
         self._pre: List[Tuple[Callable, tuple]] = []
         self._fwd: List[Tuple[Callable, tuple]] = []
         self._bwd: List[List[Tuple[Callable, tuple]]] = []  # per layer (index order)
-        if self.x0b is not None:
-            self._pre.append((h.expand_features2, (
-                self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
-                self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP, self.x0b.data_ptr(),
-                self.plans[0].cinp_f)))
-        else:
-            self._pre.append((h.expand_features, (
-                self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
-                self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP)))
+        self._pre.append((h.expand_features, (
+            self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
+            self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP)))
         for p in self.plans:
             spec = lay.layers[p.index]
             xin = self.x0 if p.index == 0 else self.act[p.index - 1]
@@ -324,11 +288,9 @@ class HipGoNet:
                     self.relu_mask[i].data_ptr() if self.relu_mask[i] is not None else 0)))
             elif p.board:
                 msk = self.relu_mask[p.index]
-                if p.cinp_f:
-                    xin = self.x0b
                 self._fwd.append((h.conv_board_ex, (
                     h.EPI_FWD, p.k, p.bm, self.wf[p.index].data_ptr(), p.KP, p.cout, p.Mpad,
-                    xin.data_ptr(), x_pad, p.cinp_f or p.cinp, self.B,
+                    xin.data_ptr(), x_pad, p.cinp, self.B,
                     self.act[p.index].data_ptr(), y_pad,
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
                     msk.data_ptr() if msk is not None else 0)))
@@ -375,7 +337,7 @@ class HipGoNet:
                                     self.eval_pred.data_ptr(), 0, 0, 0, 0, 0, 0,
                                     int(self.cfg.head_relu), 1.0 / self.global_batch))
         # training: the head runs inside the forward stack's launch when the stack ends at the
-        # last hidden layer (its image is already in LDS; conv_stack.hip + head_body.h);
+        # last hidden layer (its image is already in LDS; conv_stack2.hip + head_body.h);
         # evaluation keeps the standalone head.  DG_FUSE_HEAD=0 keeps the separate launch.
         self._fwd_train = self._fwd
         if (self.stack and self.stack[-1] == len(self.plans) - 1 and hd.k == 3
@@ -383,18 +345,15 @@ class HipGoNet:
                 and os.environ.get("DG_FUSE_HEAD", "1") != "0"
                 and os.environ.get("DG_HEAD_MFMA", "1") != "0"):
             first = self.stack[0]
-            fused = (h.conv_stack_fwd_head, (
+            fused = (h.conv_stack2_fwd_head, (
                 self._stack_table.ctypes.data, len(self.stack), self.act[first - 1].data_ptr(),
                 self.plans[first].KP, self.B, P + hd.w_off * f4, P + hd.b_off * f4,
                 P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
                 self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
                 self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
-            fused = ((h.conv_stack2_fwd_head if self.stack_v == 2 else h.conv_stack_fwd_head),
-                     fused[1])
-            self._fwd_train = [fused if f in (h.conv_stack_fwd, h.conv_stack2_fwd) else (f, a)
+            self._fwd_train = [fused if f is h.conv_stack2_fwd else (f, a)
                                for f, a in self._fwd]
-            if any(f in (h.conv_stack_fwd_head, h.conv_stack2_fwd_head)
-                   for f, _ in self._fwd_train):
+            if any(f is h.conv_stack2_fwd_head for f, _ in self._fwd_train):
                 self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -407,14 +366,9 @@ class HipGoNet:
             slab, bpart = self.slabs[i].data_ptr(), self.bparts[i].data_ptr()
             ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
                                               bpart)))
-            if p.wgrad3:
-                ops.append((h.conv_wgrad3, (self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                            xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                            p.splits, slab)))
-            else:
-                ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                           xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                           p.splits, slab)))
+            ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                       xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
+                                       p.splits, slab)))
             ops.append((h.wgrad_reduce, (slab, G + spec.w_off * f4, p.splits,
                                          p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp,
                                          bpart, self.bchunks,
@@ -440,8 +394,8 @@ class HipGoNet:
 
     def _fuse_forward_stack(self):
         """Replace the per-layer forward launches of the longest run of hidden 128->128 3x3
-        bf16 layers by ONE conv_stack_fwd launch (board-resident activations, overlapped
-        stores; csrc/kernels/conv_stack.hip).  DG_STACK=0 keeps per-layer kernels."""
+        bf16 layers by ONE conv_stack2_fwd launch (board-resident activations, overlapped
+        stores; csrc/kernels/conv_stack2.hip).  DG_STACK=0 keeps per-layer kernels."""
         self.stack = []
         if os.environ.get("DG_STACK", "1") == "0":
             return
@@ -450,7 +404,7 @@ class HipGoNet:
         def ok(p):
             return (p.index > 0 and p.board and not p.fp8 and p.k == 3 and p.cinp == 128
                     and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1
-                    and (self.stack_v != 2 or self.wfrag[p.index] is not None))
+                    and self.wfrag[p.index] is not None)
         best, cur = [], []
         for p in self.plans:
             cur = cur + [p.index] if ok(p) else []
@@ -462,13 +416,11 @@ class HipGoNet:
         rows = []
         for i in best:
             m = self.relu_mask[i]
-            A = self.wfrag[i] if self.stack_v == 2 else self.wf[i]
-            rows.append([A.data_ptr(), self.pbias_frag[i].data_ptr(),
+            rows.append([self.wfrag[i].data_ptr(), self.pbias_frag[i].data_ptr(),
                          self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
         self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
-        fn = self.h.conv_stack2_fwd if self.stack_v == 2 else self.h.conv_stack_fwd
-        op = (fn, (self._stack_table.ctypes.data, len(best),
+        op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(best),
                                       self.act[first - 1].data_ptr(), self.plans[first].KP,
                                       self.B))
         if len(self._fwd) != len(self.plans):  # fp8 quantize ops interleaved: keep per-layer
@@ -480,7 +432,7 @@ class HipGoNet:
     def _fuse_dgrad_stack(self):
         """Run the backward-data chain of the longest run of hidden 128->128 3x3 layers as
         ONE conv_stack launch in EPI_DGRAD mode: dZ_{i-1} = relu_mask_{i-1} * (W_i^T * dZ_i)
-        for i = top .. bottom, board-resident in LDS (csrc/kernels/conv_stack.hip).  The
+        for i = top .. bottom, board-resident in LDS (csrc/kernels/conv_stack2.hip).  The
         per-layer dgrad launches of those layers are dropped from ``_bwd``; their weight
         gradients run afterwards (they only read dZ_i).  DG_DSTACK=0 keeps per-layer dgrads."""
         self.dstack: List[int] = []
@@ -500,7 +452,7 @@ class HipGoNet:
             return (i > 0 and p.board_d and p.k == 3 and p.cin == 128 and p.cout == 128
                     and L[i].pad == 1 and self.dzp[i - 1] == 1 and p.KPd == p.KP
                     and self.relu_mask[i - 1] is not None
-                    and (self.stack_v != 2 or self.wdfrag[i] is not None))
+                    and self.wdfrag[i] is not None)
         run = []
         for i in range(len(self.plans) - 1, 0, -1):   # must start at the top hidden layer
             if not ok(i):
@@ -510,12 +462,10 @@ class HipGoNet:
             self._dgrads_first()
             return
         self.dstack = run
-        wd = self.wdfrag if self.stack_v == 2 else self.wd
-        rows = [[wd[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
+        rows = [[self.wdfrag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
                  self.relu_mask[i - 1].data_ptr()] for i in run]
         self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-        fn = self.h.conv_stack2 if self.stack_v == 2 else self.h.conv_stack
-        self._bwd_pre.append((fn, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+        self._bwd_pre.append((self.h.conv_stack2, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
                                                   len(run), self.dz[run[0]].data_ptr(),
                                                   self.plans[run[0]].KPd, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
@@ -589,7 +539,7 @@ class HipGoNet:
 
         def key(i):
             p = self.plans[i]
-            if (i not in dz_ready or p.wgrad3 or p.k not in (3, 5)
+            if (i not in dz_ready or p.k not in (3, 5)
                     or h.conv_wgrad_ktile(p.KPw) != 384):
                 return None
             return (p.k, p.cout, p.Mpad_w, p.KPw, p.cinp, lay[i].pad)
@@ -768,25 +718,6 @@ class HipGoNet:
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
                 fn()
-        elif self.side_mode == "light":
-            # side: bias-grad partials beside this layer's wgrad, then the slab reduce beside
-            # the next launches on the main stream (per-layer slabs: no reuse hazard)
-            side = self.side
-            side.wait_stream(main)               # dZ_i final, earlier wgrads issued
-            self._run(ops[:1], side.cuda_stream)
-            self._run(ops[1:2], main.cuda_stream)
-            side.wait_stream(main)               # wgrad(i) done
-            self._run(ops[2:3], side.cuda_stream)
-            if hooks:
-                main.wait_stream(side)           # layer i's gradients final on main
-                for fn in hooks:
-                    fn()
-        else:
-            self.side.wait_stream(main)          # dZ_i (dgrad of layer i+1 / head) ready
-            with torch.cuda.stream(self.side):
-                self._run(ops[:3], self.side.cuda_stream)
-                for fn in hooks:
-                    fn()
         self._run(ops[3:], main.cuda_stream)
 
     def join_side(self):

@@ -214,14 +214,9 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
                        0, 0, 0, 0, s)
         torch.cuda.synchronize(dev)
         return out
-    w3 = algo == "rows" or (algo == "auto" and LY.wgrad3_ok(k, cinp, pad))
-    if w3:
-        splits = splits or LY.pick_wgrad3_splits(B, h.wgrad3_tiles(Mpad, cinp),
-                                                  h.wgrad3_wgs_per_cu(cinp))
-    else:
-        splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad,
-                                                 wgs_per_cu=h.conv_wgrad_wgs_per_cu_for(KPw),
-                                                 ktile=h.conv_wgrad_ktile(KPw))
+    splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad,
+                                             wgs_per_cu=h.conv_wgrad_wgs_per_cu_for(KPw),
+                                             ktile=h.conv_wgrad_ktile(KPw))
     dzf = LY.to_frame(dz, max(1, pad))
     xf = LY.to_frame(x.to(dev), pad, cinp)
     slab = torch.empty(splits * Mpad * KPw, dtype=torch.float32, device=dev)
@@ -232,12 +227,8 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     bpart = torch.empty(nch * (NPTS + 19) * cout, dtype=torch.float32, device=dev)
     s = stream_handle()
     h.bias_grad_partial(dzf.data_ptr(), B, cout, max(1, pad), bpart.data_ptr(), s)
-    if w3:
-        h.conv_wgrad3(dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B, KPw,
-                      splits, slab.data_ptr(), s)
-    else:
-        h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B,
-                     KPw, splits, slab.data_ptr(), s)
+    h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B,
+                 KPw, splits, slab.data_ptr(), s)
     h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp,
                    bpart.data_ptr(), nch, gp.data_ptr(), gb.data_ptr(), s)
     if with_bias:

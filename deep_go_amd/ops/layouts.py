@@ -113,23 +113,11 @@ def pick_wgrad_splits(npix: int, KPw: int, Mpad: int, num_cus: int = 256,
                       wgs_per_cu: int = 2, ktile: int = 128) -> int:
     """Split-K count for the im2col wgrad: one dispatch round of (k-tiles x m-tiles x
     splits) workgroups at ``wgs_per_cu`` resident workgroups per CU (hip().
-    conv_wgrad_wgs_per_cu(): 3 for the ring kernel, 2 for the 2-stage one)."""
+    conv_wgrad_wgs_per_cu(): 2 for the 2-stage kernel)."""
     tiles = (KPw // ktile) * (Mpad // 128)
     target = max(1, (wgs_per_cu * num_cus) // tiles)
     max_split = max(1, npix // 256)
     return max(1, min(target, max_split))
-
-
-def wgrad3_ok(k: int, cin_frame: int, pad: int) -> bool:
-    """Row-stripe wgrad (conv_wgrad3.hip): 3x3 layers on frames of 64k channels, pad 1-2."""
-    return k == 3 and cin_frame % 64 == 0 and 1 <= pad <= 2
-
-
-def pick_wgrad3_splits(batch: int, tiles: int, wgs_per_cu: int = 1, num_cus: int = 256) -> int:
-    """One dispatch round: splits x tiles <= num_cus x workgroups-per-CU, and every split
-    gets at least one 64-pixel step (6 per board).  ``tiles``/``wgs_per_cu`` come from the
-    kernel (hip().wgrad3_tiles / wgrad3_wgs_per_cu: they depend on the kernel variant)."""
-    return max(1, min(num_cus * wgs_per_cu // tiles, batch * 6))
 
 
 def board_ok(k: int, cin_frame: int) -> bool:

@@ -193,21 +193,19 @@ def test_conv_board_dgrad(B, cin, cout, k, bm, monkeypatch):
                                                  (2, 40, 128, 5, 3), (5, 256, 256, 3, None),
                                                  (1, 16, 16, 3, 1), (2, 128, 128, 1, 2),
                                                  (3, 128, 128, 3, 7), (2, 128, 256, 3, None)])
-@pytest.mark.parametrize("variant", ["ring", "plain", "t3"])
+@pytest.mark.parametrize("variant", ["plain", "t3"])
 def test_conv_wgrad(B, cin, cout, k, splits, variant):
-    """im2col wgrad: ring (32-pixel 3-stage, asm LDS-DMA), 2-stage 128x128 and three-slice
-    128x384 tiles (the t3 kernel runs where K % 384 == 0, else the 2-stage one)."""
+    """im2col wgrad: 2-stage 128x128 and three-slice 128x384 tiles (the t3 kernel runs where
+    K % 384 == 0, else the 2-stage one)."""
     torch.manual_seed(3)
     from deep_go_amd.ops import functional as Fn
     from deep_go_amd.ops.native import hip
-    hip().conv_wgrad_set_ring(1 if variant == "ring" else 0)
     hip().conv_wgrad_set_t3(1 if variant == "t3" else 0)
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
     try:
         got, gp, gb = Fn.conv_wgrad(dz, x, k, splits=splits, with_bias=True, algo="im2col")
     finally:
-        hip().conv_wgrad_set_ring(0)
         hip().conv_wgrad_set_t3(1)
     w0 = torch.zeros(cout, k, k, cin, device=DEV, requires_grad=True)
     y = conv_ref(x, w0, k)
@@ -216,31 +214,6 @@ def test_conv_wgrad(B, cin, cout, k, splits, variant):
     # fused bias grads (column sums of dZ)
     assert rel_err(gp, dz.sum(0).reshape(cout, 361).t()) < 1e-4
     assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
-
-
-@pytest.mark.parametrize("B,cin,cout,splits,algo", [
-    (3, 128, 128, None, "rows"), (3, 128, 128, None, "im2col"), (9, 128, 128, 5, "rows"),
-    (2, 64, 128, 1, "rows"), (4, 192, 64, None, "rows"), (2, 256, 256, 3, "rows"),
-    (1, 128, 128, 6, "rows")])
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_conv_wgrad_algos(B, cin, cout, splits, algo, variant):
-    """Row-stripe 3x3 wgrad (conv_wgrad3.hip, each variant) vs the im2col kernel vs the fp32
-    reference."""
-    if algo != "rows" and variant != 1:
-        pytest.skip("variant only applies to the row-stripe kernel")
-    torch.manual_seed(5)
-    from deep_go_amd.ops import functional as Fn
-    from deep_go_amd.ops.native import hip
-    hip().wgrad3_set_variant(variant)
-    try:
-        x = bf(torch.randn(B, cin, 19, 19, device=DEV))
-        dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-        got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo=algo)
-        w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
-        (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
-        assert rel_err(got, gw) < 1e-3
-    finally:
-        hip().wgrad3_set_variant(1)
 
 
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),

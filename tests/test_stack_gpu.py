@@ -1,4 +1,4 @@
-"""Board-resident layer stacks (csrc/kernels/conv_stack.hip, conv_stack2.hip) against a plain
+"""The board-resident layer stack (csrc/kernels/conv_stack2.hip) against a plain
 PyTorch fp32 oracle, layer by layer (teacher-forced: each layer's oracle input is the
 kernel's own bf16 output of the layer below, so errors do not compound).
 
@@ -32,9 +32,8 @@ def _oracle(A, x_frame, mask, epi):
     return out * bits.reshape(out.shape[0], 19, 19, C).float()
 
 
-@pytest.mark.parametrize("impl", ["v1", "v2", "v2nodb"])
 @pytest.mark.parametrize("epi", ["fwd", "dgrad"])
-def test_stack_layers_match_fp32_oracle(impl, epi):
+def test_stack_layers_match_fp32_oracle(epi):
     from deep_go_amd.ops import layouts as LY
     from deep_go_amd.ops.native import hip, stream_handle
     h = hip()
@@ -49,28 +48,23 @@ def test_stack_layers_match_fp32_oracle(impl, epi):
         ys.append(LY.alloc_frame(B, C, 1, DEV))
         ms.append(torch.randint(0, 256, (B, 361, 16), dtype=torch.uint8, device=DEV))
     pb = torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=DEV)
-    ops = [LY.stack_frag(a) for a in As] if impl != "v1" else As
+    ops = [LY.stack_frag(a) for a in As]
     tab = np.array([[ops[i].data_ptr(), pb.data_ptr() if epi == "fwd" else 0, ys[i].data_ptr(),
                      ms[i].data_ptr()] for i in range(NL)], dtype=np.int64)
     masks_in = [m.clone() for m in ms]
     e = h.EPI_FWD if epi == "fwd" else h.EPI_DGRAD
-    if impl == "v1":
-        h.conv_stack(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
-    else:
-        h.conv_stack2_set_bdb(1 if impl == "v2" else 0)
-        h.conv_stack2(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
-        h.conv_stack2_set_bdb(1)  # back to the default
+    h.conv_stack2(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
     torch.cuda.synchronize()
     xin = x
     for l in range(NL):
         ref = _oracle(As[l], xin, masks_in[l], epi)
         got = LY.frame_interior(ys[l], 1).float()
         err = ((got - ref).abs().max() / (ref.abs().max() + 1e-6)).item()
-        assert err < 1e-2, f"{impl} {epi} layer {l}: rel err {err:.3g}"
+        assert err < 1e-2, f"{epi} layer {l}: rel err {err:.3g}"
         # zero border untouched
         assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
         if epi == "fwd":  # bitmask written = nonzero of the bf16 output
             nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, 16, 8).long()
             packed = (nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8)
-            assert torch.equal(packed, ms[l]), f"{impl} fwd layer {l}: mask"
+            assert torch.equal(packed, ms[l]), f"fwd layer {l}: mask"
         xin = ys[l]

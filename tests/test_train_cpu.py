@@ -256,3 +256,20 @@ def test_cli_auto_resume_after_interruption(tmp_path, ref_data):
     _, a, sa, _ = ckm.load_checkpoint(str(tmp_path / "ref" / "ref.model"))
     _, b, sb, _ = ckm.load_checkpoint(str(ck / "ar.model"))
     assert torch.equal(a, b) and sa["iterations"] == sb["iterations"] == 9
+
+
+def test_cpu_1layer_k16_preset_trains(tmp_path, ref_data):
+    """BASELINE config 1 ("1-layer 19x19 conv k=16, batch=16 on CPU"): ONE 5x5 conv of 16
+    filters (37 -> 16, both bias kinds, ReLU) under the 3x3 head — 16 filters really shape the
+    net (parameter count below) — trained end to end on the fp32 CPU path with the real data
+    fixture: finite costs and a held-out validation pass."""
+    from deep_go_amd.train.experiment import Experiment
+    cfg = get_preset("cpu-1layer-k16", synthetic=False, data_root=ref_data,
+                     checkpoint_dir=str(tmp_path), validationSize=32, validation_interval=40,
+                     loader_threads=2, seed=5)
+    assert cfg.kernels == [5, 3] and cfg.channels == [37, 16, 1]
+    assert cfg.num_params() == (16 * 25 * 37 + 16 + 361 * 16) + (9 * 16 + 1 + 361)
+    e = Experiment(cfg, id="k16")
+    res = e.run(40)
+    assert np.isfinite(res["train_cost"]) and len(e.validation_costs) == 1
+    assert np.isfinite(e.validation_costs[0])

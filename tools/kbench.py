@@ -78,53 +78,25 @@ def main():
             res.setdefault(f"nt_{bm}x{bn}", []).append(round(timeit(nt(bm, bn)), 2))
         dz = LY.alloc_frame(B, C, 1, dev)
         LY.frame_interior(dz, 1).copy_(torch.randn(B, 19, 19, C, device=dev))
-        h.conv_wgrad_set_ring(0)
         splits = LY.pick_wgrad_splits(B * 361, KPw, 128, wgs_per_cu=2)
         slab = torch.empty(splits * 128 * KPw, device=dev)
 
         def wg():
             h.conv_wgrad(3, dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, splits,
                          slab.data_ptr(), s)
-        h.conv_wgrad_set_ring(0)
         for mode in (0, 4, 6):
             h.conv_wgrad_set_ablate(mode)
             res.setdefault(f"wgrad_ablate{mode}", []).append(round(timeit(wg), 2))
         h.conv_wgrad_set_ablate(0)
-        h.conv_wgrad_set_ring(1)
-        spr = LY.pick_wgrad_splits(B * 361, KPw, 128, wgs_per_cu=3)
-        slabr = torch.empty(spr * 128 * KPw, device=dev)
-
-        def wgr():
-            h.conv_wgrad(3, dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, spr,
-                         slabr.data_ptr(), s)
-        res.setdefault("wgrad_ring", []).append(round(timeit(wgr), 2))
-        res.setdefault("splits_ring", []).append(spr)
-        h.conv_wgrad_set_ring(0)
         res.setdefault("splits", []).append(splits)
         gw = torch.empty(C * 9 * C, device=dev)
 
         def red(sp):
             def f():
-                h.wgrad_reduce(slab3.data_ptr() if sp != splits else slab.data_ptr(),
+                h.wgrad_reduce(slab.data_ptr(),
                                gw.data_ptr(), sp, C, 128, KPw, 9, C, C, 0, 0, 0, 0, s)
             return f
-        # row-stripe wgrad (conv_wgrad3.hip), each kernel variant
-        for var in (0, 1, 2):
-            h.wgrad3_set_variant(var)
-            sp3 = LY.pick_wgrad3_splits(B, h.wgrad3_tiles(128, C), h.wgrad3_wgs_per_cu(C))
-            slab3 = torch.empty(sp3 * 128 * KPw, device=dev)
-
-            def wg3():
-                h.conv_wgrad3(dz.data_ptr(), 1, C, 128, x.data_ptr(), 1, C, B, KPw, sp3,
-                              slab3.data_ptr(), s)
-            for mode in ((0, 1, 2, 4, 8, 7, 15) if var == 1 else (0, 4)):
-                h.conv_wgrad3_set_ablate(mode)
-                res.setdefault(f"wgrad3v{var}_ablate{mode}", []).append(round(timeit(wg3), 2))
-            h.conv_wgrad3_set_ablate(0)
-            res.setdefault(f"splits3v{var}", []).append(sp3)
-        h.wgrad3_set_variant(1)
         res.setdefault("reduce_im2col_splits", []).append(round(timeit(red(splits)), 2))
-        res.setdefault("reduce_rows_splits", []).append(round(timeit(red(sp3)), 2))
     out = {k: {"us": v, "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     print(json.dumps({"B": B, "C": C, **out}, indent=1))
 
