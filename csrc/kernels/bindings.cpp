@@ -28,6 +28,15 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
+void dg_conv_stack_f8_set_mode(int m);
+hipError_t dg_conv_stack_f8(const long long* table, int nl, const void* X0, int l0,
+                            const float* scales, unsigned* amax, int B, hipStream_t stream);
+hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
+                                     const float* scales, unsigned* amax, int B, const float* w,
+                                     const float* bias, const float* posb, const int* labels,
+                                     float* loss, int* pred, void* dZ, float* gw_part,
+                                     float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream);
 hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
                           hipStream_t stream);
 hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
@@ -186,6 +195,28 @@ PYBIND11_MODULE(_dghip, m) {
                                   head_relu, grad_scale, S(stream)),
           "conv_stack2_fwd_head");
   }, "conv_stack2 forward + the fused 3x3/128 policy head");
+  // conv_stack_f8.hip: the fp8 (e4m3, MX MFMA) forward stack of the hidden 128 -> 128 layers
+  m.def("conv_stack_f8", [](uintptr_t table, int nl, uintptr_t X0, int l0, uintptr_t scales,
+                            uintptr_t amax, int B, uintptr_t stream) {
+    check(dg_conv_stack_f8(P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
+                           P<unsigned>(amax), B, S(stream)),
+          "conv_stack_f8");
+  }, "fp8 forward stack: table rows {A8_frag, pbias_frag, Y, mask}; l0 = first layer index");
+  m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int l0,
+                                     uintptr_t scales, uintptr_t amax, int B, uintptr_t w,
+                                     uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                     uintptr_t loss, uintptr_t pred, uintptr_t dZ,
+                                     uintptr_t gw_part, uintptr_t dzb, int head_relu,
+                                     float grad_scale, uintptr_t stream) {
+    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
+                                    P<unsigned>(amax), B, P<float>(w), P<float>(bias),
+                                    P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
+                                    P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
+                                    grad_scale, S(stream)),
+          "conv_stack_f8_fwd_head");
+  }, "fp8 forward stack + the fused 3x3/128 policy head");
+  m.def("conv_stack_f8_set_mode", [](int m) { dg_conv_stack_f8_set_mode(m); },
+        "conv_stack_f8 timing-ablation mode (0 = production)");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
         "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
   m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,

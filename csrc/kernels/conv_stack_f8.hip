@@ -1,0 +1,430 @@
+// FP8 forward layer stack (BASELINE config 5, the MX-fp8 MFMA path): the conv_stack2 design
+// (one workgroup owns one board for ALL hidden 3x3 128 -> 128 layers, weights streamed
+// straight into VGPRs in fragment order, no barrier inside a layer) with the resident board
+// image in OCP e4m3 and the K loop on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+// (2x the bf16 MFMA rate on gfx950):
+//   * the fp8 image is 21 x 21 frame rows of 128 B (one byte per channel, 56 KB), 16-B slot
+//     (c / 16) ^ ((x + 3y) & 7) — the bf16 stack's swizzle on the same 128-B row geometry;
+//   * a layer is 9 K-steps (one tap, K = 128 channels) of one MFMA per 16 x 16 fragment:
+//     half the K-steps of the bf16 stack for the same bytes moved per step.  A fragment
+//     (16 co x 128 k, 32 B per lane: lane group g holds k = 32g .. 32g + 31,
+//     tools/fp8_mfma_probe.hip) = two global_load_dwordx4 of the fragment-ordered e4m3
+//     weights [tap 9][wm 2][i 4][half 2][lane 64][16 B] (weight_refresh writes them);
+//     B fragment = two ds_read_b128 of the image row;
+//   * epilogue: y = relu(s_x s_w acc + bias + pos-bias), its amax folded into amax[l] (one
+//     atomic per workgroup: delayed scaling, fp8_update_scales turns it into next step's
+//     s_y), and e4m3(y / s_y) written back into the image as the next layer's input;
+//   * the bf16 activation frame and ReLU bitmask of every layer (for the bf16 backward) are
+//     copied out of the image during the next layer's first 6 K-steps, dequantized
+//     (x s_y): the backward sees exactly the activations the fp8 forward consumed;
+//   * the LAST layer writes a bf16 image instead (the conv_stack2 two-64-channel-image
+//     layout over the same 112 KB), so the fused policy head (head_body.h) runs on it as in
+//     the bf16 stack;
+//   * prologue: the bf16 input frame (conv_l1's output) is quantized into the image with
+//     its scale s_x = scales[2 (l0 - 1) + 1]; its amax goes to amax[l0 - 1].
+// Scales (device, per conv layer g): scales[2g] = s_w, scales[2g + 1] = s_y (of act[g]).
+//
+// LDS: 12 KB head scratch + 112 KB image region = 124 KB: one 8-wave workgroup per CU.
+//
+// Reference ops: nn.SpatialConvolutionMM + nn.Add + nn.ReLU per hidden layer
+// (experiments.lua:137-147).
+#include "dg_common.h"
+#include "head_body.h"
+
+using namespace dg;
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+namespace {
+
+constexpr int C = 128;
+constexpr int F = 21;
+constexpr int FF = F * F;                 // 441
+constexpr int HROWS = 448;
+constexpr int H_BYTES = HROWS * 128;      // one bf16 64-channel image (last layer)
+constexpr int T = 9;                      // K-steps per layer (taps)
+constexpr int MAXL = 24;
+constexpr int MF = 4;                     // 64 co per wave
+constexpr int NF = 6;                     // 96 px per wave
+constexpr int NW = 8;
+constexpr int NT = NW * 64;
+constexpr int SCRATCH = 12 * 1024;
+constexpr int STEP_BYTES = 2 * MF * 2 * 64 * 16;  // 16 KB per tap
+constexpr int WM_BYTES = STEP_BYTES / 2;
+constexpr int PIECES8 = NPTS * 8;                 // 16-B pieces of the fp8 image (2888)
+constexpr int CO_STEPS = (PIECES8 + NT - 1) / NT; // 6
+constexpr int UNITS16 = NPTS * 16;                // 16-B pieces of the bf16 image (5776)
+constexpr float FP8_MAX = 448.f;
+
+static_assert(dghead::scratch_bytes(C) + 64 <= SCRATCH, "head scratch");
+
+struct F8Layer {
+  const char* A8;       // fragment-ordered e4m3 weights (9 x 16 KB)
+  const bf16_t* pbias;  // bf16 bias + pos-bias in the stack's fragment order
+  char* Y;              // bf16 output frame [B][21][21][128]
+  uint8_t* mask;        // [B][361][16] ReLU bits (written)
+};
+struct F8Args {
+  const char* X0;       // bf16 input frame of the first layer
+  int nl;
+  int l0;               // global conv-layer index of the first stack layer (>= 1)
+  int fuse_head;
+  const float* scales;  // [2g] = s_w of layer g, [2g + 1] = s_y of act[g]
+  unsigned* amax;       // [g]: amax of act[g] (float bits), folded in here
+  F8Layer L[MAXL];
+  dghead::HeadMArgs head;
+};
+
+DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+
+DG_DEV void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
+  __builtin_amdgcn_s_barrier();
+}
+
+DG_DEV uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+// workgroup max of non-negative v folded into *amax (one atomic per workgroup); s_tmp: 8
+// floats of LDS; every thread calls it (contains a barrier)
+DG_DEV void wg_amax(float v, unsigned* amax, float* s_tmp) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_tmp[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = s_tmp[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, s_tmp[w]);
+    atomicMax(amax, __float_as_uint(m));
+  }
+}
+
+// MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
+// 2 = no A loads in the K loop, 4 = no copy-out
+template <int MODE>
+__global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int b = blockIdx.x;
+  char* sI = smem + SCRATCH;                       // fp8 image (or the last layer's bf16)
+  float* s_amax = (float*)(smem + SCRATCH - 64);   // 2 x 8 floats (alternating per layer)
+
+  // ---- prologue: quantize the bf16 input frame into the fp8 image ----
+  {
+    const float s_in = a.scales[2 * (a.l0 - 1) + 1];
+    const float inv = 1.f / s_in;
+    const char* Xb = a.X0 + (size_t)b * FF * C * 2;
+    float m = 0.f;
+    for (int u = tid; u < FF * 16; u += NT) {     // 8-channel pieces
+      const int f = u >> 4, q = u & 15;
+      const uint4 v = *(const uint4*)(Xb + (size_t)u * 16);
+      float x[8] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                    __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u),
+                    __uint_as_float(v.z << 16), __uint_as_float(v.z & 0xFFFF0000u),
+                    __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        m = fmaxf(m, x[e]);
+        x[e] = fminf(x[e] * inv, FP8_MAX);
+      }
+      uint2 o;
+      o.x = pack_fp8x4(x[0], x[1], x[2], x[3]);
+      o.y = pack_fp8x4(x[4], x[5], x[6], x[7]);
+      *(uint2*)(sI + f * 128 + (((q >> 1) ^ fsig(f)) * 16) + (q & 1) * 8) = o;
+    }
+    wg_amax(m, a.amax + (a.l0 - 1), s_amax + 8);  // (contains the barrier: image complete)
+  }
+
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  // per fragment: row byte offset fp*128 (16 bits) | (fs & 7) << 16
+  uint32_t pk[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    pk[j] = (uint32_t)(((h + 1) * F + (w + 1)) * 128) |
+            ((uint32_t)(((w + 1) + 3 * (h + 1)) & 7) << 16);
+  }
+  const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
+
+  // A fragments i0, i0+1 of one tap (A = the tap's 16 KB): 2 KB per fragment (two halves)
+  auto load_A = [&](const char* A, int i0, i32x8 (&r)[MF]) {
+    const char* p = A + a_lane;
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i) {
+      const i32x4 lo = *(const i32x4*)(p + (2 * i) * 1024);
+      const i32x4 hi = *(const i32x4*)(p + (2 * i + 1) * 1024);
+      r[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+  };
+  // B fragments (16 pixels x 128 channels) of tap t from the fp8 image: lane group lq reads
+  // slots 2lq, 2lq + 1 (XOR the row signature; the odd slot is the even one ^ 16 B)
+  auto read_B = [&](int t, i32x8 (&bfr)[NF]) {
+    const int toff = (t / 3 - 1) * F + (t % 3 - 1);
+    const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
+    const LDS_AS char* base = (const LDS_AS char*)sI;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int off = (int)(pk[j] & 0xFFFFu) + toff * 128 +
+                      (((2 * lq) ^ (((int)(pk[j] >> 16) + tsig) & 7)) * 16);
+      const i32x4 lo = *(const LDS_AS i32x4*)(base + off);
+      const i32x4 hi = *(const LDS_AS i32x4*)(base + (off ^ 16));
+      bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+  };
+  auto mma = [&](const i32x8 (&af)[MF], int i0, const i32x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0,
+                                                                      0, 0, 127, 0, 127);
+  };
+
+  // Copy-out of the previous layer's output (the fp8 image) as bf16 (x s_prev) + ReLU bits:
+  // thread tid handles 16-B piece u = tid + 512 s (pixel u / 8, channels 16 (u % 8) ..),
+  // read from LDS in the step before it is stored.  Pieces past the board repeat the last
+  // one (same bytes): every wave issues the same stores.
+  auto co_read = [&](int s_) -> uint4 {
+    const int u = min(tid + NT * s_, PIECES8 - 1);
+    const int p = u >> 3, q = u & 7;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    const int f = (h + 1) * F + (w + 1);
+    return *(const uint4*)(sI + f * 128 + ((q ^ fsig(f)) * 16));
+  };
+  auto co_store = [&](int s_, const uint4& v, const F8Layer& Lo, float s_prev) {
+    const int u = min(tid + NT * s_, PIECES8 - 1);
+    const int p = u >> 3, q = u & 7;
+    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+    const int f = (h + 1) * F + (w + 1);
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], false);
+      const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], true);
+      o[2 * k] = pack_bf16x2(lo[0] * s_prev, lo[1] * s_prev);
+      o[2 * k + 1] = pack_bf16x2(hi[0] * s_prev, hi[1] * s_prev);
+      // ReLU bit per channel: the byte is nonzero (post-ReLU values are >= 0)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bits |= (((wd[k] >> (8 * e)) & 0xFFu) ? 1u : 0u) << (4 * k + e);
+    }
+    char* yp = Lo.Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
+    *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
+    *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
+    *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * 16 + q * 2) = (uint16_t)bits;
+  };
+
+  i32x8 Ak[MF];
+  load_A(a.L[0].A8, 0, Ak);
+  load_A(a.L[0].A8, 2, Ak);
+
+  for (int l = 0; l < a.nl; ++l) {
+    const int g = a.l0 + l;
+    const F8Layer L = a.L[l];
+    const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
+    const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
+    const bool co_on = l > 0;
+    const bool last = l + 1 == a.nl;
+    const float s_x = a.scales[2 * (g - 1) + 1];
+    const float deq = s_x * a.scales[2 * g];
+    const float inv_y = 1.f / a.scales[2 * g + 1];
+    f32x4 acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 co_v;
+
+    // (structure of conv_stack2's K loop: rolled, sched_barrier-pinned plain loads, each
+    // half of the A fragments re-loaded right after its MFMAs, copy-out store last)
+    auto kstep = [&](const int t, const bool co) {
+      const char* An = t + 1 < T ? L.A8 + (t + 1) * STEP_BYTES : A_next;
+      i32x8 bfr[NF];
+      read_B(t, bfr);
+      mma(Ak, 0, bfr, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(MODE & 2)) load_A(An, 0, Ak);
+      if (co) co_v = co_read(t);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(Ak, 2, bfr, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(MODE & 2)) load_A(An, 2, Ak);
+      if (co) co_store(t, co_v, Lprev, s_x);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // the copy-out steps and the rest as separate loops (no per-step branch; the step index
+    // laundered so the compiler does not precompute every step's copy-out addresses)
+    int t = 0;
+    if (!(MODE & 4) && co_on) {
+#pragma unroll 1
+      for (; t < CO_STEPS; ++t) {
+        int tt = t;
+        asm volatile("" : "+s"(tt));
+        kstep(tt, true);
+      }
+    }
+#pragma unroll 1
+    for (; t < T; ++t) kstep(t, false);
+
+    // ---- epilogue ----
+    // an opaque zero added to the epilogue's addresses: otherwise the compiler hoists all
+    // per-fragment table / LDS addresses out of the layer loop and spills them
+    int z0 = 0;
+    asm volatile("" : "+v"(z0));
+    uint2 eu[NF][MF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
+#pragma unroll
+      for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+    }
+    lds_barrier();  // every wave is past its last read of this layer's image
+    char* sIe = sI + z0;
+    if (last) {
+      // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
+      // head's weight-gradient pass reads against zero dz): the region held fp8 data
+      for (int u = tid; u < 87 * 8 * 2; u += NT) {
+        const int img = u / (87 * 8), k = (u >> 3) % 87, q = u & 7;
+        const int row = k < 21 ? k : k < 42 ? 420 + (k - 21) : k < 61 ? (k - 41) * 21
+                        : k < 80 ? (k - 60) * 21 + 20 : 441 + (k - 80);
+        *(uint4*)(sIe + img * H_BYTES + row * 128 + q * 16) = uint4{0, 0, 0, 0};
+      }
+    }
+    float vmax = 0.f;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = wn * NF * 16 + j * 16 + lr;
+      const int f = (int)(pk[j] & 0xFFFFu) >> 7;
+      const int sig = (int)(pk[j] >> 16);
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        f32x4 v = acc[i][j];
+        const uint2 u = eu[j][i];
+        v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
+        v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+        v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
+        v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+        if (p >= NPTS) continue;
+        if (!last) {
+          vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+          const uint32_t q8 = pack_fp8x4(fminf(v[0] * inv_y, FP8_MAX), fminf(v[1] * inv_y, FP8_MAX),
+                                         fminf(v[2] * inv_y, FP8_MAX), fminf(v[3] * inv_y, FP8_MAX));
+          // channel co = wm*64 + i*16 + lq*4 (+0..3): slot co / 16 = wm*4 + i, byte lq*4
+          *(uint32_t*)(sIe + f * 128 + (((wm * 4 + i) ^ sig) * 16) + lq * 4) = q8;
+        } else {
+          // bf16 two-image layout (conv_stack2 / head_body.h) for the fused head
+          const int cl = i * 16 + lq * 4;
+          uint2 o;
+          o.x = pack_bf16x2(v[0], v[1]);
+          o.y = pack_bf16x2(v[2], v[3]);
+          *(uint2*)(sIe + wm * H_BYTES + f * 128 + (((cl >> 3) ^ sig) * 16) + (cl & 4) * 2) = o;
+        }
+      }
+    }
+    if (!last) wg_amax(vmax, a.amax + g, s_amax + 8 * (l & 1));  // (barrier inside)
+    lds_barrier();  // the next layer's input is complete
+  }
+  // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2
+  {
+    const F8Layer Ll = a.L[a.nl - 1];
+    const int co_q = tid & 15;
+    for (int s_ = 0; s_ < (UNITS16 + NT - 1) / NT; ++s_) {
+      const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
+      const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+      const int f = (h + 1) * F + (w + 1);
+      const uint4 v =
+          *(const uint4*)(sI + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig(f)) * 16));
+      *(uint4*)(Ll.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
+      if (Ll.mask) {
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        auto nz2 = [](uint32_t x) {
+          const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
+          const uint32_t t = __builtin_bit_cast(uint32_t, m);
+          return (t | (t >> 15)) & 3u;
+        };
+        Ll.mask[((size_t)b * NPTS + p) * 16 + co_q] =
+            (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
+      }
+    }
+  }
+  if (a.fuse_head) dghead::head_body<C>(a.head, b, sI, smem, [](int) {});
+}
+
+int g_f8_mode = 0;
+
+template <int MODE>
+hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
+  constexpr size_t lds = SCRATCH + 2 * (size_t)H_BYTES;
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<MODE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+  hipLaunchKernelGGL((conv_stack_f8_kernel<MODE>), dim3(B), dim3(NT), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t f8_launch(const long long* table, int nl, const void* X0, int l0, const float* scales,
+                     unsigned* amax, int B, const dghead::HeadMArgs* head, hipStream_t stream) {
+  if (nl <= 0 || nl > MAXL || B <= 0 || l0 < 1 || !scales || !amax) return hipErrorInvalidValue;
+  F8Args a;
+  a.X0 = (const char*)X0;
+  a.nl = nl;
+  a.l0 = l0;
+  a.scales = scales;
+  a.amax = amax;
+  a.fuse_head = head ? 1 : 0;
+  a.head = head ? *head : dghead::HeadMArgs{};
+  for (int i = 0; i < nl; ++i) {
+    a.L[i].A8 = (const char*)table[4 * i];
+    a.L[i].pbias = (const bf16_t*)table[4 * i + 1];
+    a.L[i].Y = (char*)table[4 * i + 2];
+    a.L[i].mask = (uint8_t*)table[4 * i + 3];
+    if (!a.L[i].A8 || !a.L[i].pbias || !a.L[i].Y || !a.L[i].mask) return hipErrorInvalidValue;
+  }
+  switch (g_f8_mode) {
+    case 2: return launch_f8<2>(a, B, stream);
+    case 4: return launch_f8<4>(a, B, stream);
+    case 6: return launch_f8<6>(a, B, stream);
+    default: return launch_f8<0>(a, B, stream);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
+
+// table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask} (int64)
+hipError_t dg_conv_stack_f8(const long long* table, int nl, const void* X0, int l0,
+                            const float* scales, unsigned* amax, int B, hipStream_t stream) {
+  return f8_launch(table, nl, X0, l0, scales, amax, B, nullptr, stream);
+}
+
+hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
+                                     const float* scales, unsigned* amax, int B, const float* w,
+                                     const float* bias, const float* posb, const int* labels,
+                                     float* loss, int* pred, void* dZ, float* gw_part,
+                                     float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream) {
+  const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
+                            gw_part, dzb, head_relu, grad_scale};
+  return f8_launch(table, nl, X0, l0, scales, amax, B, &h, stream);
+}
+
+}  // extern "C"

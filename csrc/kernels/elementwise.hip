@@ -245,6 +245,8 @@ struct WRefreshLayer {
                        // order (cout == 128): [24 px frags][2 co halves][4][64 lanes] x 4 bf16
   uint4* wf_frag;      // conv_stack2 A operands (3x3, 128 -> 128 only), MFMA fragment order:
   uint4* wd_frag;      //   [step 18][wm 2][kk 2][i 4][lane 64] x 8 bf16 (forward / dgrad)
+  uint4* wf8_frag;     // conv_stack_f8 A operands (e4m3, quantized with s_w like wf8):
+                       //   [tap 9][wm 2][i 4][half 2][lane 64] x 16 B (requires wf8)
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -292,7 +294,7 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       }
       tileS[rr][cc] = v;
     }
-    if (L.wd || L.wf_frag) __syncthreads();
+    if (L.wd || L.wf_frag || L.wf8_frag) __syncthreads();
     if (L.wd) {
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
@@ -319,6 +321,27 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
         L.wf_frag[((size_t)(cit * 9 + t) * 2 + cot) * 512 + u] = uint4{f[0], f[1], f[2], f[3]};
         L.wd_frag[((size_t)(cot * 9 + (8 - t)) * 2 + cit) * 512 + u] = uint4{d[0], d[1], d[2], d[3]};
       }
+    }
+    if (L.wf8_frag) {
+      // this tile = rows co of co-half wm = cot, k = ci of lane groups 2 cit, 2 cit + 1 at tap
+      // t: unit (i, half, lane group, row) = 16 e4m3 bytes ci = 32 lq + 16 half + e
+      const int u = threadIdx.x;  // 256 units, one per thread
+      const int lr = u & 15, lql = (u >> 4) & 1, hf = (u >> 5) & 1, i = u >> 6;
+      const int r = i * 16 + lr, c0 = 32 * lql + 16 * hf;
+      uint32_t q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v4[k] = fmaxf(fminf(tileS[r][c0 + 4 * e + k] * inv8, 448.f), -448.f);
+        int pkd = __builtin_amdgcn_cvt_pk_fp8_f32(v4[0], v4[1], 0, false);
+        pkd = __builtin_amdgcn_cvt_pk_fp8_f32(v4[2], v4[3], pkd, true);
+        q[e] = (uint32_t)pkd;
+      }
+      const int lane = (2 * cit + lql) * 16 + lr;
+      L.wf8_frag[((((size_t)t * 2 + cot) * 4 + i) * 2 + hf) * 64 + lane] =
+          uint4{q[0], q[1], q[2], q[3]};
     }
     __syncthreads();
   }
@@ -434,9 +457,10 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
   return hipGetLastError();
 }
 
-// layers: n entries of 18 int64 words
+// layers: n entries of 19 int64 words
 //   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, pbias_frag, wf8, s_w, amax_w, bias, posb,
-//    pbias, wf_frag, wd_frag}  (pbias_frag / *_frag: stack-order tables, 128 -> 128 only, or 0)
+//    pbias, wf_frag, wd_frag, wf8_frag}  (pbias_frag / *_frag: stack-order tables,
+//    128 -> 128 only, or 0)
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -445,7 +469,7 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 18 * i;
+    const long long* t = table + 19 * i;
     a.L[i].w = (const float*)t[0];
     a.L[i].wf = (bf16_t*)t[1];
     a.L[i].wd = (bf16_t*)t[2];
@@ -466,6 +490,8 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].wf_frag = (uint4*)t[16];
     a.L[i].wd_frag = (uint4*)t[17];
     if ((a.L[i].wf_frag != nullptr) != (a.L[i].wd_frag != nullptr)) return hipErrorInvalidValue;
+    a.L[i].wf8_frag = (uint4*)t[18];
+    if (a.L[i].wf8_frag && (!a.L[i].wf8 || !a.L[i].wf_frag)) return hipErrorInvalidValue;
     if (a.L[i].wf_frag && (a.L[i].cout != 128 || a.L[i].cin != 128 || a.L[i].taps != 9))
       return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);

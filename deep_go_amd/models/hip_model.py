@@ -139,13 +139,18 @@ class HipGoNet:
         self.head = L[-1]
         # conv_stack2 (csrc/kernels/conv_stack2.hip): fragment-ordered forward / dgrad operands
         # of every hidden 3x3 128 -> 128 layer, written by weight_refresh beside wf / wd
+        # (+ conv_stack_f8.hip's e4m3 forward operands of the fp8 layers)
         self.wfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wdfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        self.wf8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         for p in self.plans:
             if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
                 self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
                                                   device=dev)
                 self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
+                if p.fp8:
+                    self.wf8frag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.uint8,
+                                                        device=dev)
 
         # ---- activation / gradient frames ----
         B = batch
@@ -171,11 +176,11 @@ class HipGoNet:
         # and ReLU bitmasks of the board-kernel outputs consumed by a board dgrad
         self.pbias = [torch.zeros((NUM_POINTS, p.cout), dtype=torch.bfloat16, device=dev)
                       if p.board and not p.fp8 else None for p in self.plans]
-        # the same table in the forward stack's accumulator-fragment order (coalesced
-        # epilogue loads), for every 128-channel board layer
+        # the same table in the forward stacks' accumulator-fragment order (coalesced
+        # epilogue loads), for every 128-channel board layer (bf16 or fp8)
         self.pbias_frag = [torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=dev)
-                           if pb is not None and p.cout == 128 else None
-                           for p, pb in zip(self.plans, self.pbias)]
+                           if (pb is not None and p.cout == 128) or self.wfrag[p.index] is not None
+                           else None for p, pb in zip(self.plans, self.pbias)]
         self.relu_mask = [None] * len(self.plans)
         for p in self.plans[:-1]:
             nxt = self.plans[p.index + 1]
@@ -255,7 +260,8 @@ class HipGoNet:
                          self.params.data_ptr() + 4 * spec.b_off,
                          self.params.data_ptr() + 4 * spec.pos_off,
                          self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0,
-                         _ptr(self.wfrag[p.index]), _ptr(self.wdfrag[p.index])])
+                         _ptr(self.wfrag[p.index]), _ptr(self.wdfrag[p.index]),
+                         _ptr(self.wf8frag[p.index])])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
     def _build_plans(self):
@@ -265,6 +271,7 @@ class HipGoNet:
         f4 = 4
         self._pre: List[Tuple[Callable, tuple]] = []
         self._fwd: List[Tuple[Callable, tuple]] = []
+        self._fwd_owner: List[int] = []   # layer each forward launch belongs to
         self._bwd: List[List[Tuple[Callable, tuple]]] = []  # per layer (index order)
         self._pre.append((h.expand_features, (
             self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
@@ -275,6 +282,7 @@ class HipGoNet:
             x_pad = spec.pad
             y_pad = lay.layers[p.index + 1].pad
             nxt = self.plans[p.index + 1] if p.index + 1 < len(self.plans) else None
+            self._fwd_owner.append(p.index)
             if p.fp8:
                 i = p.index
                 S = self.fp8_scales.data_ptr()
@@ -312,8 +320,10 @@ class HipGoNet:
                                                  P + spec.b_off * f4, P + spec.pos_off * f4, 0,
                                                  0, msk.data_ptr() if msk is not None else 0)))
             if nxt is not None and nxt.fp8 and not p.fp8:
-                # bf16 producer feeding an fp8 layer: quantize its output frame
+                # bf16 producer feeding an fp8 layer: quantize its output frame (owned by the
+                # consumer: a fused fp8 stack quantizes its own input)
                 i = p.index
+                self._fwd_owner.append(i + 1)
                 self._fwd.append((h.frame_to_fp8, (
                     self.act[i].data_ptr(), self.x8[i + 1].data_ptr(), self.act[i].numel(),
                     self.fp8_scales.data_ptr() + (2 * i + 1) * 4,
@@ -351,9 +361,15 @@ class HipGoNet:
                 P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
                 self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
                 self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
-            self._fwd_train = [fused if f is h.conv_stack2_fwd else (f, a)
+            if self.stack_fp8:
+                fused = (h.conv_stack_f8_fwd_head, (
+                    self._stack_table.ctypes.data, len(self.stack),
+                    self.act[first - 1].data_ptr(), first, self.fp8_scales.data_ptr(),
+                    self.fp8_amax.data_ptr(), self.B) + fused[1][5:])
+            self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8) else (f, a)
                                for f, a in self._fwd]
-            if any(f is h.conv_stack2_fwd_head for f, _ in self._fwd_train):
+            if any(f in (h.conv_stack2_fwd_head, h.conv_stack_f8_fwd_head)
+                   for f, _ in self._fwd_train):
                 self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -397,14 +413,17 @@ class HipGoNet:
         bf16 layers by ONE conv_stack2_fwd launch (board-resident activations, overlapped
         stores; csrc/kernels/conv_stack2.hip).  DG_STACK=0 keeps per-layer kernels."""
         self.stack = []
+        self.stack_fp8 = False
         if os.environ.get("DG_STACK", "1") == "0":
             return
         L = self.layout.layers
+        fp8 = self.fp8
 
         def ok(p):
-            return (p.index > 0 and p.board and not p.fp8 and p.k == 3 and p.cinp == 128
+            return (p.index > 0 and p.board and p.fp8 == fp8 and p.k == 3 and p.cinp == 128
                     and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1
-                    and self.wfrag[p.index] is not None)
+                    and self.wfrag[p.index] is not None
+                    and (not fp8 or self.wf8frag[p.index] is not None))
         best, cur = [], []
         for p in self.plans:
             cur = cur + [p.index] if ok(p) else []
@@ -416,18 +435,38 @@ class HipGoNet:
         rows = []
         for i in best:
             m = self.relu_mask[i]
-            rows.append([self.wfrag[i].data_ptr(), self.pbias_frag[i].data_ptr(),
+            if fp8 and m is None:
+                # the fp8 stack always writes ReLU bits (its dgrad consumer may read them)
+                m = self.relu_mask[i] = torch.zeros((self.B, NUM_POINTS, 16), dtype=torch.uint8,
+                                                    device=self.device)
+            A = self.wf8frag[i] if fp8 else self.wfrag[i]
+            rows.append([A.data_ptr(), self.pbias_frag[i].data_ptr(),
                          self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
         self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
-        op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(best),
-                                      self.act[first - 1].data_ptr(), self.plans[first].KP,
-                                      self.B))
-        if len(self._fwd) != len(self.plans):  # fp8 quantize ops interleaved: keep per-layer
-            self.stack = []
-            return
-        # self._fwd holds exactly one launch per plan here
-        self._fwd = self._fwd[:first] + [op] + self._fwd[best[-1] + 1:]
+        if fp8:
+            # fp8 forward stack (conv_stack_f8.hip): quantizes its bf16 input frame itself
+            # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out
+            op = (self.h.conv_stack_f8, (self._stack_table.ctypes.data, len(best),
+                                         self.act[first - 1].data_ptr(), first,
+                                         self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr(),
+                                         self.B))
+            self.stack_fp8 = True
+        else:
+            op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(best),
+                                          self.act[first - 1].data_ptr(), self.plans[first].KP,
+                                          self.B))
+        # every launch owned by a stack layer goes; the stack launch takes the first's place
+        members = set(best)
+        keep, placed = [], False
+        for fop, owner in zip(self._fwd, self._fwd_owner):
+            if owner in members:
+                if not placed:
+                    keep.append(op)
+                    placed = True
+            else:
+                keep.append(fop)
+        self._fwd = keep
 
     def _fuse_dgrad_stack(self):
         """Run the backward-data chain of the longest run of hidden 128->128 3x3 layers as

@@ -76,6 +76,16 @@ def stack_frag(A: torch.Tensor) -> torch.Tensor:
     return a.permute(4, 3, 0, 5, 1, 6, 2, 7).reshape(-1).contiguous()
 
 
+def stack_frag_f8(w8: torch.Tensor) -> torch.Tensor:
+    """conv_stack_f8 A-operand order of e4m3 forward weights ``w8`` [128 co][9 taps][128 ci]
+    (uint8 bytes): flat [tap 9][wm 2][i 4][half 2][lane 64][e 16] with co = wm*64 + i*16 +
+    (lane & 15), ci = 32*(lane >> 4) + 16*half + e (the MX-MFMA lane group g holds
+    k = 32g .. 32g + 31)."""
+    assert tuple(w8.shape) == (128, 9, 128)
+    a = w8.reshape(2, 4, 16, 9, 4, 2, 16)               # wm i lr | tap | lq half e
+    return a.permute(3, 0, 1, 5, 4, 2, 6).reshape(-1).contiguous()
+
+
 def conv_dims(k: int, cin_frame: int, cout: int, bm: int):
     """K/M padding for a conv whose input frame has ``cin_frame`` channels."""
     ngroups = k * k * cin_frame // 8

@@ -182,3 +182,18 @@ def test_stack_frag_layout_indexing():
         col = tap * 128 + chunk * 64 + kk * 32 + (lane >> 4) * 8 + e
         idx = ((((s * 2 + wm) * 2 + kk) * 4 + i) * 64 + lane) * 8 + e
         assert f[idx].item() == A[row, col].item()
+
+
+def test_stack_frag_f8_layout_indexing():
+    """layouts.stack_frag_f8 puts byte w8[co][tap][ci] where conv_stack_f8 loads it."""
+    import torch
+    from deep_go_amd.ops import layouts as LY
+    w = torch.arange(128 * 9 * 128, dtype=torch.int64).reshape(128, 9, 128)
+    f = LY.stack_frag_f8(w)
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        t, wm, i, half, lane, e = (int(rng.integers(n)) for n in (9, 2, 4, 2, 64, 16))
+        co = wm * 64 + i * 16 + (lane & 15)
+        ci = 32 * (lane >> 4) + 16 * half + e
+        idx = ((((t * 2 + wm) * 4 + i) * 2 + half) * 64 + lane) * 16 + e
+        assert f[idx].item() == w[co, t, ci].item()

@@ -68,3 +68,69 @@ def test_stack_layers_match_fp32_oracle(epi):
             packed = (nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8)
             assert torch.equal(packed, ms[l]), f"fwd layer {l}: mask"
         xin = ys[l]
+
+
+def _q8(x):
+    """e4m3 (OCP, RNE) rounding of x (|x| <= 448) as float32."""
+    return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+
+
+@pytest.mark.parametrize("nl", [2, 4])
+def test_fp8_stack_matches_emulated_oracle(nl):
+    """conv_stack_f8 (e4m3 image + weights, MX MFMA) vs a PyTorch fp32 oracle that applies the
+    same quantization: layer l's input = e4m3(Y_{l-1} / s_x) (teacher-forced on the kernel's
+    own dequantized bf16 output, which re-quantizes to the exact fp8 bytes), weights =
+    e4m3(W / s_w), y = relu(s_x s_w acc + bias); non-last layers output bf16(e4m3(y / s_y) s_y),
+    the last layer bf16(y).  Also: ReLU bits = nonzero outputs, amax of every quantized
+    activation folded in, zero borders."""
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    torch.manual_seed(11)
+    B, l0 = 5, 1
+    x = LY.alloc_frame(B, C, 1, DEV)
+    LY.frame_interior(x, 1).copy_(torch.randn(B, 19, 19, C, device=DEV).relu())
+    # scales[2g] = s_w of layer g, scales[2g + 1] = s_y of act[g]
+    scales = torch.empty(2 * (l0 + nl), device=DEV)
+    scales[2 * (l0 - 1) + 1] = x.float().abs().max() / 448.0
+    W8, ys, ms, pbs = [], [], [], []
+    for l in range(nl):
+        g = l0 + l
+        w = torch.randn(C, 9, C, device=DEV) / (3 * C ** 0.5)
+        s_w = w.abs().max() / 448.0
+        scales[2 * g] = s_w
+        scales[2 * g + 1] = 0.05 + 0.02 * l            # arbitrary output scales
+        W8.append((w / s_w).clamp(-448, 448).to(torch.float8_e4m3fn))
+        ys.append(LY.alloc_frame(B, C, 1, DEV))
+        ms.append(torch.zeros(B, 361, 16, dtype=torch.uint8, device=DEV))
+        pbs.append(torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=DEV))
+    frags = [LY.stack_frag_f8(w8.view(torch.uint8)) for w8 in W8]
+    amax = torch.zeros(l0 + nl, dtype=torch.int32, device=DEV)
+    tab = np.array([[frags[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr()]
+                    for i in range(nl)], dtype=np.int64)
+    h.conv_stack_f8(tab.ctypes.data, nl, x.data_ptr(), l0, scales.data_ptr(), amax.data_ptr(), B,
+                    stream_handle())
+    torch.cuda.synchronize()
+    amax_f = amax.view(torch.float32)
+    assert abs(amax_f[l0 - 1].item() - x.float().max().item()) < 1e-6
+    xin = x
+    for l in range(nl):
+        g = l0 + l
+        s_x, s_w, s_y = scales[2 * (g - 1) + 1], scales[2 * g], scales[2 * g + 1]
+        xq = _q8(LY.frame_interior(xin, 1).float() / s_x).permute(0, 3, 1, 2)
+        wq = W8[l].float().reshape(C, 3, 3, C).permute(0, 3, 1, 2)
+        v = (F.conv2d(xq, wq, padding=1) * (s_x * s_w)).relu().permute(0, 2, 3, 1)
+        got = LY.frame_interior(ys[l], 1).float()
+        last = l == nl - 1
+        ref = v if last else _q8(v / s_y) * s_y
+        err = ((got - ref).abs().max() / (ref.abs().max() + 1e-6)).item()
+        # accumulation-order differences may move a value across an e4m3 rounding boundary
+        # (one e4m3 step = 1/8 .. 1/16 relative); the bulk must match to bf16 rounding
+        close = ((got - ref).abs() <= 1e-2 * ref.abs() + 1e-6).float().mean().item()
+        assert err < (1e-2 if last else 0.07) and close > 0.995, (l, err, close)
+        if not last:
+            assert abs(amax_f[g].item() - v.max().item()) <= 1e-3 * v.max().item()
+        nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, 16, 8).long()
+        assert torch.equal((nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8), ms[l])
+        assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
+        xin = ys[l]

@@ -1,0 +1,46 @@
+"""Timeline of ONE training step from a rocprofv3 --kernel-trace CSV of bench.py in hipGraph
+mode: every kernel of the second-to-last complete step (steps delimited by
+expand_features launches) with its start offset, duration and queue, plus the busy time
+of the union of all kernels (so side-stream overlap is visible).
+Usage: python tools/step_timeline.py TRACE.csv"""
+import csv
+import re
+import sys
+
+
+def short(s):
+    s = s.replace("(anonymous namespace)::", "").replace("void ", "")
+    m = re.match(r"([\w:]+(<[^>]*>)?)", s)
+    return (m.group(1) if m else s)[:58]
+
+
+def main(path):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "expand_features" in r["Kernel_Name"]]
+    a, b = starts[-3], starts[-2]
+    seg = rows[a:b]
+    t0 = int(seg[0]["Start_Timestamp"])
+    wall = (int(rows[b]["Start_Timestamp"]) - t0) / 1e3
+    print(f"step wall {wall:.1f} us, {len(seg)} kernels")
+    print(f"{'start':>8s} {'dur':>7s} {'q':>2s}  kernel")
+    iv = []
+    for r in seg:
+        s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
+        iv.append((s, e))
+        print(f"{s / 1e3:8.1f} {(e - s) / 1e3:7.1f} {r['Queue_Id']:>2s}  {short(r['Kernel_Name'])}")
+    iv.sort()
+    busy, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    print(f"GPU busy (union of kernels) {busy / 1e3:.1f} us = {100 * busy / 1e3 / wall:.1f}% of "
+          f"the step; idle {wall - busy / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
