@@ -54,12 +54,15 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic batches")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--bucket-mb", type=float, default=3.0,
-                    help="DP gradient bucket size (3 MB: head + one 5-layer wgrad group)")
+    ap.add_argument("--bucket-mb", type=float, default=6.0,
+                    help="DP gradient bucket size (6 MB: head + the grouped hidden layers in "
+                         "one bucket, fired beside the first layer's gradient chain; the first "
+                         "layer in a second one)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch"],
+    ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
-                         "torch = torch.distributed between graph segments")
+                         "torch = torch.distributed between graph segments, proxy = world-1 "
+                         "stand-in kernel on the comm stream (overlap measurement)")
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="after the timed run, N extra steps with roctx ranges (load / segments"
                          " / allreduce / optimizer) and a host phase breakdown; run under "

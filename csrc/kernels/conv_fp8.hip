@@ -226,7 +226,8 @@ conv_board_fp8_kernel(Fp8Args a) {
 
 // Per step, BEFORE the weight refresh: s_w[l] from the weight amax the previous refresh
 // observed (delayed weight scaling, 5% headroom: SGD moves weights slowly; values past it
-// saturate at +-448), s_y[l] from the activation amax of the last forward; both reset.
+// saturate at +-448), s_y[l] from the activation amax of the last forward (rounded up to a
+// power of two); both reset.
 // scales[2l] = s_w, scales[2l+1] = s_y; amax_w / amax_y: float bits.
 __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
                                          float w_margin) {
@@ -235,7 +236,9 @@ __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w,
   const float mw = __uint_as_float(amax_w[l]);
   if (mw > 0.f) scales[2 * l] = mw * w_margin / FP8_MAX;
   const float my = __uint_as_float(amax_y[l]);
-  if (my > 0.f) scales[2 * l + 1] = my / FP8_MAX;
+  // activation scales are powers of two (the smallest with amax / s <= 448): e4m3 <-> bf16
+  // conversions then scale exactly (conv_stack_f8's v_cvt_scalef32_pk_bf16_fp8 copy-out)
+  if (my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(my / FP8_MAX)));
   amax_w[l] = 0u;
   amax_y[l] = 0u;
 }

@@ -105,7 +105,8 @@ DG_DEV void wg_amax(float v, unsigned* amax, float* s_tmp) {
 }
 
 // MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out
+// 2 = no A loads in the K loop, 4 = no copy-out (copy-out store first in the step measured
+// 196 vs 187 us for 10 layers: removed)
 template <int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -212,13 +213,18 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], false);
-      const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], true);
-      o[2 * k] = pack_bf16x2(lo[0] * s_prev, lo[1] * s_prev);
-      o[2 * k + 1] = pack_bf16x2(hi[0] * s_prev, hi[1] * s_prev);
-      // ReLU bit per channel: the byte is nonzero (post-ReLU values are >= 0)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bits |= (((wd[k] >> (8 * e)) & 0xFFu) ? 1u : 0u) << (4 * k + e);
+      // 2 e4m3 -> 2 bf16 scaled by s_prev in one v_cvt_scalef32_pk_bf16_fp8 (s_prev is a
+      // power of two: fp8_update_scales rounds every activation scale up to one)
+      o[2 * k] = __builtin_bit_cast(uint32_t,
+                                    __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, false));
+      o[2 * k + 1] = __builtin_bit_cast(uint32_t,
+                                        __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, true));
+      // ReLU bit per channel = byte nonzero (post-ReLU values are >= 0): OR-fold each byte
+      // into its bit 0, then gather bits 0, 8, 16, 24 into bits 21..24 with one multiply
+      uint32_t t = wd[k] | (wd[k] >> 4);
+      t |= t >> 2;
+      t = (t | (t >> 1)) & 0x01010101u;
+      bits |= ((t * 0x204081u) >> 21 & 0xFu) << (4 * k);
     }
     char* yp = Lo.Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
     *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};

@@ -54,7 +54,7 @@ class ExperimentConfig:
     head_relu: bool = True         # reference applies ReLU to the head (parity)
     optimizer: str = "sgd"         # sgd | rmsprop (the reference's misnamed AdagradOptimizer)
     rmsprop_decay: float = 0.9
-    bucket_mb: float = 3.0         # DP gradient bucket size (12x128: head + 5 layers per bucket)
+    bucket_mb: float = 6.0         # DP gradient bucket size (12x128: head + hidden layers | layer 0)
     grad_dtype: str = "fp32"       # all-reduce dtype: fp32 | bf16
     reference_validation_quirks: bool = False  # train.lua:23-44 floor/off-by-one
     sampling: str = "game"         # game (reference, data.lua:29-37) | position

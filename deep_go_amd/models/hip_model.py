@@ -561,15 +561,16 @@ class HipGoNet:
         splits, so each layer is cut into ~5x fewer splits: ~5x fewer fp32 partial slabs
         to write and reduce (50 -> 10 MB per 128-channel layer).
 
-        Default group size: 5 under data parallelism (a DP bucket fires at a group's top
-        layer, so two groups let the first all-reduce overlap the second group), and all
-        hidden layers in one launch on a single GPU (12x128: 245k -> 248k boards/s,
-        gpurun_out/ab.txt sweep of 4/5/7/10)."""
+        Default group size: all hidden layers in one launch (12x128: 245k -> 248k boards/s
+        vs groups of 4/5/7/10), under data parallelism too.  Round 1 used groups of 5 under
+        DP so the first bucket's all-reduce could overlap the second group; round 2 measured
+        that a comm-stream kernel does NOT co-schedule with these full-machine launches
+        (every CU's VGPR file is full: bench.py --force-dp --comm proxy, 0% overlap,
+        profiles/r2_comm_overlap_proxy.txt), so the split only costs."""
         self.wgroups: List[List[int]] = []
         self.win_groups = set()
         self._l0_side_at = None
-        G = int(os.environ.get("DG_WGRAD_GROUP",
-                               "5" if self.global_batch != self.B else "16"))
+        G = int(os.environ.get("DG_WGRAD_GROUP", "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
         if G < 2 or self.side_mode not in ("none", "bias"):
             return

@@ -200,6 +200,35 @@ class NativeComm:
         self.c.destroy()
 
 
+class ProxyComm:
+    """World-1 stand-in for an in-graph collective (``bench.py --force-dp --comm proxy``):
+    ``all_reduce_`` launches a bandwidth-bound elementwise kernel (read + write the bucket,
+    x *= 1) on the comm stream, where the RCCL all-reduce kernel would run.  Its kernel trace
+    shows whether comm-stream kernels co-schedule with the step's full-machine compute kernels
+    (tools/overlap_report.py).  Not a collective: world must be 1."""
+    kind = "proxy"
+    in_graph = True
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.world, self.rank = 1, 0
+        self.stream = torch.cuda.Stream(device=self.device)
+
+    def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
+        with torch.cuda.stream(stream if stream is not None else self.stream):
+            t.mul_(1.0)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0):
+        return t
+
+    def async_error(self) -> str:
+        return ""
+
+    def close(self):
+        pass
+
+
 def make_communicator(kind: str, device):
     """``native`` | ``torch`` | ``auto``.  ``auto`` takes the native in-graph communicator and
     falls back to torch.distributed if the native module is missing or its self-test (a
@@ -207,6 +236,10 @@ def make_communicator(kind: str, device):
     ``comm.kind`` (bench JSON "comm")."""
     if kind == "torch":
         return TorchComm()
+    if kind == "proxy":
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            raise ValueError("the proxy communicator is world-1 only")
+        return ProxyComm(device)
     try:
         c = NativeComm(device)
         if kind == "auto":

@@ -49,6 +49,20 @@ def main():
         return f
     abl = [2, 4, 6, 10, 14] if "--ablate" in sys.argv else []
     out = {}
+    # the fp8 forward stack (conv_stack_f8) on the same shapes: e4m3 weights / image
+    w8 = [LY.stack_frag_f8(torch.randint(0, 0x78, (C, 9, C), dtype=torch.uint8, device=dev))
+          for _ in range(NL)]
+    scales = torch.full((2 * (NL + 1),), 0.01, device=dev)
+    amax = torch.zeros(NL + 1, dtype=torch.int32, device=dev)
+    t8 = np.array([[w8[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr()]
+                   for i in range(NL)], dtype=np.int64)
+
+    def run8(mode=0, nl=NL):
+        def f():
+            h.conv_stack_f8_set_mode(mode)
+            h.conv_stack_f8(t8.ctypes.data, nl, x.data_ptr(), 1, scales.data_ptr(),
+                            amax.data_ptr(), B, s)
+        return f
     flops = 2.0 * C * C * 9 * 361 * B * NL
     times = {}
     for _ in range(3):
@@ -56,7 +70,13 @@ def main():
             times.setdefault(name, []).append(round(timeit(run(name)), 1))
         for m in abl:
             times.setdefault(f"fwd_mode{m}", []).append(round(timeit(run("fwd", m)), 1))
+        times.setdefault("fp8_fwd", []).append(round(timeit(run8()), 1))
+        times.setdefault("fp8_fwd_1layer", []).append(round(timeit(run8(nl=1)), 1))
+        times.setdefault("fp8_fwd_2layers", []).append(round(timeit(run8(nl=2)), 1))
+        for m in ([2, 4, 6] if abl else []):
+            times.setdefault(f"fp8_fwd_mode{m}", []).append(round(timeit(run8(m)), 1))
     h.conv_stack2_set_mode(0)
+    h.conv_stack_f8_set_mode(0)
     for k, v in times.items():
         out[k] = {"us": v, "us_per_layer": round(min(v) / NL, 2),
                   "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)}
