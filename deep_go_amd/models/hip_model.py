@@ -197,6 +197,9 @@ class HipGoNet:
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
+        # saturation events per layer ([2l] weights, [2l + 1] activations): a step whose
+        # observed amax exceeded 448 x the scale in use (values were clamped)
+        self.fp8_sat = torch.zeros(2 * len(self.plans), dtype=torch.int32, device=dev)
         self._fp8_calibrated = not self.fp8
         # backward side stream ("bias", the default): the HBM-bound bias-grad partials run on
         # it beside the MFMA-bound weight-gradient launch of the same layers, and the first
@@ -811,7 +814,7 @@ class HipGoNet:
         if self.fp8:
             self.h.fp8_update_scales(len(self.plans), self.fp8_scales.data_ptr(),
                                      self.fp8_amax_w.data_ptr(), self.fp8_amax.data_ptr(), 1.05,
-                                     s)
+                                     self.fp8_sat.data_ptr(), s)
 
     def calibrate_fp8(self):
         """Forwards on the current inputs to observe activation ranges, then derive the
@@ -821,6 +824,7 @@ class HipGoNet:
             self.evaluate()
             self._fp8_update(s)
             self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table), s)
+        self.fp8_sat.zero_()   # the calibration passes start from unit scales
         self._fp8_calibrated = True
 
     def train_step(self):
