@@ -29,7 +29,7 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
 void dg_conv_stack_f8_set_mode(int m);
-hipError_t dg_conv_stack_f8(const long long* table, int nl, const void* X0, int l0,
+hipError_t dg_conv_stack_f8(int C, const long long* table, int nl, const void* X0, int l0,
                             const float* scales, unsigned* amax, int B, hipStream_t stream);
 hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
                                      const float* scales, unsigned* amax, int B, const float* w,
@@ -196,12 +196,13 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_stack2_fwd_head");
   }, "conv_stack2 forward + the fused 3x3/128 policy head");
   // conv_stack_f8.hip: the fp8 (e4m3, MX MFMA) forward stack of the hidden 128 -> 128 layers
-  m.def("conv_stack_f8", [](uintptr_t table, int nl, uintptr_t X0, int l0, uintptr_t scales,
-                            uintptr_t amax, int B, uintptr_t stream) {
-    check(dg_conv_stack_f8(P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
+  m.def("conv_stack_f8", [](int C, uintptr_t table, int nl, uintptr_t X0, int l0,
+                            uintptr_t scales, uintptr_t amax, int B, uintptr_t stream) {
+    check(dg_conv_stack_f8(C, P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
                            P<unsigned>(amax), B, S(stream)),
           "conv_stack_f8");
-  }, "fp8 forward stack: table rows {A8_frag, pbias_frag, Y, mask}; l0 = first layer index");
+  }, "fp8 forward stack (C = 128 | 256): table rows {A8_frag, pbias_frag, Y, mask}; l0 = first "
+     "layer index");
   m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int l0,
                                      uintptr_t scales, uintptr_t amax, int B, uintptr_t w,
                                      uintptr_t bias, uintptr_t posb, uintptr_t labels,

@@ -1,5 +1,5 @@
 // FP8 forward layer stack (BASELINE config 5, the MX-fp8 MFMA path): the conv_stack2 design
-// (one workgroup owns one board for ALL hidden 3x3 128 -> 128 layers, weights streamed
+// (one workgroup owns one board for ALL hidden 3x3 C -> C layers, weights streamed
 // straight into VGPRs in fragment order, no barrier inside a layer) with the resident board
 // image in OCP e4m3 and the K loop on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
 // (2x the bf16 MFMA rate on gfx950):
@@ -24,7 +24,16 @@
 //     its scale s_x = scales[2 (l0 - 1) + 1]; its amax goes to amax[l0 - 1].
 // Scales (device, per conv layer g): scales[2g] = s_w, scales[2g + 1] = s_y (of act[g]).
 //
-// LDS: 12 KB head scratch + 112 KB image region = 124 KB: one 8-wave workgroup per CU.
+// C = 256 (config 5's d = 256): the e4m3 image is 441 rows of 256 B (113 KB, slot swizzle
+// ((x + 3y) & 15)) — resident where a bf16 one (226 KB) cannot be.  The 256 output channels
+// run as two passes of 128 (96 accumulator registers per lane each); pass 0's e4m3 output
+// is parked in the LDS left over (around the image) until pass 1 has read the whole input,
+// then both halves go into the image.  A K-step is one (tap, 128-channel chunk) pair: 18 per
+// pass.  The last layer's bf16 output goes straight to HBM from the epilogue (no bf16
+// image fits): the head runs as its own launch (head_mfma<256>).
+//
+// LDS: 12 KB head scratch + 112 KB image region = 124 KB (C = 128); 160 KB (C = 256):
+// one 8-wave workgroup per CU.
 //
 // Reference ops: nn.SpatialConvolutionMM + nn.Add + nn.ReLU per hidden layer
 // (experiments.lua:137-147).
@@ -38,45 +47,64 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 namespace {
 
-constexpr int C = 128;
 constexpr int F = 21;
 constexpr int FF = F * F;                 // 441
 constexpr int HROWS = 448;
-constexpr int H_BYTES = HROWS * 128;      // one bf16 64-channel image (last layer)
-constexpr int T = 9;                      // K-steps per layer (taps)
+constexpr int H_BYTES = HROWS * 128;      // one bf16 64-channel image (C = 128 last layer)
+constexpr int T = 9;                      // taps
 constexpr int MAXL = 24;
 constexpr int MF = 4;                     // 64 co per wave
 constexpr int NF = 6;                     // 96 px per wave
 constexpr int NW = 8;
 constexpr int NT = NW * 64;
 constexpr int SCRATCH = 12 * 1024;
-constexpr int STEP_BYTES = 2 * MF * 2 * 64 * 16;  // 16 KB per tap
+constexpr int STEP_BYTES = 2 * MF * 2 * 64 * 16;  // 16 KB per (tap, chunk) K-step
 constexpr int WM_BYTES = STEP_BYTES / 2;
-constexpr int PIECES8 = NPTS * 8;                 // 16-B pieces of the fp8 image (2888)
-constexpr int CO_STEPS = (PIECES8 + NT - 1) / NT; // 6
-constexpr int UNITS16 = NPTS * 16;                // 16-B pieces of the bf16 image (5776)
 constexpr float FP8_MAX = 448.f;
 
-static_assert(dghead::scratch_bytes(C) + 64 <= SCRATCH, "head scratch");
+static_assert(dghead::scratch_bytes(128) + 64 <= SCRATCH, "head scratch");
+
+// per-channel-count geometry
+template <int C>
+struct Geo {
+  static constexpr int NC = C / 128;              // 128-channel chunks = output passes
+  static constexpr int ROWB = C;                  // image row bytes (e4m3)
+  static constexpr int SLOTS = C / 16;            // 16-B slots per row
+  static constexpr int SIGM = SLOTS - 1;          // swizzle mask
+  static constexpr int STEPS = T * NC;            // K-steps per pass
+  static constexpr int PIECES = NPTS * SLOTS;     // copy-out pieces
+  static constexpr int CO_STEPS = (PIECES + NT - 1) / NT;   // 6 | 12
+  static constexpr int IMG = FF * ROWB;           // image bytes
+  static constexpr int PARK1 = SCRATCH / 128;     // C = 256: pass-0 pixels parked in [0, 12K)
+  static constexpr int LDS = C == 128 ? SCRATCH + 2 * H_BYTES : 160 * 1024;
+  static constexpr int AMAX_OFF = C == 128 ? SCRATCH - 64 : SCRATCH + IMG + (NPTS - PARK1) * 128;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(C == 128 || AMAX_OFF + 64 <= LDS, "park area");
+};
 
 struct F8Layer {
-  const char* A8;       // fragment-ordered e4m3 weights (9 x 16 KB)
-  const bf16_t* pbias;  // bf16 bias + pos-bias in the stack's fragment order
-  char* Y;              // bf16 output frame [B][21][21][128]
-  uint8_t* mask;        // [B][361][16] ReLU bits (written)
+  const char* A8;       // fragment-ordered e4m3 weights (9 x 16 KB x (C/128)^2)
+  const bf16_t* pbias;  // bf16 bias + pos-bias in the stack's fragment order (per pass)
+  char* Y;              // bf16 output frame [B][21][21][C]
+  uint8_t* mask;        // [B][361][C/8] ReLU bits (written)
 };
 struct F8Args {
   const char* X0;       // bf16 input frame of the first layer
   int nl;
   int l0;               // global conv-layer index of the first stack layer (>= 1)
-  int fuse_head;
+  int fuse_head;        // C = 128 only
   const float* scales;  // [2g] = s_w of layer g, [2g + 1] = s_y of act[g]
   unsigned* amax;       // [g]: amax of act[g] (float bits), folded in here
   F8Layer L[MAXL];
   dghead::HeadMArgs head;
 };
 
-DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+// swizzle signature of frame row f: (x + 3y) & mask — distinct for any 16 raster-consecutive
+// pixels (also across a board-row wrap), so 16 lanes reading one slot of 16 pixel rows hit
+// 16 different 16-B bank groups
+template <int C>
+DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & Geo<C>::SIGM; }
+DG_DEV int fsig8(int f) { return ((f % F) + 3 * (f / F)) & 7; }
 
 DG_DEV void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
@@ -104,28 +132,37 @@ DG_DEV void wg_amax(float v, unsigned* amax, float* s_tmp) {
   }
 }
 
+// 4 e4m3 bytes -> 4 bf16 (scaled by the power of two s) + their 4 ReLU bits
+DG_DEV uint32_t nzbits4(uint32_t w) {
+  uint32_t t = w | (w >> 4);
+  t |= t >> 2;
+  t = (t | (t >> 1)) & 0x01010101u;
+  return (t * 0x204081u) >> 21 & 0xFu;   // bits 0, 8, 16, 24 gathered into 21..24
+}
+
 // MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out (copy-out store first in the step measured
-// 196 vs 187 us for 10 layers: removed)
-template <int MODE>
+// 2 = no A loads in the K loop, 4 = no copy-out
+template <int C, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
+  using G = Geo<C>;
+  constexpr int NC = G::NC;
+  constexpr int ROWB = G::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int b = blockIdx.x;
-  char* sI = smem + SCRATCH;                       // fp8 image (or the last layer's bf16)
-  float* s_amax = (float*)(smem + SCRATCH - 64);   // 2 x 8 floats (alternating per layer)
+  char* sI = smem + SCRATCH;                       // e4m3 image (C = 128 last layer: bf16)
+  float* s_amax = (float*)(smem + G::AMAX_OFF);    // 2 x 8 floats (alternating per layer)
 
-  // ---- prologue: quantize the bf16 input frame into the fp8 image ----
+  // ---- prologue: quantize the bf16 input frame into the e4m3 image ----
   {
-    const float s_in = a.scales[2 * (a.l0 - 1) + 1];
-    const float inv = 1.f / s_in;
+    const float inv = 1.f / a.scales[2 * (a.l0 - 1) + 1];
     const char* Xb = a.X0 + (size_t)b * FF * C * 2;
     float m = 0.f;
-    for (int u = tid; u < FF * 16; u += NT) {     // 8-channel pieces
-      const int f = u >> 4, q = u & 15;
+    for (int u = tid; u < FF * (C / 8); u += NT) {     // 8-channel pieces
+      const int f = u / (C / 8), q = u % (C / 8);
       const uint4 v = *(const uint4*)(Xb + (size_t)u * 16);
       float x[8] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
                     __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u),
@@ -139,26 +176,26 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       uint2 o;
       o.x = pack_fp8x4(x[0], x[1], x[2], x[3]);
       o.y = pack_fp8x4(x[4], x[5], x[6], x[7]);
-      *(uint2*)(sI + f * 128 + (((q >> 1) ^ fsig(f)) * 16) + (q & 1) * 8) = o;
+      *(uint2*)(sI + f * ROWB + (((q >> 1) ^ fsig<C>(f)) * 16) + (q & 1) * 8) = o;
     }
     wg_amax(m, a.amax + (a.l0 - 1), s_amax + 8);  // (contains the barrier: image complete)
   }
 
   const int lr = lane & 15;
   const int lq = lane >> 4;
-  // per fragment: row byte offset fp*128 (16 bits) | (fs & 7) << 16
+  // per fragment: row byte offset f*ROWB (20 bits) | sig << 20
   uint32_t pk[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     int p = wn * NF * 16 + j * 16 + lr;
     if (p >= NPTS) p = 0;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
-    pk[j] = (uint32_t)(((h + 1) * F + (w + 1)) * 128) |
-            ((uint32_t)(((w + 1) + 3 * (h + 1)) & 7) << 16);
+    const int f = (h + 1) * F + (w + 1);
+    pk[j] = (uint32_t)(f * ROWB) | ((uint32_t)fsig<C>(f) << 20);
   }
   const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
 
-  // A fragments i0, i0+1 of one tap (A = the tap's 16 KB): 2 KB per fragment (two halves)
+  // A fragments i0, i0+1 of one K-step (A = the step's 16 KB): 2 KB per fragment
   auto load_A = [&](const char* A, int i0, i32x8 (&r)[MF]) {
     const char* p = A + a_lane;
 #pragma unroll
@@ -168,16 +205,18 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       r[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     }
   };
-  // B fragments (16 pixels x 128 channels) of tap t from the fp8 image: lane group lq reads
-  // slots 2lq, 2lq + 1 (XOR the row signature; the odd slot is the even one ^ 16 B)
-  auto read_B = [&](int t, i32x8 (&bfr)[NF]) {
+  // B fragments (16 pixels x 128 channels of chunk c) of K-step st = t * NC + c (the weight
+  // layout's [tap][chunk] order): lane group lq reads slots 8c + 2lq, 8c + 2lq + 1 (XOR the
+  // row signature; the odd slot = even ^ 16 B)
+  auto read_B = [&](int st, i32x8 (&bfr)[NF]) {
+    const int t = st / NC, c = st - (st / NC) * NC;
     const int toff = (t / 3 - 1) * F + (t % 3 - 1);
     const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
     const LDS_AS char* base = (const LDS_AS char*)sI;
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-      const int off = (int)(pk[j] & 0xFFFFu) + toff * 128 +
-                      (((2 * lq) ^ (((int)(pk[j] >> 16) + tsig) & 7)) * 16);
+      const int off = (int)(pk[j] & 0xFFFFFu) + toff * ROWB +
+                      (((8 * c + 2 * lq) ^ (((int)(pk[j] >> 20) + tsig) & G::SIGM)) * 16);
       const i32x4 lo = *(const LDS_AS i32x4*)(base + off);
       const i32x4 hi = *(const LDS_AS i32x4*)(base + (off ^ 16));
       bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -192,20 +231,20 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
                                                                       0, 0, 127, 0, 127);
   };
 
-  // Copy-out of the previous layer's output (the fp8 image) as bf16 (x s_prev) + ReLU bits:
-  // thread tid handles 16-B piece u = tid + 512 s (pixel u / 8, channels 16 (u % 8) ..),
+  // Copy-out of the previous layer's output (the e4m3 image) as bf16 (x s_prev) + ReLU bits:
+  // thread tid handles 16-B piece u = tid + 512 s (pixel u / SLOTS, channels 16 (u % SLOTS)),
   // read from LDS in the step before it is stored.  Pieces past the board repeat the last
   // one (same bytes): every wave issues the same stores.
   auto co_read = [&](int s_) -> uint4 {
-    const int u = min(tid + NT * s_, PIECES8 - 1);
-    const int p = u >> 3, q = u & 7;
+    const int u = min(tid + NT * s_, G::PIECES - 1);
+    const int p = u / G::SLOTS, q = u % G::SLOTS;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    return *(const uint4*)(sI + f * 128 + ((q ^ fsig(f)) * 16));
+    return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
   };
   auto co_store = [&](int s_, const uint4& v, const F8Layer& Lo, float s_prev) {
-    const int u = min(tid + NT * s_, PIECES8 - 1);
-    const int p = u >> 3, q = u & 7;
+    const int u = min(tid + NT * s_, G::PIECES - 1);
+    const int p = u / G::SLOTS, q = u % G::SLOTS;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
@@ -215,21 +254,16 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     for (int k = 0; k < 4; ++k) {
       // 2 e4m3 -> 2 bf16 scaled by s_prev in one v_cvt_scalef32_pk_bf16_fp8 (s_prev is a
       // power of two: fp8_update_scales rounds every activation scale up to one)
-      o[2 * k] = __builtin_bit_cast(uint32_t,
-                                    __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, false));
-      o[2 * k + 1] = __builtin_bit_cast(uint32_t,
-                                        __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, true));
-      // ReLU bit per channel = byte nonzero (post-ReLU values are >= 0): OR-fold each byte
-      // into its bit 0, then gather bits 0, 8, 16, 24 into bits 21..24 with one multiply
-      uint32_t t = wd[k] | (wd[k] >> 4);
-      t |= t >> 2;
-      t = (t | (t >> 1)) & 0x01010101u;
-      bits |= ((t * 0x204081u) >> 21 & 0xFu) << (4 * k);
+      o[2 * k] = __builtin_bit_cast(
+          uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, false));
+      o[2 * k + 1] = __builtin_bit_cast(
+          uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, true));
+      bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
     }
     char* yp = Lo.Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
     *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
     *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
-    *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * 16 + q * 2) = (uint16_t)bits;
+    *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
   };
 
   i32x8 Ak[MF];
@@ -246,147 +280,204 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const float s_x = a.scales[2 * (g - 1) + 1];
     const float deq = s_x * a.scales[2 * g];
     const float inv_y = 1.f / a.scales[2 * g + 1];
-    f32x4 acc[MF][NF];
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float vmax = 0.f;
     uint4 co_v;
 
-    // (structure of conv_stack2's K loop: rolled, sched_barrier-pinned plain loads, each
-    // half of the A fragments re-loaded right after its MFMAs, copy-out store last)
-    auto kstep = [&](const int t, const bool co) {
-      const char* An = t + 1 < T ? L.A8 + (t + 1) * STEP_BYTES : A_next;
-      i32x8 bfr[NF];
-      read_B(t, bfr);
-      mma(Ak, 0, bfr, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(MODE & 2)) load_A(An, 0, Ak);
-      if (co) co_v = co_read(t);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(Ak, 2, bfr, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(MODE & 2)) load_A(An, 2, Ak);
-      if (co) co_store(t, co_v, Lprev, s_x);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // the copy-out steps and the rest as separate loops (no per-step branch; the step index
-    // laundered so the compiler does not precompute every step's copy-out addresses)
-    int t = 0;
-    if (!(MODE & 4) && co_on) {
-#pragma unroll 1
-      for (; t < CO_STEPS; ++t) {
-        int tt = t;
-        asm volatile("" : "+s"(tt));
-        kstep(tt, true);
-      }
-    }
-#pragma unroll 1
-    for (; t < T; ++t) kstep(t, false);
+    for (int hp = 0; hp < NC; ++hp) {     // output pass: channels 128 hp .. 128 hp + 127
+      const char* Ap = L.A8 + (size_t)hp * G::STEPS * STEP_BYTES;
+      // the A fragments to prefetch after this pass's last step: the next pass / layer
+      const char* A_after = hp + 1 < NC ? Ap + G::STEPS * STEP_BYTES : A_next;
+      f32x4 acc[MF][NF];
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ---- epilogue ----
-    // an opaque zero added to the epilogue's addresses: otherwise the compiler hoists all
-    // per-fragment table / LDS addresses out of the layer loop and spills them
-    int z0 = 0;
-    asm volatile("" : "+v"(z0));
-    uint2 eu[NF][MF];
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
-#pragma unroll
-      for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
-    }
-    lds_barrier();  // every wave is past its last read of this layer's image
-    char* sIe = sI + z0;
-    if (last) {
-      // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
-      // head's weight-gradient pass reads against zero dz): the region held fp8 data
-      for (int u = tid; u < 87 * 8 * 2; u += NT) {
-        const int img = u / (87 * 8), k = (u >> 3) % 87, q = u & 7;
-        const int row = k < 21 ? k : k < 42 ? 420 + (k - 21) : k < 61 ? (k - 41) * 21
-                        : k < 80 ? (k - 60) * 21 + 20 : 441 + (k - 80);
-        *(uint4*)(sIe + img * H_BYTES + row * 128 + q * 16) = uint4{0, 0, 0, 0};
+      // (structure of conv_stack2's K loop: rolled, sched_barrier-pinned plain loads, each
+      // half of the A fragments re-loaded right after its MFMAs, copy-out store last)
+      auto kstep = [&](const int st, const int cs, const bool co) {
+        const char* An = st + 1 < G::STEPS ? Ap + (st + 1) * STEP_BYTES : A_after;
+        i32x8 bfr[NF];
+        read_B(st, bfr);
+        mma(Ak, 0, bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(MODE & 2)) load_A(An, 0, Ak);
+        if (co) co_v = co_read(cs);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(Ak, 2, bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(MODE & 2)) load_A(An, 2, Ak);
+        if (co) co_store(cs, co_v, Lprev, s_x);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      // the copy-out steps (the first CO_STEPS of pass 0) and the rest as separate loops
+      // (no per-step branch; the step index laundered so the compiler does not precompute
+      // every step's copy-out addresses)
+      int st = 0;
+      if (!(MODE & 4) && co_on && hp == 0) {
+#pragma unroll 1
+        for (; st < G::CO_STEPS; ++st) {
+          int tt = st;
+          asm volatile("" : "+s"(tt));
+          kstep(tt, tt, true);
+        }
       }
-    }
-    float vmax = 0.f;
+#pragma unroll 1
+      for (; st < G::STEPS; ++st) kstep(st, 0, false);
+
+      // ---- pass epilogue ----
+      // an opaque zero added to the epilogue's addresses: otherwise the compiler hoists all
+      // per-fragment table / LDS addresses out of the layer loop and spills them
+      int z0 = 0;
+      asm volatile("" : "+v"(z0));
+      uint2 eu[NF][MF];
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int p = wn * NF * 16 + j * 16 + lr;
-      const int f = (int)(pk[j] & 0xFFFFu) >> 7;
-      const int sig = (int)(pk[j] >> 16);
+      for (int j = 0; j < NF; ++j) {
+        const uint2* pf = (const uint2*)L.pbias + hp * (24 * 2 * 4 * 64) +
+                          ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
 #pragma unroll
-      for (int i = 0; i < MF; ++i) {
-        f32x4 v = acc[i][j];
-        const uint2 u = eu[j][i];
-        v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
-        v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
-        v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
-        v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
-        if (p >= NPTS) continue;
-        if (!last) {
-          vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-          const uint32_t q8 = pack_fp8x4(fminf(v[0] * inv_y, FP8_MAX), fminf(v[1] * inv_y, FP8_MAX),
-                                         fminf(v[2] * inv_y, FP8_MAX), fminf(v[3] * inv_y, FP8_MAX));
-          // channel co = wm*64 + i*16 + lq*4 (+0..3): slot co / 16 = wm*4 + i, byte lq*4
-          *(uint32_t*)(sIe + f * 128 + (((wm * 4 + i) ^ sig) * 16) + lq * 4) = q8;
-        } else {
-          // bf16 two-image layout (conv_stack2 / head_body.h) for the fused head
-          const int cl = i * 16 + lq * 4;
-          uint2 o;
-          o.x = pack_bf16x2(v[0], v[1]);
-          o.y = pack_bf16x2(v[2], v[3]);
-          *(uint2*)(sIe + wm * H_BYTES + f * 128 + (((cl >> 3) ^ sig) * 16) + (cl & 4) * 2) = o;
+        for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+      }
+      // C = 128 and the last pass of C = 256: every wave is past its last read of the
+      // image before it is overwritten (pass 0 of C = 256 only writes the park area)
+      const bool to_image = !last && hp == NC - 1;
+      if (C == 128 || hp == NC - 1) lds_barrier();
+      char* sIe = smem + SCRATCH + z0;
+      if (C == 128 && last) {
+        // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
+        // head's weight-gradient pass reads against zero dz): the region held e4m3 data
+        for (int u = tid; u < 87 * 8 * 2; u += NT) {
+          const int img = u / (87 * 8), k = (u >> 3) % 87, q = u & 7;
+          const int row = k < 21 ? k : k < 42 ? 420 + (k - 21) : k < 61 ? (k - 41) * 21
+                          : k < 80 ? (k - 60) * 21 + 20 : 441 + (k - 80);
+          *(uint4*)(sIe + img * H_BYTES + row * 128 + q * 16) = uint4{0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int p = wn * NF * 16 + j * 16 + lr;
+        const int f = (int)(pk[j] & 0xFFFFFu) / ROWB;
+        const int sig = (int)(pk[j] >> 20);
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          f32x4 v = acc[i][j];
+          const uint2 u = eu[j][i];
+          v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
+          v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+          v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
+          v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+          if (p >= NPTS) continue;
+          const int cl = wm * 64 + i * 16 + lq * 4;      // channel within the pass (0..127)
+          if (!last) {
+            vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+            const uint32_t q8 = pack_fp8x4(fminf(v[0] * inv_y, FP8_MAX), fminf(v[1] * inv_y, FP8_MAX),
+                                           fminf(v[2] * inv_y, FP8_MAX), fminf(v[3] * inv_y, FP8_MAX));
+            if (to_image) {
+              // channel co = 128 hp + cl: slot co / 16 (XOR sig), byte co % 16
+              const int co = 128 * hp + cl;
+              *(uint32_t*)(sIe + f * ROWB + (((co >> 4) ^ sig) * 16) + (co & 15)) = q8;
+            } else {
+              // C = 256 pass 0: park (pixel-major 128-B rows) in the LDS around the image
+              char* pr = p < G::PARK1 ? smem + p * 128
+                                      : smem + SCRATCH + G::IMG + (p - G::PARK1) * 128;
+              *(uint32_t*)(pr + z0 + cl) = q8;
+            }
+          } else if constexpr (C == 128) {
+            // bf16 two-image layout (conv_stack2 / head_body.h) for the fused head
+            const int cw = i * 16 + lq * 4;
+            uint2 o;
+            o.x = pack_bf16x2(v[0], v[1]);
+            o.y = pack_bf16x2(v[2], v[3]);
+            *(uint2*)(sIe + wm * H_BYTES + f * 128 + (((cw >> 3) ^ fsig8(f)) * 16) + (cw & 4) * 2) = o;
+          } else {
+            // C = 256 last layer: bf16 straight to the output frame (+ ReLU bits)
+            const int co = 128 * hp + cl;
+            uint2 o;
+            o.x = pack_bf16x2(v[0], v[1]);
+            o.y = pack_bf16x2(v[2], v[3]);
+            *(uint2*)(L.Y + ((size_t)(b * FF + f) * C + co) * 2) = o;
+            const uint32_t nib = (v[0] > 0.f ? 1u : 0u) | (v[1] > 0.f ? 2u : 0u) |
+                                 (v[2] > 0.f ? 4u : 0u) | (v[3] > 0.f ? 8u : 0u);
+            // 4 bits of one mask byte: the lane pair (lq even, odd) shares the byte
+            const uint32_t other = __shfl_xor(nib, 16, 64);
+            if ((lq & 1) == 0)
+              L.mask[((size_t)b * NPTS + p) * (C / 8) + (co >> 3)] = (uint8_t)(nib | (other << 4));
+          }
+        }
+      }
+      if (C == 256 && to_image) {
+        // pass 0's parked half into the image (every wave is past the barrier above, and
+        // every parked write precedes it in this wave... all waves: barrier first)
+        lds_barrier();
+        for (int u = tid; u < NPTS * 8; u += NT) {     // 16-B pieces of channels 0..127
+          const int p = u >> 3, q = u & 7;
+          const char* pr = p < G::PARK1 ? smem + p * 128
+                                        : smem + SCRATCH + G::IMG + (p - G::PARK1) * 128;
+          const uint4 v = *(const uint4*)(pr + z0 + q * 16);
+          const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+          const int f = (h + 1) * F + (w + 1);
+          *(uint4*)(sIe + f * ROWB + ((q ^ fsig<C>(f)) * 16)) = v;
         }
       }
     }
     if (!last) wg_amax(vmax, a.amax + g, s_amax + 8 * (l & 1));  // (barrier inside)
     lds_barrier();  // the next layer's input is complete
   }
-  // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2
-  {
+  if constexpr (C == 128) {
+    // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2
     const F8Layer Ll = a.L[a.nl - 1];
     const int co_q = tid & 15;
-    for (int s_ = 0; s_ < (UNITS16 + NT - 1) / NT; ++s_) {
+    for (int s_ = 0; s_ < (NPTS * 16 + NT - 1) / NT; ++s_) {
       const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
       const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
       const int f = (h + 1) * F + (w + 1);
       const uint4 v =
-          *(const uint4*)(sI + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig(f)) * 16));
+          *(const uint4*)(sI + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig8(f)) * 16));
       *(uint4*)(Ll.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
-      if (Ll.mask) {
-        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-        auto nz2 = [](uint32_t x) {
-          const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
-          const uint32_t t = __builtin_bit_cast(uint32_t, m);
-          return (t | (t >> 15)) & 3u;
-        };
-        Ll.mask[((size_t)b * NPTS + p) * 16 + co_q] =
-            (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
-      }
+      typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+      auto nz2 = [](uint32_t x) {
+        const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
+        const uint32_t t = __builtin_bit_cast(uint32_t, m);
+        return (t | (t >> 15)) & 3u;
+      };
+      Ll.mask[((size_t)b * NPTS + p) * 16 + co_q] =
+          (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
     }
+    if (a.fuse_head) dghead::head_body<C>(a.head, b, sI, smem, [](int) {});
   }
-  if (a.fuse_head) dghead::head_body<C>(a.head, b, sI, smem, [](int) {});
 }
 
 int g_f8_mode = 0;
 
-template <int MODE>
+template <int C, int MODE>
 hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
-  constexpr size_t lds = SCRATCH + 2 * (size_t)H_BYTES;
-  static_assert(lds <= 160 * 1024, "LDS");
+  constexpr size_t lds = Geo<C>::LDS;
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<MODE>,
+    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<C, MODE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack_f8_kernel<MODE>), dim3(B), dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((conv_stack_f8_kernel<C, MODE>), dim3(B), dim3(NT), lds, stream, a);
   return hipGetLastError();
 }
 
-hipError_t f8_launch(const long long* table, int nl, const void* X0, int l0, const float* scales,
-                     unsigned* amax, int B, const dghead::HeadMArgs* head, hipStream_t stream) {
+template <int C>
+hipError_t launch_mode(const F8Args& a, int B, hipStream_t stream) {
+  switch (g_f8_mode) {
+    case 2: return launch_f8<C, 2>(a, B, stream);
+    case 4: return launch_f8<C, 4>(a, B, stream);
+    case 6: return launch_f8<C, 6>(a, B, stream);
+    default: return launch_f8<C, 0>(a, B, stream);
+  }
+}
+
+hipError_t f8_launch(int C, const long long* table, int nl, const void* X0, int l0,
+                     const float* scales, unsigned* amax, int B, const dghead::HeadMArgs* head,
+                     hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || B <= 0 || l0 < 1 || !scales || !amax) return hipErrorInvalidValue;
+  if (C != 128 && C != 256) return hipErrorInvalidValue;
+  if (head && C != 128) return hipErrorInvalidValue;
   F8Args a;
   a.X0 = (const char*)X0;
   a.nl = nl;
@@ -402,12 +493,7 @@ hipError_t f8_launch(const long long* table, int nl, const void* X0, int l0, con
     a.L[i].mask = (uint8_t*)table[4 * i + 3];
     if (!a.L[i].A8 || !a.L[i].pbias || !a.L[i].Y || !a.L[i].mask) return hipErrorInvalidValue;
   }
-  switch (g_f8_mode) {
-    case 2: return launch_f8<2>(a, B, stream);
-    case 4: return launch_f8<4>(a, B, stream);
-    case 6: return launch_f8<6>(a, B, stream);
-    default: return launch_f8<0>(a, B, stream);
-  }
+  return C == 128 ? launch_mode<128>(a, B, stream) : launch_mode<256>(a, B, stream);
 }
 
 }  // namespace
@@ -417,9 +503,9 @@ extern "C" {
 void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 
 // table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask} (int64)
-hipError_t dg_conv_stack_f8(const long long* table, int nl, const void* X0, int l0,
+hipError_t dg_conv_stack_f8(int C, const long long* table, int nl, const void* X0, int l0,
                             const float* scales, unsigned* amax, int B, hipStream_t stream) {
-  return f8_launch(table, nl, X0, l0, scales, amax, B, nullptr, stream);
+  return f8_launch(C, table, nl, X0, l0, scales, amax, B, nullptr, stream);
 }
 
 hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
@@ -430,7 +516,7 @@ hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void*
                                      hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return f8_launch(table, nl, X0, l0, scales, amax, B, &h, stream);
+  return f8_launch(128, table, nl, X0, l0, scales, amax, B, &h, stream);
 }
 
 }  // extern "C"

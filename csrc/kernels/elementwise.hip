@@ -323,8 +323,10 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       }
     }
     if (L.wf8_frag) {
-      // this tile = rows co of co-half wm = cot, k = ci of lane groups 2 cit, 2 cit + 1 at tap
-      // t: unit (i, half, lane group, row) = 16 e4m3 bytes ci = 32 lq + 16 half + e
+      // this tile = rows co of output pass h = cot / 2, co-half wm = cot % 2; k = ci of
+      // 128-channel chunk c = cit / 2, lane groups 2 (cit % 2), +1; at tap t.  Layout
+      // [h][t][c][wm 2][i 4][half 2][lane 64] x 16 B (C = 128: h = c = 0); unit (i, half,
+      // lane group, row) = 16 e4m3 bytes ci = 32 lq + 16 half + e
       const int u = threadIdx.x;  // 256 units, one per thread
       const int lr = u & 15, lql = (u >> 4) & 1, hf = (u >> 5) & 1, i = u >> 6;
       const int r = i * 16 + lr, c0 = 32 * lql + 16 * hf;
@@ -339,8 +341,9 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
         pkd = __builtin_amdgcn_cvt_pk_fp8_f32(v4[2], v4[3], pkd, true);
         q[e] = (uint32_t)pkd;
       }
-      const int lane = (2 * cit + lql) * 16 + lr;
-      L.wf8_frag[((((size_t)t * 2 + cot) * 4 + i) * 2 + hf) * 64 + lane] =
+      const int nc = L.cout / 128, h = cot >> 1, wm = cot & 1, c = cit >> 1;
+      const int lane = (2 * (cit & 1) + lql) * 16 + lr;
+      L.wf8_frag[((((((size_t)h * 9 + t) * nc + c) * 2 + wm) * 4 + i) * 2 + hf) * 64 + lane] =
           uint4{q[0], q[1], q[2], q[3]};
     }
     __syncthreads();
@@ -352,14 +355,17 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       L.pbias[e] = f2bf(L.bias[e % L.cout] + L.posb[e]);
   }
   if (L.pbias_frag) {
-    // element e = ((jg * 2 + wm) * 4 + i) * 64 + lane: pixel jg*16 + (lane & 15), channels
-    // wm*64 + i*16 + (lane >> 4)*4 .. +3 — one coalesced 512-B load per epilogue fragment
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < 24 * 2 * 4 * 64; e += gridDim.x * 256) {
-      const int lane = e & 63, i = (e >> 6) & 3, wm = (e >> 8) & 1, jg = e >> 9;
+    // element e = (((h * 24 + jg) * 2 + wm) * 4 + i) * 64 + lane: pixel jg*16 + (lane & 15),
+    // channels 128h + wm*64 + i*16 + (lane >> 4)*4 .. +3 (h: output pass of 128 channels)
+    // — one coalesced 512-B load per epilogue fragment
+    const int ne = (L.cout / 128) * 24 * 2 * 4 * 64;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < ne; e += gridDim.x * 256) {
+      const int lane = e & 63, i = (e >> 6) & 3, wm = (e >> 8) & 1, jg = (e >> 9) % 24,
+                h = e / (24 * 512);
       int p = jg * 16 + (lane & 15);
       p = p < NPTS ? p : NPTS - 1;
-      const int c = wm * 64 + i * 16 + (lane >> 4) * 4;
-      const float* pb = L.posb + (size_t)p * 128 + c;
+      const int c = 128 * h + wm * 64 + i * 16 + (lane >> 4) * 4;
+      const float* pb = L.posb + (size_t)p * L.cout + c;
       L.pbias_frag[e] = uint2{pack_bf16x2(L.bias[c] + pb[0], L.bias[c + 1] + pb[1]),
                               pack_bf16x2(L.bias[c + 2] + pb[2], L.bias[c + 3] + pb[3])};
     }
@@ -486,12 +492,14 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].posb = (const float*)t[14];
     a.L[i].pbias = (bf16_t*)t[15];
     a.L[i].pbias_frag = (uint2*)t[9];
-    if (a.L[i].pbias_frag && a.L[i].cout != 128) return hipErrorInvalidValue;
+    if (a.L[i].pbias_frag && a.L[i].cout != 128 && a.L[i].cout != 256) return hipErrorInvalidValue;
     a.L[i].wf_frag = (uint4*)t[16];
     a.L[i].wd_frag = (uint4*)t[17];
     if ((a.L[i].wf_frag != nullptr) != (a.L[i].wd_frag != nullptr)) return hipErrorInvalidValue;
     a.L[i].wf8_frag = (uint4*)t[18];
-    if (a.L[i].wf8_frag && (!a.L[i].wf8 || !a.L[i].wf_frag)) return hipErrorInvalidValue;
+    if (a.L[i].wf8_frag && (!a.L[i].wf8 || a.L[i].taps != 9 || a.L[i].cout != a.L[i].cin ||
+                            (a.L[i].cout != 128 && a.L[i].cout != 256)))
+      return hipErrorInvalidValue;
     if (a.L[i].wf_frag && (a.L[i].cout != 128 || a.L[i].cin != 128 || a.L[i].taps != 9))
       return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);

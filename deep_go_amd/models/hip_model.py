@@ -148,9 +148,10 @@ class HipGoNet:
                 self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
                                                   device=dev)
                 self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
-                if p.fp8:
-                    self.wf8frag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.uint8,
-                                                        device=dev)
+            if (p.fp8 and p.index > 0 and p.k == 3 and p.cin == p.cout == p.cinp
+                    and p.cout in (128, 256)):
+                self.wf8frag[p.index] = torch.zeros(p.cout * 9 * p.cin, dtype=torch.uint8,
+                                                    device=dev)
 
         # ---- activation / gradient frames ----
         B = batch
@@ -178,8 +179,10 @@ class HipGoNet:
                       if p.board and not p.fp8 else None for p in self.plans]
         # the same table in the forward stacks' accumulator-fragment order (coalesced
         # epilogue loads), for every 128-channel board layer (bf16 or fp8)
-        self.pbias_frag = [torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=dev)
-                           if (pb is not None and p.cout == 128) or self.wfrag[p.index] is not None
+        self.pbias_frag = [torch.zeros((p.cout // 128) * 24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16,
+                                       device=dev)
+                           if ((pb is not None and p.cout == 128) or self.wfrag[p.index] is not None
+                               or self.wf8frag[p.index] is not None)
                            else None for p, pb in zip(self.plans, self.pbias)]
         self.relu_mask = [None] * len(self.plans)
         for p in self.plans[:-1]:
@@ -423,13 +426,15 @@ class HipGoNet:
         fp8 = self.fp8
 
         def ok(p):
-            return (p.index > 0 and p.board and p.fp8 == fp8 and p.k == 3 and p.cinp == 128
-                    and p.cout == 128 and L[p.index].pad == 1 and L[p.index + 1].pad == 1
-                    and self.wfrag[p.index] is not None
-                    and (not fp8 or self.wf8frag[p.index] is not None))
+            if not (p.index > 0 and p.board and p.fp8 == fp8 and p.k == 3
+                    and L[p.index].pad == 1 and L[p.index + 1].pad == 1):
+                return False
+            # bf16: 128 channels (conv_stack2); fp8: 128 or 256 (conv_stack_f8)
+            return self.wf8frag[p.index] is not None if fp8 else self.wfrag[p.index] is not None
         best, cur = [], []
         for p in self.plans:
-            cur = cur + [p.index] if ok(p) else []
+            cur = cur + [p.index] if ok(p) and (not cur or
+                                                 self.plans[cur[0]].cout == p.cout) else []
             if len(cur) > len(best):
                 best = list(cur)
         if len(best) < 2:
@@ -440,8 +445,8 @@ class HipGoNet:
             m = self.relu_mask[i]
             if fp8 and m is None:
                 # the fp8 stack always writes ReLU bits (its dgrad consumer may read them)
-                m = self.relu_mask[i] = torch.zeros((self.B, NUM_POINTS, 16), dtype=torch.uint8,
-                                                    device=self.device)
+                m = self.relu_mask[i] = torch.zeros((self.B, NUM_POINTS, self.plans[i].cout // 8),
+                                                    dtype=torch.uint8, device=self.device)
             A = self.wf8frag[i] if fp8 else self.wfrag[i]
             rows.append([A.data_ptr(), self.pbias_frag[i].data_ptr(),
                          self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
@@ -450,8 +455,8 @@ class HipGoNet:
         if fp8:
             # fp8 forward stack (conv_stack_f8.hip): quantizes its bf16 input frame itself
             # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out
-            op = (self.h.conv_stack_f8, (self._stack_table.ctypes.data, len(best),
-                                         self.act[first - 1].data_ptr(), first,
+            op = (self.h.conv_stack_f8, (self.plans[first].cout, self._stack_table.ctypes.data,
+                                         len(best), self.act[first - 1].data_ptr(), first,
                                          self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr(),
                                          self.B))
             self.stack_fp8 = True

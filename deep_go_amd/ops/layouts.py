@@ -77,13 +77,15 @@ def stack_frag(A: torch.Tensor) -> torch.Tensor:
 
 
 def stack_frag_f8(w8: torch.Tensor) -> torch.Tensor:
-    """conv_stack_f8 A-operand order of e4m3 forward weights ``w8`` [128 co][9 taps][128 ci]
-    (uint8 bytes): flat [tap 9][wm 2][i 4][half 2][lane 64][e 16] with co = wm*64 + i*16 +
-    (lane & 15), ci = 32*(lane >> 4) + 16*half + e (the MX-MFMA lane group g holds
-    k = 32g .. 32g + 31)."""
-    assert tuple(w8.shape) == (128, 9, 128)
-    a = w8.reshape(2, 4, 16, 9, 4, 2, 16)               # wm i lr | tap | lq half e
-    return a.permute(3, 0, 1, 5, 4, 2, 6).reshape(-1).contiguous()
+    """conv_stack_f8 A-operand order of e4m3 forward weights ``w8`` [C co][9 taps][C ci]
+    (uint8 bytes, C = 128 | 256): flat [h C/128][tap 9][c C/128][wm 2][i 4][half 2][lane 64]
+    [e 16] with co = 128h + wm*64 + i*16 + (lane & 15), ci = 128c + 32*(lane >> 4) + 16*half
+    + e (the MX-MFMA lane group g holds k = 32g .. 32g + 31; h = output pass, c = K chunk)."""
+    C = w8.shape[0]
+    assert C in (128, 256) and tuple(w8.shape) == (C, 9, C)
+    n = C // 128
+    a = w8.reshape(n, 2, 4, 16, 9, n, 4, 2, 16)         # h wm i lr | tap | c lq half e
+    return a.permute(0, 4, 5, 1, 2, 7, 6, 3, 8).reshape(-1).contiguous()
 
 
 def conv_dims(k: int, cin_frame: int, cout: int, bm: int):

@@ -197,3 +197,12 @@ def test_stack_frag_f8_layout_indexing():
         ci = 32 * (lane >> 4) + 16 * half + e
         idx = ((((t * 2 + wm) * 4 + i) * 2 + half) * 64 + lane) * 16 + e
         assert f[idx].item() == w[co, t, ci].item()
+    # 256 channels: [h][tap][c][wm][i][half][lane][e]
+    w = torch.arange(256 * 9 * 256, dtype=torch.int64).reshape(256, 9, 256)
+    f = LY.stack_frag_f8(w)
+    for _ in range(200):
+        h, t, c, wm, i, half, lane, e = (int(rng.integers(n)) for n in (2, 9, 2, 2, 4, 2, 64, 16))
+        co = 128 * h + wm * 64 + i * 16 + (lane & 15)
+        ci = 128 * c + 32 * (lane >> 4) + 16 * half + e
+        idx = ((((((h * 9 + t) * 2 + c) * 2 + wm) * 4 + i) * 2 + half) * 64 + lane) * 16 + e
+        assert f[idx].item() == w[co, t, ci].item()

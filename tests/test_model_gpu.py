@@ -358,21 +358,22 @@ def test_lr_decay_fused_into_weight_refresh():
     assert abs(net.lr.item() - cfg.rate * (1 - 1e-3) ** 3) < 1e-15
 
 
-@pytest.mark.parametrize("layers,stack", [(4, "1"), (4, "0"), (12, "1")])
-def test_fp8_forward_model_tracks_bf16(layers, stack, monkeypatch):
+@pytest.mark.parametrize("layers,stack,ch", [(4, "1", 128), (4, "0", 128), (12, "1", 128),
+                                            (5, "1", 256), (5, "0", 256)])
+def test_fp8_forward_model_tracks_bf16(layers, stack, ch, monkeypatch):
     """dtype='fp8': hidden-layer forwards on e4m3 MX-MFMA with delayed scaling — the fused
     fp8 layer stack (conv_stack_f8, default) or the per-layer fp8 kernels (DG_STACK=0); loss
     and gradients stay close to the bf16 model with the same weights and batch."""
-    _, net_b, _ = _setup(layers, 128, 6, seed=3)
+    _, net_b, _ = _setup(layers, ch, 6, seed=3)
     monkeypatch.setenv("DG_STACK", stack)
-    _, net_8, _ = _setup(layers, 128, 6, seed=3, dtype="fp8")
+    _, net_8, _ = _setup(layers, ch, 6, seed=3, dtype="fp8")
     assert any(p.fp8 for p in net_8.plans) and net_8._fp8_calibrated
     assert net_8.stack_fp8 == (stack == "1")
     if stack == "1":
         from deep_go_amd.ops import layouts as LY
         i = net_8.stack[0]
         assert torch.equal(net_8.wf8frag[i], LY.stack_frag_f8(
-            net_8.wf8[i][:128, :9 * 128].reshape(128, 9, 128)))
+            net_8.wf8[i][:ch, :9 * ch].reshape(ch, 9, ch)))
     net_b.forward_backward()
     net_8.forward_backward()
     torch.cuda.synchronize()

@@ -66,7 +66,7 @@ def test_stack_layers_match_fp32_oracle(epi):
         # zero border untouched
         assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
         if epi == "fwd":  # bitmask written = nonzero of the bf16 output
-            nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, 16, 8).long()
+            nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, C // 8, 8).long()
             packed = (nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8)
             assert torch.equal(packed, ms[l]), f"fwd layer {l}: mask"
         xin = ys[l]
@@ -77,8 +77,8 @@ def _q8(x):
     return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
 
 
-@pytest.mark.parametrize("nl", [2, 4])
-def test_fp8_stack_matches_emulated_oracle(nl):
+@pytest.mark.parametrize("C,nl", [(128, 2), (128, 4), (256, 2), (256, 3)])
+def test_fp8_stack_matches_emulated_oracle(C, nl):
     """conv_stack_f8 (e4m3 image + weights, MX MFMA) vs a PyTorch fp32 oracle that applies the
     same quantization: layer l's input = e4m3(Y_{l-1} / s_x) (teacher-forced on the kernel's
     own dequantized bf16 output, which re-quantizes to the exact fp8 bytes), weights =
@@ -90,6 +90,7 @@ def test_fp8_stack_matches_emulated_oracle(nl):
     h = hip()
     torch.manual_seed(11)
     B, l0 = 5, 1
+    npb = (C // 128) * 24 * 2 * 4 * 64 * 4
     x = LY.alloc_frame(B, C, 1, DEV)
     LY.frame_interior(x, 1).copy_(torch.randn(B, 19, 19, C, device=DEV).relu())
     # scales[2g] = s_w of layer g, scales[2g + 1] = s_y of act[g]
@@ -106,14 +107,14 @@ def test_fp8_stack_matches_emulated_oracle(nl):
         scales[2 * g + 1] = 2.0 ** (-4 - l)            # arbitrary (power-of-two) output scales
         W8.append((w / s_w).clamp(-448, 448).to(torch.float8_e4m3fn))
         ys.append(LY.alloc_frame(B, C, 1, DEV))
-        ms.append(torch.zeros(B, 361, 16, dtype=torch.uint8, device=DEV))
-        pbs.append(torch.zeros(24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16, device=DEV))
+        ms.append(torch.zeros(B, 361, C // 8, dtype=torch.uint8, device=DEV))
+        pbs.append(torch.zeros(npb, dtype=torch.bfloat16, device=DEV))
     frags = [LY.stack_frag_f8(w8.view(torch.uint8)) for w8 in W8]
     amax = torch.zeros(l0 + nl, dtype=torch.int32, device=DEV)
     tab = np.array([[frags[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr()]
                     for i in range(nl)], dtype=np.int64)
-    h.conv_stack_f8(tab.ctypes.data, nl, x.data_ptr(), l0, scales.data_ptr(), amax.data_ptr(), B,
-                    stream_handle())
+    h.conv_stack_f8(C, tab.ctypes.data, nl, x.data_ptr(), l0, scales.data_ptr(), amax.data_ptr(),
+                    B, stream_handle())
     torch.cuda.synchronize()
     amax_f = amax.view(torch.float32)
     assert abs(amax_f[l0 - 1].item() - x.float().max().item()) < 1e-6
@@ -134,7 +135,7 @@ def test_fp8_stack_matches_emulated_oracle(nl):
         assert err < (1e-2 if last else 0.07) and close > 0.995, (l, err, close)
         if not last:
             assert abs(amax_f[g].item() - v.max().item()) <= 1e-3 * v.max().item()
-        nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, 16, 8).long()
+        nz = (LY.frame_interior(ys[l], 1) != 0).reshape(B, 361, C // 8, 8).long()
         assert torch.equal((nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8), ms[l])
         assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
         xin = ys[l]

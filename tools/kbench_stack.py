@@ -60,7 +60,7 @@ def main():
     def run8(mode=0, nl=NL):
         def f():
             h.conv_stack_f8_set_mode(mode)
-            h.conv_stack_f8(t8.ctypes.data, nl, x.data_ptr(), 1, scales.data_ptr(),
+            h.conv_stack_f8(C, t8.ctypes.data, nl, x.data_ptr(), 1, scales.data_ptr(),
                             amax.data_ptr(), B, s)
         return f
     flops = 2.0 * C * C * 9 * 361 * B * NL
