@@ -29,10 +29,10 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
 void dg_conv_stack_f8_set_mode(int m);
-hipError_t dg_conv_stack_f8(int C, const long long* table, int nl, const void* X0, int l0,
-                            const float* scales, unsigned* amax, int B, hipStream_t stream);
-hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
-                                     const float* scales, unsigned* amax, int B, const float* w,
+hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
+                            const float* s_x0, unsigned* amax_x0, int B, hipStream_t stream);
+hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
+                                     const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
                                      float* dzb, int head_relu, float grad_scale,
@@ -74,7 +74,7 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
                              const float* s_w, const float* s_y, unsigned* amax_y, void* mask,
                              hipStream_t stream);
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y, float w_margin,
-                               int* sat, hipStream_t s);
+                               int* sat, float* gscales, unsigned* gamax, hipStream_t s);
 hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
                          const float* s_w, hipStream_t s);
 hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
@@ -196,21 +196,21 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_stack2_fwd_head");
   }, "conv_stack2 forward + the fused 3x3/128 policy head");
   // conv_stack_f8.hip: the fp8 (e4m3, MX MFMA) forward stack of the hidden 128 -> 128 layers
-  m.def("conv_stack_f8", [](int C, uintptr_t table, int nl, uintptr_t X0, int l0,
-                            uintptr_t scales, uintptr_t amax, int B, uintptr_t stream) {
-    check(dg_conv_stack_f8(C, P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
-                           P<unsigned>(amax), B, S(stream)),
+  m.def("conv_stack_f8", [](int C, int epi, uintptr_t table, int nl, uintptr_t X0,
+                            uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t stream) {
+    check(dg_conv_stack_f8(C, epi, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+                           P<unsigned>(amax_x0), B, S(stream)),
           "conv_stack_f8");
-  }, "fp8 forward stack (C = 128 | 256): table rows {A8_frag, pbias_frag, Y, mask}; l0 = first "
-     "layer index");
-  m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int l0,
-                                     uintptr_t scales, uintptr_t amax, int B, uintptr_t w,
+  }, "fp8 layer stack (C = 128 | 256; epi 1 forward e4m3, 2 backward-data e5m2): table rows "
+     "{A8_frag, pbias_frag, Y, mask, s_in, s_w, s_out, amax_out}; X0 quantized with *s_x0");
+  m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0,
+                                     uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t w,
                                      uintptr_t bias, uintptr_t posb, uintptr_t labels,
                                      uintptr_t loss, uintptr_t pred, uintptr_t dZ,
                                      uintptr_t gw_part, uintptr_t dzb, int head_relu,
                                      float grad_scale, uintptr_t stream) {
-    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), l0, P<float>(scales),
-                                    P<unsigned>(amax), B, P<float>(w), P<float>(bias),
+    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+                                    P<unsigned>(amax_x0), B, P<float>(w), P<float>(bias),
                                     P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
                                     P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
                                     grad_scale, S(stream)),
@@ -244,9 +244,11 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_board_fp8");
   });
   m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, uintptr_t amax_y,
-                                float w_margin, uintptr_t sat, uintptr_t stream) {
+                                float w_margin, uintptr_t sat, uintptr_t gscales,
+                                uintptr_t gamax, uintptr_t stream) {
     check(dg_fp8_update_scales(n, P<float>(scales), P<unsigned>(amax_w), P<unsigned>(amax_y),
-                               w_margin, P<int>(sat), S(stream)),
+                               w_margin, P<int>(sat), P<float>(gscales), P<unsigned>(gamax),
+                               S(stream)),
           "fp8_update_scales");
   });
   m.def("weight_fp8", [](uintptr_t w, uintptr_t wf8, int cout, int cin, int taps, int cinp,

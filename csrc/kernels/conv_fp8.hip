@@ -229,13 +229,22 @@ conv_board_fp8_kernel(Fp8Args a) {
 // saturate at +-448), s_y[l] from the activation amax of the last forward (rounded up to a
 // power of two); both reset.
 // scales[2l] = s_w, scales[2l+1] = s_y; amax_w / amax_y: float bits.
-// sat (optional): saturation counters [2l] weights, [2l + 1] activations, incremented when
-// the amax just observed exceeds the range of the scale that was in use (448 s): values of
-// that tensor were clamped to +-448 in the last refresh / forward.
+// sat (optional): saturation counters [2l] weights, [2l + 1] activations (+ [2n + l]
+// gradients), incremented when the amax just observed exceeds the range of the scale that
+// was in use (448 s; e5m2 57344 s): values of that tensor were clamped in the last refresh /
+// forward / backward.  gscales / gamax (optional): the e5m2 gradient scales of dz[l] (fp8
+// backward-data stack), powers of two with 1.25x headroom like the activation scales.
 __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
-                                         float w_margin, int* sat) {
+                                         float w_margin, int* sat, float* gscales,
+                                         unsigned* gamax) {
   const int l = threadIdx.x;
   if (l >= n) return;
+  if (gscales) {
+    const float mg = __uint_as_float(gamax[l]);
+    if (sat && mg > 57344.f * gscales[l]) sat[2 * n + l] += 1;
+    if (mg > 0.f) gscales[l] = exp2f(ceilf(log2f(1.25f * mg / 57344.f)));
+    gamax[l] = 0u;
+  }
   const float mw = __uint_as_float(amax_w[l]);
   if (sat) {
     if (mw > FP8_MAX * scales[2 * l]) sat[2 * l] += 1;
@@ -349,10 +358,11 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
 }
 
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
-                               float w_margin, int* sat, hipStream_t s) {
+                               float w_margin, int* sat, float* gscales, unsigned* gamax,
+                               hipStream_t s) {
   if (n <= 0 || n > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(1), dim3(n < 64 ? 64 : (n + 63) / 64 * 64), 0,
-                     s, n, scales, amax_w, amax_y, w_margin, sat);
+                     s, n, scales, amax_w, amax_y, w_margin, sat, gscales, gamax);
   return hipGetLastError();
 }
 

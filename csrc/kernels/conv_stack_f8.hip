@@ -21,8 +21,12 @@
 //     layout over the same 112 KB), so the fused policy head (head_body.h) runs on it as in
 //     the bf16 stack;
 //   * prologue: the bf16 input frame (conv_l1's output) is quantized into the image with
-//     its scale s_x = scales[2 (l0 - 1) + 1]; its amax goes to amax[l0 - 1].
-// Scales (device, per conv layer g): scales[2g] = s_w, scales[2g + 1] = s_y (of act[g]).
+//     its scale; its amax is folded in as well.
+// Scales are device scalars named per layer in the launch table (s_in, s_w, s_out, amax_out):
+// HipGoNet points them into its fp8_scales / fp8_gscales arrays (delayed scaling).
+// EPI_DGRAD runs the backward-data chain the same way: e5m2 gradient image (the wider range),
+// e4m3 flipped/transposed weights (MX MFMA A e4m3 x B e5m2), ReLU-mask epilogue, dequantized
+// bf16 dZ frames copied out for the weight gradients.
 //
 // C = 256 (config 5's d = 256): the e4m3 image is 441 rows of 256 B (113 KB, slot swizzle
 // ((x + 3y) & 15)) — resident where a bf16 one (226 KB) cannot be.  The 256 output channels
@@ -60,7 +64,10 @@ constexpr int NT = NW * 64;
 constexpr int SCRATCH = 12 * 1024;
 constexpr int STEP_BYTES = 2 * MF * 2 * 64 * 16;  // 16 KB per (tap, chunk) K-step
 constexpr int WM_BYTES = STEP_BYTES / 2;
-constexpr float FP8_MAX = 448.f;
+constexpr float FP8_MAX = 448.f;      // e4m3
+constexpr float BF8_MAX = 57344.f;    // e5m2
+constexpr int EPI_FWD = 1;
+constexpr int EPI_DGRAD = 2;
 
 static_assert(dghead::scratch_bytes(128) + 64 <= SCRATCH, "head scratch");
 
@@ -83,18 +90,22 @@ struct Geo {
 };
 
 struct F8Layer {
-  const char* A8;       // fragment-ordered e4m3 weights (9 x 16 KB x (C/128)^2)
-  const bf16_t* pbias;  // bf16 bias + pos-bias in the stack's fragment order (per pass)
-  char* Y;              // bf16 output frame [B][21][21][C]
-  uint8_t* mask;        // [B][361][C/8] ReLU bits (written)
+  const char* A8;       // fragment-ordered e4m3 weights (9 x 16 KB x (C/128)^2); dgrad: the
+                        // flipped, transposed operand
+  const bf16_t* pbias;  // EPI_FWD: bf16 bias + pos-bias in the stack's fragment order
+  char* Y;              // bf16 output frame [B][21][21][C] (activation / dZ of the layer below)
+  uint8_t* mask;        // [B][361][C/8] ReLU bits: EPI_FWD writes, EPI_DGRAD reads (layer below)
+  const float* s_in;    // scale of this layer's quantized input (device scalar)
+  const float* s_w;     // scale of its e4m3 weights
+  const float* s_out;   // scale its output is quantized with (the next layer's s_in)
+  unsigned* amax_out;   // |output| max folded in here (float bits; delayed scaling)
 };
 struct F8Args {
   const char* X0;       // bf16 input frame of the first layer
+  const float* s_x0;    // its quantization scale
+  unsigned* amax_x0;    // its |x| max (folded in by the prologue)
   int nl;
-  int l0;               // global conv-layer index of the first stack layer (>= 1)
-  int fuse_head;        // C = 128 only
-  const float* scales;  // [2g] = s_w of layer g, [2g + 1] = s_y of act[g]
-  unsigned* amax;       // [g]: amax of act[g] (float bits), folded in here
+  int fuse_head;        // C = 128, EPI_FWD only
   F8Layer L[MAXL];
   dghead::HeadMArgs head;
 };
@@ -132,7 +143,23 @@ DG_DEV void wg_amax(float v, unsigned* amax, float* s_tmp) {
   }
 }
 
-// 4 e4m3 bytes -> 4 bf16 (scaled by the power of two s) + their 4 ReLU bits
+// e4m3 (EPI_FWD: activations) or e5m2 (EPI_DGRAD: gradients, the wider range) packing
+template <int EPI>
+DG_DEV uint32_t pack8x4(float a, float b, float c, float d) {
+  if constexpr (EPI == EPI_FWD) return pack_fp8x4(a, b, c, d);
+  int v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+// 2 e4m3 / e5m2 -> 2 bf16 scaled by the power of two s (one v_cvt_scalef32_pk_bf16_*)
+template <int EPI, bool HI>
+DG_DEV uint32_t deq2(uint32_t w, float s) {
+  if constexpr (EPI == EPI_FWD)
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, s, HI));
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8((int)w, s, HI));
+}
+
+// 4 e4m3 bytes -> their 4 ReLU bits
 DG_DEV uint32_t nzbits4(uint32_t w) {
   uint32_t t = w | (w >> 4);
   t |= t >> 2;
@@ -140,13 +167,19 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
   return (t * 0x204081u) >> 21 & 0xFu;   // bits 0, 8, 16, 24 gathered into 21..24
 }
 
+// EPI_FWD: the forward stack (e4m3 activations, bias + pos-bias + ReLU, ReLU bits out);
+// EPI_DGRAD: the backward-data chain dZ_{l-1} = mask_{l-1} * (W_l^T dZ_l) (e5m2 gradients,
+// e4m3 weights: MX MFMA with A e4m3 / B e5m2), dequantized bf16 dZ frames out.
 // MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
 // 2 = no A loads in the K loop, 4 = no copy-out
-template <int C, int MODE>
+template <int C, int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   using G = Geo<C>;
   constexpr int NC = G::NC;
   constexpr int ROWB = G::ROWB;
+  constexpr float QMAX = EPI == EPI_FWD ? FP8_MAX : BF8_MAX;
+  constexpr int BFMT = EPI == EPI_FWD ? 0 : 1;   // MX MFMA B-operand format: e4m3 | e5m2
+  constexpr bool BF16_LAST_IMAGE = C == 128 && EPI == EPI_FWD;  // last layer feeds the head
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -156,9 +189,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   char* sI = smem + SCRATCH;                       // e4m3 image (C = 128 last layer: bf16)
   float* s_amax = (float*)(smem + G::AMAX_OFF);    // 2 x 8 floats (alternating per layer)
 
-  // ---- prologue: quantize the bf16 input frame into the e4m3 image ----
+  // ---- prologue: quantize the bf16 input frame into the image ----
   {
-    const float inv = 1.f / a.scales[2 * (a.l0 - 1) + 1];
+    const float inv = 1.f / *a.s_x0;
     const char* Xb = a.X0 + (size_t)b * FF * C * 2;
     float m = 0.f;
     for (int u = tid; u < FF * (C / 8); u += NT) {     // 8-channel pieces
@@ -170,15 +203,15 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
                     __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        m = fmaxf(m, x[e]);
-        x[e] = fminf(x[e] * inv, FP8_MAX);
+        m = fmaxf(m, fabsf(x[e]));
+        x[e] = fmaxf(fminf(x[e] * inv, QMAX), -QMAX);
       }
       uint2 o;
-      o.x = pack_fp8x4(x[0], x[1], x[2], x[3]);
-      o.y = pack_fp8x4(x[4], x[5], x[6], x[7]);
+      o.x = pack8x4<EPI>(x[0], x[1], x[2], x[3]);
+      o.y = pack8x4<EPI>(x[4], x[5], x[6], x[7]);
       *(uint2*)(sI + f * ROWB + (((q >> 1) ^ fsig<C>(f)) * 16) + (q & 1) * 8) = o;
     }
-    wg_amax(m, a.amax + (a.l0 - 1), s_amax + 8);  // (contains the barrier: image complete)
+    wg_amax(m, a.amax_x0, s_amax + 8);  // (contains the barrier: image complete)
   }
 
   const int lr = lane & 15;
@@ -228,7 +261,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0,
-                                                                      0, 0, 127, 0, 127);
+                                                                      BFMT, 0, 127, 0, 127);
   };
 
   // Copy-out of the previous layer's output (the e4m3 image) as bf16 (x s_prev) + ReLU bits:
@@ -252,18 +285,17 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      // 2 e4m3 -> 2 bf16 scaled by s_prev in one v_cvt_scalef32_pk_bf16_fp8 (s_prev is a
-      // power of two: fp8_update_scales rounds every activation scale up to one)
-      o[2 * k] = __builtin_bit_cast(
-          uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, false));
-      o[2 * k + 1] = __builtin_bit_cast(
-          uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)wd[k], s_prev, true));
-      bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
+      // (s_prev is a power of two: fp8_update_scales rounds every such scale up to one)
+      o[2 * k] = deq2<EPI, false>(wd[k], s_prev);
+      o[2 * k + 1] = deq2<EPI, true>(wd[k], s_prev);
+      if constexpr (EPI == EPI_FWD)
+        bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
     }
     char* yp = Lo.Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
     *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
     *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
-    *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
+    if constexpr (EPI == EPI_FWD)
+      *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
   };
 
   i32x8 Ak[MF];
@@ -271,15 +303,14 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   load_A(a.L[0].A8, 2, Ak);
 
   for (int l = 0; l < a.nl; ++l) {
-    const int g = a.l0 + l;
     const F8Layer L = a.L[l];
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
     const bool co_on = l > 0;
     const bool last = l + 1 == a.nl;
-    const float s_x = a.scales[2 * (g - 1) + 1];
-    const float deq = s_x * a.scales[2 * g];
-    const float inv_y = 1.f / a.scales[2 * g + 1];
+    const float s_x = *L.s_in;
+    const float deq = s_x * *L.s_w;
+    const float inv_y = 1.f / *L.s_out;
     float vmax = 0.f;
     uint4 co_v;
 
@@ -330,20 +361,27 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       // per-fragment table / LDS addresses out of the layer loop and spills them
       int z0 = 0;
       asm volatile("" : "+v"(z0));
-      uint2 eu[NF][MF];
+      // EPI_FWD: bias table pieces; EPI_DGRAD: the 64 ReLU bits (of the layer below) of this
+      // wave's channels per pixel fragment
+      uint2 eu[NF][EPI == EPI_FWD ? MF : 1];
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
-        const uint2* pf = (const uint2*)L.pbias + hp * (24 * 2 * 4 * 64) +
-                          ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
+        if constexpr (EPI == EPI_FWD) {
+          const uint2* pf = (const uint2*)L.pbias + hp * (24 * 2 * 4 * 64) +
+                            ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
 #pragma unroll
-        for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+          for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+        } else {
+          const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
+          eu[j][0] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * (C / 8) + 16 * hp + 8 * wm + z0);
+        }
       }
       // C = 128 and the last pass of C = 256: every wave is past its last read of the
       // image before it is overwritten (pass 0 of C = 256 only writes the park area)
       const bool to_image = !last && hp == NC - 1;
       if (C == 128 || hp == NC - 1) lds_barrier();
       char* sIe = smem + SCRATCH + z0;
-      if (C == 128 && last) {
+      if (BF16_LAST_IMAGE && last) {
         // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
         // head's weight-gradient pass reads against zero dz): the region held e4m3 data
         for (int u = tid; u < 87 * 8 * 2; u += NT) {
@@ -361,17 +399,25 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           f32x4 v = acc[i][j];
-          const uint2 u = eu[j][i];
-          v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
-          v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
-          v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
-          v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+          if constexpr (EPI == EPI_FWD) {
+            const uint2 u = eu[j][i];
+            v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
+            v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+            v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
+            v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+          } else {
+            const int cw = i * 16 + lq * 4;                // channel within the wave's 64
+            const uint32_t word = (cw < 32) ? eu[j][0].x : eu[j][0].y;
+            const uint32_t bits = word >> ((cw & 31) >> 3 << 3) >> (cw & 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] * deq : 0.f;
+          }
           if (p >= NPTS) continue;
           const int cl = wm * 64 + i * 16 + lq * 4;      // channel within the pass (0..127)
           if (!last) {
-            vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-            const uint32_t q8 = pack_fp8x4(fminf(v[0] * inv_y, FP8_MAX), fminf(v[1] * inv_y, FP8_MAX),
-                                           fminf(v[2] * inv_y, FP8_MAX), fminf(v[3] * inv_y, FP8_MAX));
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            auto qz = [&](float x) { return fmaxf(fminf(x * inv_y, QMAX), -QMAX); };
+            const uint32_t q8 = pack8x4<EPI>(qz(v[0]), qz(v[1]), qz(v[2]), qz(v[3]));
             if (to_image) {
               // channel co = 128 hp + cl: slot co / 16 (XOR sig), byte co % 16
               const int co = 128 * hp + cl;
@@ -382,7 +428,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
                                       : smem + SCRATCH + G::IMG + (p - G::PARK1) * 128;
               *(uint32_t*)(pr + z0 + cl) = q8;
             }
-          } else if constexpr (C == 128) {
+          } else if constexpr (BF16_LAST_IMAGE) {
             // bf16 two-image layout (conv_stack2 / head_body.h) for the fused head
             const int cw = i * 16 + lq * 4;
             uint2 o;
@@ -390,18 +436,21 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
             o.y = pack_bf16x2(v[2], v[3]);
             *(uint2*)(sIe + wm * H_BYTES + f * 128 + (((cw >> 3) ^ fsig8(f)) * 16) + (cw & 4) * 2) = o;
           } else {
-            // C = 256 last layer: bf16 straight to the output frame (+ ReLU bits)
+            // last layer (C = 256 forward, any dgrad): bf16 straight to the output frame
+            // (+ the forward's ReLU bits)
             const int co = 128 * hp + cl;
             uint2 o;
             o.x = pack_bf16x2(v[0], v[1]);
             o.y = pack_bf16x2(v[2], v[3]);
             *(uint2*)(L.Y + ((size_t)(b * FF + f) * C + co) * 2) = o;
+            if constexpr (EPI == EPI_FWD) {
             const uint32_t nib = (v[0] > 0.f ? 1u : 0u) | (v[1] > 0.f ? 2u : 0u) |
                                  (v[2] > 0.f ? 4u : 0u) | (v[3] > 0.f ? 8u : 0u);
             // 4 bits of one mask byte: the lane pair (lq even, odd) shares the byte
             const uint32_t other = __shfl_xor(nib, 16, 64);
             if ((lq & 1) == 0)
               L.mask[((size_t)b * NPTS + p) * (C / 8) + (co >> 3)] = (uint8_t)(nib | (other << 4));
+            }
           }
         }
       }
@@ -420,10 +469,10 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         }
       }
     }
-    if (!last) wg_amax(vmax, a.amax + g, s_amax + 8 * (l & 1));  // (barrier inside)
+    if (!last) wg_amax(vmax, L.amax_out, s_amax + 8 * (l & 1));  // (barrier inside)
     lds_barrier();  // the next layer's input is complete
   }
-  if constexpr (C == 128) {
+  if constexpr (BF16_LAST_IMAGE) {
     // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2
     const F8Layer Ll = a.L[a.nl - 1];
     const int co_q = tid & 15;
@@ -449,51 +498,60 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
 int g_f8_mode = 0;
 
-template <int C, int MODE>
+template <int C, int EPI, int MODE>
 hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
   constexpr size_t lds = Geo<C>::LDS;
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<C, MODE>,
+    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<C, EPI, MODE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack_f8_kernel<C, MODE>), dim3(B), dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((conv_stack_f8_kernel<C, EPI, MODE>), dim3(B), dim3(NT), lds, stream, a);
   return hipGetLastError();
 }
 
 template <int C>
-hipError_t launch_mode(const F8Args& a, int B, hipStream_t stream) {
+hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
+  if (epi == EPI_DGRAD) return launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
   switch (g_f8_mode) {
-    case 2: return launch_f8<C, 2>(a, B, stream);
-    case 4: return launch_f8<C, 4>(a, B, stream);
-    case 6: return launch_f8<C, 6>(a, B, stream);
-    default: return launch_f8<C, 0>(a, B, stream);
+    case 2: return launch_f8<C, EPI_FWD, 2>(a, B, stream);
+    case 4: return launch_f8<C, EPI_FWD, 4>(a, B, stream);
+    case 6: return launch_f8<C, EPI_FWD, 6>(a, B, stream);
+    default: return launch_f8<C, EPI_FWD, 0>(a, B, stream);
   }
 }
 
-hipError_t f8_launch(int C, const long long* table, int nl, const void* X0, int l0,
-                     const float* scales, unsigned* amax, int B, const dghead::HeadMArgs* head,
+// table: nl rows of 8 int64 {A8, pbias, Y, mask, s_in, s_w, s_out, amax_out}
+hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void* X0,
+                     const float* s_x0, unsigned* amax_x0, int B, const dghead::HeadMArgs* head,
                      hipStream_t stream) {
-  if (nl <= 0 || nl > MAXL || B <= 0 || l0 < 1 || !scales || !amax) return hipErrorInvalidValue;
-  if (C != 128 && C != 256) return hipErrorInvalidValue;
-  if (head && C != 128) return hipErrorInvalidValue;
+  if (nl <= 0 || nl > MAXL || B <= 0 || !s_x0 || !amax_x0) return hipErrorInvalidValue;
+  if ((C != 128 && C != 256) || (epi != EPI_FWD && epi != EPI_DGRAD)) return hipErrorInvalidValue;
+  if (head && (C != 128 || epi != EPI_FWD)) return hipErrorInvalidValue;
   F8Args a;
   a.X0 = (const char*)X0;
+  a.s_x0 = s_x0;
+  a.amax_x0 = amax_x0;
   a.nl = nl;
-  a.l0 = l0;
-  a.scales = scales;
-  a.amax = amax;
   a.fuse_head = head ? 1 : 0;
   a.head = head ? *head : dghead::HeadMArgs{};
   for (int i = 0; i < nl; ++i) {
-    a.L[i].A8 = (const char*)table[4 * i];
-    a.L[i].pbias = (const bf16_t*)table[4 * i + 1];
-    a.L[i].Y = (char*)table[4 * i + 2];
-    a.L[i].mask = (uint8_t*)table[4 * i + 3];
-    if (!a.L[i].A8 || !a.L[i].pbias || !a.L[i].Y || !a.L[i].mask) return hipErrorInvalidValue;
+    const long long* t = table + 8 * i;
+    F8Layer& L = a.L[i];
+    L.A8 = (const char*)t[0];
+    L.pbias = (const bf16_t*)t[1];
+    L.Y = (char*)t[2];
+    L.mask = (uint8_t*)t[3];
+    L.s_in = (const float*)t[4];
+    L.s_w = (const float*)t[5];
+    L.s_out = (const float*)t[6];
+    L.amax_out = (unsigned*)t[7];
+    if (!L.A8 || !L.Y || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
+      return hipErrorInvalidValue;
+    if (epi == EPI_FWD && !L.pbias) return hipErrorInvalidValue;
   }
-  return C == 128 ? launch_mode<128>(a, B, stream) : launch_mode<256>(a, B, stream);
+  return C == 128 ? launch_mode<128>(epi, a, B, stream) : launch_mode<256>(epi, a, B, stream);
 }
 
 }  // namespace
@@ -502,21 +560,22 @@ extern "C" {
 
 void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 
-// table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask} (int64)
-hipError_t dg_conv_stack_f8(int C, const long long* table, int nl, const void* X0, int l0,
-                            const float* scales, unsigned* amax, int B, hipStream_t stream) {
-  return f8_launch(C, table, nl, X0, l0, scales, amax, B, nullptr, stream);
+// table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask, s_in, s_w,
+// s_out, amax_out} (int64); epi 1 forward, 2 backward-data
+hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
+                            const float* s_x0, unsigned* amax_x0, int B, hipStream_t stream) {
+  return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, stream);
 }
 
-hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0, int l0,
-                                     const float* scales, unsigned* amax, int B, const float* w,
+hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
+                                     const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
                                      float* dzb, int head_relu, float grad_scale,
                                      hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return f8_launch(128, table, nl, X0, l0, scales, amax, B, &h, stream);
+  return f8_launch(128, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, stream);
 }
 
 }  // extern "C"

@@ -246,7 +246,8 @@ struct WRefreshLayer {
   uint4* wf_frag;      // conv_stack2 A operands (3x3, 128 -> 128 only), MFMA fragment order:
   uint4* wd_frag;      //   [step 18][wm 2][kk 2][i 4][lane 64] x 8 bf16 (forward / dgrad)
   uint4* wf8_frag;     // conv_stack_f8 A operands (e4m3, quantized with s_w like wf8):
-                       //   [tap 9][wm 2][i 4][half 2][lane 64] x 16 B (requires wf8)
+                       //   [h][tap 9][c][wm 2][i 4][half 2][lane 64] x 16 B (requires wf8)
+  uint4* wd8_frag;     // the same for the backward-data operand (flipped taps, transposed)
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
@@ -294,7 +295,7 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       }
       tileS[rr][cc] = v;
     }
-    if (L.wd || L.wf_frag || L.wf8_frag) __syncthreads();
+    if (L.wd || L.wf_frag || L.wf8_frag || L.wd8_frag) __syncthreads();
     if (L.wd) {
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
@@ -345,6 +346,28 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       const int lane = (2 * (cit & 1) + lql) * 16 + lr;
       L.wf8_frag[((((((size_t)h * 9 + t) * nc + c) * 2 + wm) * 4 + i) * 2 + hf) * 64 + lane] =
           uint4{q[0], q[1], q[2], q[3]};
+    }
+    if (L.wd8_frag) {
+      // dgrad operand A_d[ci][8 - t][co] = W[co][t][ci]: rows ci (pass h = cit / 2, co-half
+      // wm = cit % 2), k = co (chunk c = cot / 2, lane groups 2 (cot % 2), +1) at tap 8 - t
+      const int u = threadIdx.x;
+      const int lr = u & 15, lql = (u >> 4) & 1, hf = (u >> 5) & 1, i = u >> 6;
+      const int r = i * 16 + lr, c0 = 32 * lql + 16 * hf;
+      uint32_t q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v4[k] = fmaxf(fminf(tileS[c0 + 4 * e + k][r] * inv8, 448.f), -448.f);
+        int pkd = __builtin_amdgcn_cvt_pk_fp8_f32(v4[0], v4[1], 0, false);
+        pkd = __builtin_amdgcn_cvt_pk_fp8_f32(v4[2], v4[3], pkd, true);
+        q[e] = (uint32_t)pkd;
+      }
+      const int nc = L.cout / 128, h = cit >> 1, wm = cit & 1, c = cot >> 1;
+      const int lane = (2 * (cot & 1) + lql) * 16 + lr;
+      L.wd8_frag[((((((size_t)h * 9 + (8 - t)) * nc + c) * 2 + wm) * 4 + i) * 2 + hf) * 64 +
+                 lane] = uint4{q[0], q[1], q[2], q[3]};
     }
     __syncthreads();
   }
@@ -463,10 +486,10 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
   return hipGetLastError();
 }
 
-// layers: n entries of 19 int64 words
+// layers: n entries of 20 int64 words
 //   {w, wf, wd, cout, cin, taps, cinp, kpf, kpd, pbias_frag, wf8, s_w, amax_w, bias, posb,
-//    pbias, wf_frag, wd_frag, wf8_frag}  (pbias_frag / *_frag: stack-order tables,
-//    128 -> 128 only, or 0)
+//    pbias, wf_frag, wd_frag, wf8_frag, wd8_frag}  (pbias_frag / *_frag: stack-order tables,
+//    or 0)
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
@@ -475,7 +498,7 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 19 * i;
+    const long long* t = table + 20 * i;
     a.L[i].w = (const float*)t[0];
     a.L[i].wf = (bf16_t*)t[1];
     a.L[i].wd = (bf16_t*)t[2];
@@ -497,6 +520,8 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].wd_frag = (uint4*)t[17];
     if ((a.L[i].wf_frag != nullptr) != (a.L[i].wd_frag != nullptr)) return hipErrorInvalidValue;
     a.L[i].wf8_frag = (uint4*)t[18];
+    a.L[i].wd8_frag = (uint4*)t[19];
+    if (a.L[i].wd8_frag && !a.L[i].wf8_frag) return hipErrorInvalidValue;
     if (a.L[i].wf8_frag && (!a.L[i].wf8 || a.L[i].taps != 9 || a.L[i].cout != a.L[i].cin ||
                             (a.L[i].cout != 128 && a.L[i].cout != 256)))
       return hipErrorInvalidValue;

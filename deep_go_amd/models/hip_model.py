@@ -143,6 +143,7 @@ class HipGoNet:
         self.wfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wdfrag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wf8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        self.wd8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         for p in self.plans:
             if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
                 self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
@@ -152,6 +153,9 @@ class HipGoNet:
                     and p.cout in (128, 256)):
                 self.wf8frag[p.index] = torch.zeros(p.cout * 9 * p.cin, dtype=torch.uint8,
                                                     device=dev)
+                # the fp8 backward-data stack's operand (DG_FP8_DGRAD=0: bf16 backward-data)
+                if os.environ.get("DG_FP8_DGRAD", "1") != "0":
+                    self.wd8frag[p.index] = torch.zeros_like(self.wf8frag[p.index])
 
         # ---- activation / gradient frames ----
         B = batch
@@ -202,7 +206,12 @@ class HipGoNet:
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         # saturation events per layer ([2l] weights, [2l + 1] activations): a step whose
         # observed amax exceeded 448 x the scale in use (values were clamped)
-        self.fp8_sat = torch.zeros(2 * len(self.plans), dtype=torch.int32, device=dev)
+        # ([2L + l] gradients: the e5m2 dz[l] of the fp8 backward-data stack)
+        self.fp8_sat = torch.zeros(3 * len(self.plans), dtype=torch.int32, device=dev)
+        # e5m2 scales of the gradient frames dz[l] the fp8 backward-data stack quantizes, and
+        # their observed |dz| max (delayed scaling, powers of two)
+        self.fp8_gscales = torch.ones(len(self.plans), dtype=torch.float32, device=dev)
+        self.fp8_gamax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self._fp8_calibrated = not self.fp8
         # backward side stream ("bias", the default): the HBM-bound bias-grad partials run on
         # it beside the MFMA-bound weight-gradient launch of the same layers, and the first
@@ -267,7 +276,7 @@ class HipGoNet:
                          self.params.data_ptr() + 4 * spec.pos_off,
                          self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0,
                          _ptr(self.wfrag[p.index]), _ptr(self.wdfrag[p.index]),
-                         _ptr(self.wf8frag[p.index])])
+                         _ptr(self.wf8frag[p.index]), _ptr(self.wd8frag[p.index])])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
     def _build_plans(self):
@@ -368,10 +377,11 @@ class HipGoNet:
                 self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
                 self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
             if self.stack_fp8:
+                S, AM = self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr()
                 fused = (h.conv_stack_f8_fwd_head, (
                     self._stack_table.ctypes.data, len(self.stack),
-                    self.act[first - 1].data_ptr(), first, self.fp8_scales.data_ptr(),
-                    self.fp8_amax.data_ptr(), self.B) + fused[1][5:])
+                    self.act[first - 1].data_ptr(), S + 4 * (2 * (first - 1) + 1),
+                    AM + 4 * (first - 1), self.B) + fused[1][5:])
             self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8) else (f, a)
                                for f, a in self._fwd]
             if any(f in (h.conv_stack2_fwd_head, h.conv_stack_f8_fwd_head)
@@ -447,17 +457,24 @@ class HipGoNet:
                 # the fp8 stack always writes ReLU bits (its dgrad consumer may read them)
                 m = self.relu_mask[i] = torch.zeros((self.B, NUM_POINTS, self.plans[i].cout // 8),
                                                     dtype=torch.uint8, device=self.device)
-            A = self.wf8frag[i] if fp8 else self.wfrag[i]
-            rows.append([A.data_ptr(), self.pbias_frag[i].data_ptr(),
-                         self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
+            if fp8:
+                S, AM = self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr()
+                rows.append([self.wf8frag[i].data_ptr(), self.pbias_frag[i].data_ptr(),
+                             self.act[i].data_ptr(), m.data_ptr(),
+                             S + 4 * (2 * i - 1), S + 4 * 2 * i, S + 4 * (2 * i + 1), AM + 4 * i])
+            else:
+                rows.append([self.wfrag[i].data_ptr(), self.pbias_frag[i].data_ptr(),
+                             self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
         self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
         if fp8:
             # fp8 forward stack (conv_stack_f8.hip): quantizes its bf16 input frame itself
             # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out
-            op = (self.h.conv_stack_f8, (self.plans[first].cout, self._stack_table.ctypes.data,
-                                         len(best), self.act[first - 1].data_ptr(), first,
-                                         self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr(),
+            S, AM = self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr()
+            op = (self.h.conv_stack_f8, (self.plans[first].cout, self.h.EPI_FWD,
+                                         self._stack_table.ctypes.data, len(best),
+                                         self.act[first - 1].data_ptr(),
+                                         S + 4 * (2 * (first - 1) + 1), AM + 4 * (first - 1),
                                          self.B))
             self.stack_fp8 = True
         else:
@@ -483,6 +500,7 @@ class HipGoNet:
         per-layer dgrad launches of those layers are dropped from ``_bwd``; their weight
         gradients run afterwards (they only read dZ_i).  DG_DSTACK=0 keeps per-layer dgrads."""
         self.dstack: List[int] = []
+        self.dstack_fp8 = False
         self.wgroups: List[List[int]] = []
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
@@ -494,12 +512,19 @@ class HipGoNet:
             return
         L = self.layout.layers
 
+        # fp8 models: the e5m2 backward-data stack (conv_stack_f8 EPI_DGRAD, 128 | 256 ch)
+        fp8 = self.fp8 and any(w is not None for w in self.wd8frag)
+
         def ok(i):
             p = self.plans[i]
-            return (i > 0 and p.board_d and p.k == 3 and p.cin == 128 and p.cout == 128
-                    and L[i].pad == 1 and self.dzp[i - 1] == 1 and p.KPd == p.KP
-                    and self.relu_mask[i - 1] is not None
-                    and self.wdfrag[i] is not None)
+            if not (i > 0 and p.board_d and p.k == 3 and L[i].pad == 1
+                    and self.dzp[i - 1] == 1 and p.KPd == p.KP
+                    and self.relu_mask[i - 1] is not None):
+                return False
+            if fp8:
+                return (self.wd8frag[i] is not None
+                        and p.cout == self.plans[len(self.plans) - 1].cout)
+            return p.cin == 128 and p.cout == 128 and self.wdfrag[i] is not None
         run = []
         for i in range(len(self.plans) - 1, 0, -1):   # must start at the top hidden layer
             if not ok(i):
@@ -509,12 +534,26 @@ class HipGoNet:
             self._dgrads_first()
             return
         self.dstack = run
-        rows = [[self.wdfrag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
-                 self.relu_mask[i - 1].data_ptr()] for i in run]
-        self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-        self._bwd_pre.append((self.h.conv_stack2, (self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
-                                                  len(run), self.dz[run[0]].data_ptr(),
-                                                  self.plans[run[0]].KPd, self.B)))
+        self.dstack_fp8 = fp8
+        if fp8:
+            S = self.fp8_scales.data_ptr()
+            GS, GA = self.fp8_gscales.data_ptr(), self.fp8_gamax.data_ptr()
+            rows = [[self.wd8frag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
+                     self.relu_mask[i - 1].data_ptr(), GS + 4 * i, S + 4 * 2 * i,
+                     GS + 4 * (i - 1), GA + 4 * (i - 1)] for i in run]
+            self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+            self._bwd_pre.append((self.h.conv_stack_f8, (
+                self.plans[run[0]].cout, self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+                len(run), self.dz[run[0]].data_ptr(), GS + 4 * run[0], GA + 4 * run[0],
+                self.B)))
+        else:
+            rows = [[self.wdfrag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
+                     self.relu_mask[i - 1].data_ptr()] for i in run]
+            self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+            self._bwd_pre.append((self.h.conv_stack2, (self.h.EPI_DGRAD,
+                                                      self._dstack_table.ctypes.data, len(run),
+                                                      self.dz[run[0]].data_ptr(),
+                                                      self.plans[run[0]].KPd, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
             self._bwd[i] = self._bwd[i][:3]
         # the remaining per-layer dgrads below the stack (layer 1 -> dZ_0) right after it, so
@@ -819,14 +858,20 @@ class HipGoNet:
         if self.fp8:
             self.h.fp8_update_scales(len(self.plans), self.fp8_scales.data_ptr(),
                                      self.fp8_amax_w.data_ptr(), self.fp8_amax.data_ptr(), 1.05,
-                                     self.fp8_sat.data_ptr(), s)
+                                     self.fp8_sat.data_ptr(), self.fp8_gscales.data_ptr(),
+                                     self.fp8_gamax.data_ptr(), s)
 
     def calibrate_fp8(self):
-        """Forwards on the current inputs to observe activation ranges, then derive the
-        fp8 scales (called automatically on the first batch of an fp8 model)."""
+        """Forward(+backward) passes on the current inputs to observe activation (and, with
+        the fp8 backward-data stack, gradient) ranges, then derive the fp8 scales (called
+        automatically on the first batch of an fp8 model).  Three passes: each layer's range
+        is observed through inputs quantized with the scales of the pass before."""
         s = stream_handle()
-        for _ in range(2):
-            self.evaluate()
+        for _ in range(3):
+            if self.dstack_fp8:
+                self.forward_backward()
+            else:
+                self.evaluate()
             self._fp8_update(s)
             self.h.weight_refresh(self._refresh_table.ctypes.data, len(self._refresh_table), s)
         self.fp8_sat.zero_()   # the calibration passes start from unit scales

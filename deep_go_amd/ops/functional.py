@@ -326,7 +326,7 @@ def weight_refresh(w: torch.Tensor, cinp: int, KP: int, Mpad: int, KPd: int = 0,
         ff = torch.zeros(cout * k * k * cin, dtype=torch.bfloat16, device=w.device)
         fd = torch.zeros_like(ff)
     tbl = np.array([[w.data_ptr(), wf.data_ptr(), _ptr(wd), cout, cin, k * k, cinp, KP, KPd, 0,
-                     0, 0, 0, 0, 0, 0, _ptr(ff), _ptr(fd), 0]],
+                     0, 0, 0, 0, 0, 0, _ptr(ff), _ptr(fd), 0, 0]],
                    dtype=np.int64)
     h.weight_refresh(tbl.ctypes.data, 1, stream_handle())
     torch.cuda.synchronize()

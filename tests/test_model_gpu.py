@@ -380,8 +380,33 @@ def test_fp8_forward_model_tracks_bf16(layers, stack, ch, monkeypatch):
     lb, l8 = net_b.mean_loss().item(), net_8.mean_loss().item()
     assert abs(lb - l8) < 0.03 * abs(lb), (lb, l8)
     gb, g8 = net_b.grads, net_8.grads
-    assert ((g8 - gb).norm() / gb.norm()).item() < 0.15
+    # fp8 forward + (stack) e5m2 backward-data: ~1% cosine gap on a random-init net
+    assert ((g8 - gb).norm() / gb.norm()).item() < (0.2 if net_8.dstack_fp8 else 0.15)
     assert torch.isfinite(net_8.fp8_scales).all() and (net_8.fp8_scales > 0).all()
+
+
+@pytest.mark.parametrize("layers,ch", [(6, 128), (5, 256)])
+def test_fp8_dgrad_stack_vs_bf16_dgrad(layers, ch, monkeypatch):
+    """The e5m2 backward-data stack (DG_FP8_DGRAD=1, default with dtype='fp8') against the
+    same fp8-forward model with the bf16 dgrad stack: identical loss (same forward), weight
+    gradients within the e5m2 rounding noise, gradient scales finite powers of two."""
+    monkeypatch.setenv("DG_FP8_DGRAD", "0")
+    _, net_0, _ = _setup(layers, ch, 6, seed=5, dtype="fp8")
+    monkeypatch.setenv("DG_FP8_DGRAD", "1")
+    _, net_1, _ = _setup(layers, ch, 6, seed=5, dtype="fp8")
+    assert net_1.dstack_fp8 and not net_0.dstack_fp8 and net_1.stack_fp8
+    net_0.fp8_scales.copy_(net_1.fp8_scales)
+    net_0.forward_backward()
+    net_1.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(net_0.loss, net_1.loss)
+    g0, g1 = net_0.grads, net_1.grads
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 0.12, rel
+    gs = net_1.fp8_gscales
+    assert torch.isfinite(gs).all() and (gs > 0).all()
+    assert torch.equal(torch.exp2(torch.log2(gs).round()), gs)
+    assert int(net_1.fp8_sat.sum().item()) == 0
 
 
 def test_fp8_training_reduces_loss():

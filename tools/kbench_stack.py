@@ -52,15 +52,21 @@ def main():
     # the fp8 forward stack (conv_stack_f8) on the same shapes: e4m3 weights / image
     w8 = [LY.stack_frag_f8(torch.randint(0, 0x78, (C, 9, C), dtype=torch.uint8, device=dev))
           for _ in range(NL)]
-    scales = torch.full((2 * (NL + 1),), 0.01, device=dev)
+    sc = torch.full((NL + 1,), 2.0 ** -6, device=dev)
     amax = torch.zeros(NL + 1, dtype=torch.int32, device=dev)
-    t8 = np.array([[w8[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr()]
-                   for i in range(NL)], dtype=np.int64)
+    t8 = np.array([[w8[i].data_ptr(), pbs[i].data_ptr(), ys[i].data_ptr(), ms[i].data_ptr(),
+                    sc.data_ptr() + 4 * i, sc.data_ptr() + 4 * i, sc.data_ptr() + 4 * (i + 1),
+                    amax.data_ptr() + 4 * (i + 1)] for i in range(NL)], dtype=np.int64)
 
-    def run8(mode=0, nl=NL):
+    t8d = t8.copy()
+    t8d[:, 1] = 0
+
+    def run8(mode=0, nl=NL, epi=None):
+        tt = t8 if epi is None else t8d
+
         def f():
             h.conv_stack_f8_set_mode(mode)
-            h.conv_stack_f8(C, t8.ctypes.data, nl, x.data_ptr(), 1, scales.data_ptr(),
+            h.conv_stack_f8(C, epi or h.EPI_FWD, tt.ctypes.data, nl, x.data_ptr(), sc.data_ptr(),
                             amax.data_ptr(), B, s)
         return f
     flops = 2.0 * C * C * 9 * 361 * B * NL
@@ -71,6 +77,7 @@ def main():
         for m in abl:
             times.setdefault(f"fwd_mode{m}", []).append(round(timeit(run("fwd", m)), 1))
         times.setdefault("fp8_fwd", []).append(round(timeit(run8()), 1))
+        times.setdefault("fp8_dgrad", []).append(round(timeit(run8(epi=h.EPI_DGRAD)), 1))
         times.setdefault("fp8_fwd_1layer", []).append(round(timeit(run8(nl=1)), 1))
         times.setdefault("fp8_fwd_2layers", []).append(round(timeit(run8(nl=2)), 1))
         for m in ([2, 4, 6] if abl else []):
