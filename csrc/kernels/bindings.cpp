@@ -82,9 +82,7 @@ hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* sc
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
-hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int splits, int M, int Mpad,
-                                 int KP, int taps, int cin, int cinp, int bchunks,
-                                 hipStream_t stream);
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, hipStream_t stream);
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
                                       hipStream_t s);
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
@@ -104,6 +102,7 @@ hipError_t dg_expand_features(const uint8_t* planes, const uint8_t* player, cons
 hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* part,
                                 hipStream_t s);
 int dg_bias_chunks(int B);
+int dg_bias_chunks_multi(int B);
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
                   const float* gate, hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
@@ -263,12 +262,10 @@ PYBIND11_MODULE(_dghip, m) {
                           S(stream)),
           "frame_to_fp8");
   });
-  m.def("wgrad_reduce_multi", [](uintptr_t table, int nl, int splits, int M, int Mpad, int KP,
-                                 int taps, int cin, int cinp, int bchunks, uintptr_t stream) {
-    check(dg_wgrad_reduce_multi(P<long long>(table), nl, splits, M, Mpad, KP, taps, cin, cinp,
-                                bchunks, S(stream)),
-          "wgrad_reduce_multi");
-  });
+  m.def("wgrad_reduce_multi", [](uintptr_t table, int nl, uintptr_t stream) {
+    check(dg_wgrad_reduce_multi(P<long long>(table), nl, S(stream)), "wgrad_reduce_multi");
+  }, "slab reduce + bias pass 2 of nl layers: table rows {slab, out, bpart, gposb, gbias, "
+     "splits, M, Mpad, KP, taps, cin, cinp, bchunks}");
   m.def("bias_grad_partial_multi", [](uintptr_t table, int nl, int B, int C, int pad,
                                       uintptr_t stream) {
     check(dg_bias_grad_partial_multi(P<long long>(table), nl, B, C, pad, S(stream)),
@@ -309,6 +306,7 @@ PYBIND11_MODULE(_dghip, m) {
           "bias_grad_partial");
   });
   m.def("bias_chunks", [](int B) { return dg_bias_chunks(B); });
+  m.def("bias_chunks_multi", [](int B) { return dg_bias_chunks_multi(B); });
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
                   uintptr_t gate, uintptr_t stream) {
     check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, P<float>(gate), S(stream)),

@@ -643,23 +643,27 @@ conv_wgrad_t3_kernel(WgradArgs a, WgradLayers Ls) {
 // several loads are in flight; the slabs are normally still resident in the Infinity
 // Cache when this runs.
 constexpr int RD_MAXL = 16;
-struct ReduceLayers {  // blockIdx.y = layer (several same-shape layers in one launch)
+struct ReduceLayers {  // blockIdx.y = layer (several layers, each with its own shape)
   const float* slab[RD_MAXL];
   float* out[RD_MAXL];
   const float* bpart[RD_MAXL];
   float* gposb[RD_MAXL];
   float* gbias[RD_MAXL];
+  int splits[RD_MAXL], M[RD_MAXL], Mpad[RD_MAXL], KP[RD_MAXL], taps[RD_MAXL], cin[RD_MAXL],
+      cinp[RD_MAXL], bchunks[RD_MAXL], main_blocks[RD_MAXL];
 };
-__global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(ReduceLayers Ls, int splits, int M, int Mpad, int KP, int taps, int cin,
-                    int cinp, int bchunks, int main_blocks) {
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
   const int ly = blockIdx.y;
   const float* __restrict__ slab = Ls.slab[ly];
   float* __restrict__ out = Ls.out[ly];
   const float* __restrict__ bpart = Ls.bpart[ly];
   float* __restrict__ gposb = Ls.gposb[ly];
   float* __restrict__ gbias = Ls.gbias[ly];
-  const int pos_blocks = (NPTS * M + 255) / 256;
+  const int splits = Ls.splits[ly], M = Ls.M[ly], Mpad = Ls.Mpad[ly], KP = Ls.KP[ly];
+  const int taps = Ls.taps[ly], cin = Ls.cin[ly], cinp = Ls.cinp[ly];
+  const int bchunks = Ls.bchunks[ly], main_blocks = Ls.main_blocks[ly];
+  const int pos_blocks = bpart ? (NPTS * M + 255) / 256 : 0;
+  if ((int)blockIdx.x >= main_blocks + pos_blocks + (bpart ? M : 0)) return;  // (shorter layer)
   if ((int)blockIdx.x >= main_blocks + pos_blocks) {
     // gbias[c] = sum over (chunk, row) of rowpart; one workgroup per channel
     __shared__ float s_r[4];
@@ -938,45 +942,58 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
   return launch_t3(kw, a, Ls, stream);
 }
 
+static void reduce_layer(ReduceLayers& Ls, int i, const float* slab, float* out,
+                         const float* bpart, float* gposb, float* gbias, int splits, int M,
+                         int Mpad, int KP, int taps, int cin, int cinp, int bchunks) {
+  int blocks = (M * (KP / 4) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  Ls.slab[i] = slab;
+  Ls.out[i] = out;
+  Ls.bpart[i] = bpart;
+  Ls.gposb[i] = gposb;
+  Ls.gbias[i] = gbias;
+  Ls.splits[i] = splits;
+  Ls.M[i] = M;
+  Ls.Mpad[i] = Mpad;
+  Ls.KP[i] = KP;
+  Ls.taps[i] = taps;
+  Ls.cin[i] = cin;
+  Ls.cinp[i] = cinp;
+  Ls.bchunks[i] = bchunks;
+  Ls.main_blocks[i] = blocks;
+}
+static int reduce_grid_x(const ReduceLayers& Ls, int i) {
+  return Ls.main_blocks[i] + (Ls.bpart[i] ? (NPTS * Ls.M[i] + 255) / 256 + Ls.M[i] : 0);
+}
+
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
                            float* gposb, float* gbias, hipStream_t stream) {
-  const int total = M * (KP / 4);
-  int blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  const int extra = bpart ? (NPTS * M + 255) / 256 + M : 0;
   ReduceLayers Ls{};
-  Ls.slab[0] = slab;
-  Ls.out[0] = out;
-  Ls.bpart[0] = bpart;
-  Ls.gposb[0] = gposb;
-  Ls.gbias[0] = gbias;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra, 1), dim3(256), 0, stream, Ls,
-                     splits, M, Mpad, KP, taps, cin, cinp, bchunks, blocks);
+  reduce_layer(Ls, 0, slab, out, bpart, gposb, gbias, splits, M, Mpad, KP, taps, cin, cinp,
+               bchunks);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(reduce_grid_x(Ls, 0), 1), dim3(256), 0, stream,
+                     Ls);
   return hipGetLastError();
 }
 
-// Slab reduce + bias-gradient pass 2 of nl same-shape layers in one launch: table = nl
-// rows of {slab, out (weight grad), bpart, gposb, gbias}.
-hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int splits, int M, int Mpad,
-                                 int KP, int taps, int cin, int cinp, int bchunks,
-                                 hipStream_t stream) {
+// Slab reduce + bias-gradient pass 2 of nl layers (any shapes) in one launch: table = nl
+// rows of 13 int64 {slab, out (weight grad), bpart, gposb, gbias, splits, M, Mpad, KP, taps,
+// cin, cinp, bchunks}.
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, hipStream_t stream) {
   if (nl <= 0 || nl > RD_MAXL) return hipErrorInvalidValue;
-  const int total = M * (KP / 4);
-  int blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
   ReduceLayers Ls{};
+  int gx = 1;
   for (int i = 0; i < nl; ++i) {
-    Ls.slab[i] = (const float*)table[5 * i];
-    Ls.out[i] = (float*)table[5 * i + 1];
-    Ls.bpart[i] = (const float*)table[5 * i + 2];
-    Ls.gposb[i] = (float*)table[5 * i + 3];
-    Ls.gbias[i] = (float*)table[5 * i + 4];
-    if (!Ls.slab[i] || !Ls.out[i] || !Ls.bpart[i]) return hipErrorInvalidValue;
+    const long long* t = table + 13 * i;
+    if (!t[0] || !t[1] || !t[2] || t[5] <= 0 || t[6] <= 0 || t[8] % 4 != 0)
+      return hipErrorInvalidValue;
+    reduce_layer(Ls, i, (const float*)t[0], (float*)t[1], (const float*)t[2], (float*)t[3],
+                 (float*)t[4], (int)t[5], (int)t[6], (int)t[7], (int)t[8], (int)t[9],
+                 (int)t[10], (int)t[11], (int)t[12]);
+    gx = gx > reduce_grid_x(Ls, i) ? gx : reduce_grid_x(Ls, i);
   }
-  const int extra = (NPTS * M + 255) / 256 + M;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks + extra, nl), dim3(256), 0, stream, Ls,
-                     splits, M, Mpad, KP, taps, cin, cinp, bchunks, blocks);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, nl), dim3(256), 0, stream, Ls);
   return hipGetLastError();
 }
 

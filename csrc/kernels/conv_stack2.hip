@@ -91,8 +91,32 @@ DG_DEV void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> packed bf16 (RNE, v_cvt_pk_bf16_f32)
+DG_DEV uint32_t bf16x2_bits(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+// ... then ReLU as a packed int16 max with 0 (v_pk_max_i16)
+DG_DEV uint32_t relu_bf16x2(f32x2 v) {
+  const s16x2 h = __builtin_bit_cast(s16x2, __builtin_convertvector(v, bf16x2v));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, s16x2{0, 0}));
+}
+// packed bf16 pair -> two fp32
+DG_DEV f32x2 bf16x2_f32(uint32_t u) {
+  return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+}
+// bits 0 / 1 of nib -> 0xffff / 0xffff0000 halves (v_bfe_i32 x 2 + v_perm_b32)
+DG_DEV uint32_t pair_mask(uint32_t nib) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)nib, 0, 1);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)nib, 1, 1);
+  return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
+}
+
 // MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop
+// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop; 16 = two
+// branch-free K loops (exact waits; slower, kept for the A/B)
 template <int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -180,15 +204,14 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     const int f = (h + 1) * F + (w + 1);
     *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
     if (EPI == EPI_FWD && Lo.mask) {
-      // bit per nonzero bf16 half (as the gates test it): packed min(x, 1) per half
-      typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-      auto nz2 = [](uint32_t x) {
-        const us2 m = __builtin_elementwise_min(__builtin_bit_cast(us2, x), us2{1, 1});
-        const uint32_t t = __builtin_bit_cast(uint32_t, m);
-        return (t | (t >> 15)) & 3u;
-      };
-      Lo.mask[((size_t)b * NPTS + p) * 16 + co_q] =
-          (uint8_t)(nz2(v.x) | (nz2(v.y) << 2) | (nz2(v.z) << 4) | (nz2(v.w) << 6));
+      // bit per nonzero bf16 half (post-ReLU: every half is in [0, 0x7fff]): h + 0x7fff has
+      // bit 15 set iff h != 0, with no carry out of the half; gather bits 15 / 31 of the
+      // four words to channel order (bit 2k: word k low half, 2k + 1: its high half)
+      const uint32_t m = (((v.x + 0x7fff7fffu) >> 15) & 0x10001u) |
+                         (((v.y + 0x7fff7fffu) >> 13) & 0x40004u) |
+                         (((v.z + 0x7fff7fffu) >> 11) & 0x100010u) |
+                         (((v.w + 0x7fff7fffu) >> 9) & 0x400040u);
+      Lo.mask[((size_t)b * NPTS + p) * 16 + co_q] = (uint8_t)(m | (m >> 15));
     }
   };
 
@@ -216,13 +239,7 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     // loads the compiler counts; the sched_barriers pin where they issue (left alone, the
     // scheduler sinks them next to their consumer).  The copy-out store goes last, after
     // the loads, so waiting for a load never waits for a store issued after it.
-    // Rolled on purpose: the compiler's wait at the loop head is then vmcnt(0) (the k-half-1
-    // loads and the copy-out stores of the previous step drain there), and unrolled by 2 or
-    // 3 every wait names exactly the loads it needs, yet measured 267 / 279 us vs 233 us
-    // for the 10-layer forward (profiles/r2_kbench_stack2.json: with precise waits the
-    // copy-out stores pile up behind the loads, 60 vs 20 us of copy-out cost)
-#pragma unroll 1
-    for (int s = 0; s < NSTEP; ++s) {
+    auto kstep = [&](const int s, const bool co) {
       // (past the last step of the last layer: a harmless re-load of step 0)
       const char* An = s + 1 < NSTEP ? L.A + (s + 1) * STEP_BYTES : A_next;
       bf16x8 bfr[NF];
@@ -230,28 +247,54 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       mma(Ak[0], bfr, acc);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!(MODE & 2)) load_A(An, 0, Ak[0]);
-      if (!(MODE & 4) && co_on && s < CO_STEPS) co_v = co_read(s);
+      if (co) co_v = co_read(s);
       if constexpr (!(MODE & 8)) read_B(s, 1, bfr);
       __builtin_amdgcn_sched_barrier(0);
       mma(Ak[1], bfr, acc);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!(MODE & 2)) load_A(An, 1, Ak[1]);
-      if (!(MODE & 4) && co_on && s < CO_STEPS) co_store(s, co_v, Lprev);
+      if (co) co_store(s, co_v, Lprev);
       __builtin_amdgcn_sched_barrier(0);
+    };
+    // One rolled loop with a per-step copy-out branch.  The compiler's wait at its head is
+    // then vmcnt(0) (the k-half-1 loads of the step before and its copy-out store drain
+    // there); measured faster than every variant with exact waits: two branch-free loops
+    // (copy-out steps / the rest, MODE 16: fwd 229 -> 234 us, dgrad 216 -> 224 us) and
+    // unrolled by 2 or 3 (267 / 279 us; profiles/r2_kbench_stack2.json).
+    int s = 0;
+    if constexpr (!(MODE & 16)) {
+#pragma unroll 1
+      for (; s < NSTEP; ++s) kstep(s, !(MODE & 4) && co_on && s < CO_STEPS);
+    } else {
+      if (!(MODE & 4) && co_on) {
+#pragma unroll 1
+        for (; s < CO_STEPS; ++s) {
+          int tt = s;
+          asm volatile("" : "+s"(tt));
+          kstep(tt, true);
+        }
+      }
+#pragma unroll 1
+      for (; s < NSTEP; ++s) kstep(s, false);
     }
 
     // ---- epilogue: write the layer's output back into the LDS image ----
     // every global load of the epilogue is issued before the first use
-    uint2 eu[NF][EPI == EPI_FWD ? MF : 1];
+    // (an opaque zero in the addresses: otherwise the compiler hoists all per-fragment
+    // table addresses out of the layer loop and spills them)
+    int z0 = 0;
+    asm volatile("" : "+v"(z0));
+    uint2 eb[NF][EPI == EPI_FWD ? MF : 1];
+    uint2 em[NF];
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
       if constexpr (EPI == EPI_FWD) {
-        const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane;
+        const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
 #pragma unroll
-        for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+        for (int i = 0; i < MF; ++i) eb[j][i] = pf[i * 64];
       } else {  // 64 channel bits of this wave's image half
-        eu[j][0] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8);
+        em[j] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8 + z0);
       }
     }
     lds_barrier();  // every wave is past its last read of this layer's image
@@ -262,24 +305,22 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
-        f32x4 v = acc[i][j];
-        if constexpr (EPI == EPI_FWD) {
-          const uint2 u = eu[j][i];
-          v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
-          v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
-          v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
-          v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
-        } else {
-          const uint32_t word = (cl < 32) ? eu[j][0].x : eu[j][0].y;
-          const uint32_t bits = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] : 0.f;
-        }
+        const f32x4 v = acc[i][j];
         uint2 o;
-        o.x = pack_bf16x2(v[0], v[1]);
-        o.y = pack_bf16x2(v[2], v[3]);
+        if constexpr (EPI == EPI_FWD) {
+          // packed fp32 bias add, bf16 pack, ReLU on the packed bf16 (max as int16: the
+          // same as relu before the rounding, -0 included)
+          o.x = relu_bf16x2(f32x2{v[0], v[1]} + bf16x2_f32(eb[j][i].x));
+          o.y = relu_bf16x2(f32x2{v[2], v[3]} + bf16x2_f32(eb[j][i].y));
+        } else {
+          // the 4 ReLU bits of these channels gate the bf16 pairs
+          const uint32_t word = (i < 2) ? em[j].x : em[j].y;
+          const uint32_t nib = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
+          o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
+          o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
+        }
         const int slot = (cl >> 3) ^ (int)(pk[j] >> 16);
-        if (p < NPTS) *(uint2*)(sH + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
+        if (p < NPTS) *(uint2*)(sH + z0 + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
       }
     }
     lds_barrier();  // the next layer's input is complete
@@ -335,6 +376,7 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     a.head = *head;
   }
   if (epi == EPI_DGRAD) {
+    if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16>(a, B, stream);
     return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
   }
   switch (g_stack2_mode) {  // forward: the MODE ablations too (kbench_stack.py)
@@ -343,6 +385,7 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     case 14: return launch_stack2<EPI_FWD, 14>(a, B, stream);
     case 4: return launch_stack2<EPI_FWD, 4>(a, B, stream);
     case 10: return launch_stack2<EPI_FWD, 10>(a, B, stream);
+    case 16: return launch_stack2<EPI_FWD, 16>(a, B, stream);
     default: return launch_stack2<EPI_FWD, 0>(a, B, stream);
   }
 }

@@ -363,17 +363,18 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       asm volatile("" : "+v"(z0));
       // EPI_FWD: bias table pieces; EPI_DGRAD: the 64 ReLU bits (of the layer below) of this
       // wave's channels per pixel fragment
-      uint2 eu[NF][EPI == EPI_FWD ? MF : 1];
+      uint2 eb[NF][EPI == EPI_FWD ? MF : 1];
+      uint2 em[NF];
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         if constexpr (EPI == EPI_FWD) {
           const uint2* pf = (const uint2*)L.pbias + hp * (24 * 2 * 4 * 64) +
                             ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
 #pragma unroll
-          for (int i = 0; i < MF; ++i) eu[j][i] = pf[i * 64];
+          for (int i = 0; i < MF; ++i) eb[j][i] = pf[i * 64];
         } else {
           const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
-          eu[j][0] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * (C / 8) + 16 * hp + 8 * wm + z0);
+          em[j] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * (C / 8) + 16 * hp + 8 * wm + z0);
         }
       }
       // C = 128 and the last pass of C = 256: every wave is past its last read of the
@@ -400,14 +401,14 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         for (int i = 0; i < MF; ++i) {
           f32x4 v = acc[i][j];
           if constexpr (EPI == EPI_FWD) {
-            const uint2 u = eu[j][i];
+            const uint2 u = eb[j][i];
             v[0] = fmaxf(v[0] * deq + __uint_as_float(u.x << 16), 0.f);
             v[1] = fmaxf(v[1] * deq + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
             v[2] = fmaxf(v[2] * deq + __uint_as_float(u.y << 16), 0.f);
             v[3] = fmaxf(v[3] * deq + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
           } else {
             const int cw = i * 16 + lq * 4;                // channel within the wave's 64
-            const uint32_t word = (cw < 32) ? eu[j][0].x : eu[j][0].y;
+            const uint32_t word = (cw < 32) ? em[j].x : em[j].y;
             const uint32_t bits = word >> ((cw & 31) >> 3 << 3) >> (cw & 4);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = ((bits >> r) & 1u) ? v[r] * deq : 0.f;

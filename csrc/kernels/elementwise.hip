@@ -81,20 +81,23 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
 // the chunk) and writes plain coalesced partials — no atomics, deterministic.  Pass 2
 // (sum over chunks -> gposb, gbias) runs inside the wgrad slab-reduce launch.
 // Reference: nn.Add / conv bias backward (experiments.lua:138,144).
-constexpr int BG_BT = 16;
+constexpr int BG_BT = 16;   // boards per chunk of a single-layer launch
+constexpr int BG_BT_MULTI = 64;  // ... of a multi-layer launch (enough workgroups from the
+                            // layers: 4x fewer partials for the slab reduce to read)
+constexpr int BG_LD = 16;   // 16-B loads in flight per thread
 constexpr int BG_MAXL = 16;
 struct BiasLayers {  // blockIdx.z = layer (several same-shape layers in one launch)
   const char* dZ[BG_MAXL];
   float* part[BG_MAXL];
 };
 __global__ void __launch_bounds__(1024)
-bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
+bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int bt) {
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
   const int h = blockIdx.x;
   const int chunk = blockIdx.y;
   const char* __restrict__ dZ = Ls.dZ[blockIdx.z];
   float* __restrict__ part = Ls.part[blockIdx.z];
-  const int b0 = chunk * BG_BT;
+  const int b0 = chunk * bt;
   const int G = C / 8;
   const int F = BOARD + 2 * pad;
   const int items = BOARD * G;  // (w, g) pairs of the row
@@ -108,19 +111,21 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
     const int w = it / G, g = it - (it / G) * G;
     const char* src = row0 + ((size_t)w * C + g * 8) * 2;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    uint4 v[BG_BT];
+    for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
+      uint4 v[BG_LD];
 #pragma unroll
-    for (int j = 0; j < BG_BT; ++j) {
-      const int b = b0 + j;
-      v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
-    }
+      for (int j = 0; j < BG_LD; ++j) {
+        const int b = b0 + jb + j;
+        v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
+      }
 #pragma unroll
-    for (int j = 0; j < BG_BT; ++j) {
-      const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      for (int j = 0; j < BG_LD; ++j) {
+        const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[2 * e] += __uint_as_float(u[e] << 16);
-        acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(u[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+        }
       }
     }
     f32x4* dst = (f32x4*)(prow + w * C + g * 8);
@@ -422,15 +427,16 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
   Ls.dZ[0] = (const char*)dZ;
   Ls.part[0] = part;
   hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, 1), dim3(threads),
-                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
+                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT);
   return hipGetLastError();
 }
 
-// Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part}.
+// Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part};
+// chunks of BG_BT_MULTI boards (dg_bias_chunks_multi).
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
                                       hipStream_t s) {
   if (C % 8 != 0 || C > 2048 || nl <= 0 || nl > BG_MAXL) return hipErrorInvalidValue;
-  const int nchunks = (B + BG_BT - 1) / BG_BT;
+  const int nchunks = (B + BG_BT_MULTI - 1) / BG_BT_MULTI;
   int threads = (BOARD * (C / 8) + 63) / 64 * 64;
   if (threads > 1024) threads = 1024;
   if (threads < 64) threads = 64;
@@ -440,10 +446,11 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
     Ls.part[i] = (float*)table[2 * i + 1];
   }
   hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, nl), dim3(threads),
-                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
+                     (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);
   return hipGetLastError();
 }
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
+int dg_bias_chunks_multi(int B) { return (B + BG_BT_MULTI - 1) / BG_BT_MULTI; }
 
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
                   const float* gate, hipStream_t s) {

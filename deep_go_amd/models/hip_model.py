@@ -223,7 +223,8 @@ class HipGoNet:
         self.side_mode = {"0": "none"}.get(side_mode, side_mode)
         if self.side_mode not in ("none", "bias"):
             raise ValueError(f"DG_SIDE_STREAM={side_mode!r}: expected 0 or bias")
-        self.bchunks = self.h.bias_chunks(batch)
+        self.bchunks = self.h.bias_chunks(batch)            # per-layer bias partials
+        self.bchunks_g = self.h.bias_chunks_multi(batch)    # grouped (multi-layer) ones
         slab = torch.empty(max(p.splits * p.Mpad_w * p.KPw for p in self.plans),
                            dtype=torch.float32, device=dev)
         cmax = max(p.cout for p in self.plans)
@@ -680,7 +681,7 @@ class HipGoNet:
             plan_splits[tuple(g)] = S
             gslab_elems = max(gslab_elems, len(g) * S * p.Mpad_w * p.KPw)
         self.gslab = torch.empty(gslab_elems, dtype=torch.float32, device=self.device)
-        bpart_per = self.bchunks * (NUM_POINTS + 19) * max(self.plans[g[0]].cout for g in groups)
+        bpart_per = self.bchunks_g * (NUM_POINTS + 19) * max(self.plans[g[0]].cout for g in groups)
         self.gbpart = torch.empty(G * bpart_per, dtype=torch.float32, device=self.device)
         G_ = self.grads.data_ptr()
         f4 = 4
@@ -699,7 +700,8 @@ class HipGoNet:
                 wrows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
                 brows.append([self.dz[i].data_ptr(), bpart])
                 rrows.append([slab, G_ + spec.w_off * f4, bpart, G_ + spec.pos_off * f4,
-                              G_ + spec.b_off * f4])
+                              G_ + spec.b_off * f4, S, p0.cout, p0.Mpad_w, p0.KPw,
+                              p0.k * p0.k, p0.cin, p0.cinp, self.bchunks_g])
                 self.plans[i].splits = S
                 # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
                 # launches all three passes for the whole group
@@ -709,7 +711,7 @@ class HipGoNet:
             self._wgroup_tables.extend(tabs)
             wt, bt, rt = tabs
             self._bwd[g[0]][0:3] = [
-                (h.bias_grad_partial_multi, (bt.ctypes.data, len(g), self.B, p0.cout,
+                (h.bias_grad_partial_multi, (bt.ctypes.data, len(bt), self.B, p0.cout,
                                              self.dzp[g[0]])),
                 (h.conv_wgrad_win, (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp,
                                     self.B, p0.KPw, S))
@@ -717,8 +719,7 @@ class HipGoNet:
                 (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
                                       S)),
-                (h.wgrad_reduce_multi, (rt.ctypes.data, len(g), S, p0.cout, p0.Mpad_w, p0.KPw,
-                                        p0.k * p0.k, p0.cin, p0.cinp, self.bchunks)),
+                (h.wgrad_reduce_multi, (rt.ctypes.data, len(rt))),
             ]
 
     # ------------------------------------------------------------------ execution
@@ -764,8 +765,7 @@ class HipGoNet:
         self._run(self._fwd_train, s)
         f, a = self._head_train
         f(*a, s)
-        f, a = self._head_red
-        f(*a, s)
+        self.head_reduce()
         self._run(self._bwd_pre, s)
         hooks = dict()
         for li, fn in self.grad_hooks:
@@ -775,6 +775,13 @@ class HipGoNet:
         for i in range(self.L - 2, -1, -1):
             self.backward_layer(i, hooks.get(i, ()))
         self.join_side()
+
+    def head_reduce(self):
+        """The head's weight / bias gradient reduce over the fused head's per-board partials
+        (main stream: on the side stream, beside the backward-data stack it could not
+        co-schedule and the step measured 1% slower)."""
+        f, a = self._head_red
+        f(*a, stream_handle())
 
     def backward_layer(self, i: int, hooks=()):
         """Layer i's backward: bias grads + wgrad + slab reduce (final grads of layer i, then
@@ -935,7 +942,7 @@ class SegmentedStep:
         emit(lambda: net._run(net._pre, stream_handle()))
         emit(lambda: net._run(net._fwd_train, stream_handle()))
         emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
-        emit(lambda: net._head_red[0](*net._head_red[1], stream_handle()))
+        emit(net.head_reduce)
         emit(lambda: net._run(net._bwd_pre, stream_handle()))
         if net.L - 1 in fire_after:
             segs.append((cur, fire_after[net.L - 1]))

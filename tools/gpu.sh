@@ -15,6 +15,8 @@
 #                    a per-kernel summary (tools/pmc_summary.py)
 #   pmcpy:SCRIPT     the pmc counters (+ LDS wait / LDS-active) over python SCRIPT (a kernel
 #                    micro-benchmark) -> gpurun_out/pmcpy_<n>/ and a per-kernel summary
+#   pmcx:C1,C2,..:SCRIPT  one rocprofv3 --pmc pass of the listed counters over python SCRIPT
+#   list             rocprofv3 -L -> gpurun_out/counters.txt
 #   py:SCRIPT ARGS   python SCRIPT ARGS (a tools/ script), stdout -> gpurun_out/py_<n>.log
 #   ab:R:A|B|...     R interleaved rounds of bench.py under env settings A, B, ... ("-" = none)
 set -o pipefail
@@ -68,6 +70,16 @@ for step in "$@"; do
         f=$(find gpurun_out/pmcpy_$n -name '*counter_collection.csv' | head -1)
         python tools/pmc_summary.py "$f" > gpurun_out/pmcpy_$n.txt && cat gpurun_out/pmcpy_$n.txt
       fi ;;
+    pmcx)
+      # pmcx:COUNTERS(comma-separated):SCRIPT — one pass of the given counters over SCRIPT
+      C=$(echo "${arg%%:*}" | tr ',' ' ')
+      scr=${arg#*:}
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $C \
+        --output-format csv -d $R/gpurun_out/pmcx_$n -o run -- \
+        python3 $R/$scr > $R/gpurun_out/pmcx_$n.log 2>&1)
+      rc=$? ;;
+    list)
+      timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$? ;;
     py)
       timeout -k 10 600 python $arg > gpurun_out/py_$n.log 2>&1
       rc=$?; tail -5 gpurun_out/py_$n.log ;;
