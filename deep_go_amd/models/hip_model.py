@@ -254,8 +254,12 @@ class HipGoNet:
         self.head_dzb = torch.zeros((B, NUM_POINTS), dtype=torch.float32, device=dev)
 
         self.side = torch.cuda.Stream(device=dev) if self.side_mode != "none" else None
+        self._head_red_defer = False
+        self._head_red_pending = False
         self._refresh_table = self._build_refresh_table()
         self._build_plans()
+        self._head_red_defer = (self.side_mode == "bias" and bool(self.wgroups)
+                                and os.environ.get("DG_HEAD_RED_DEFER", "1") != "0")
         self.refresh_weights()
         self.grad_hooks: List[Tuple[int, Callable[[], None]]] = []  # (after bwd layer i, fn)
 
@@ -770,6 +774,8 @@ class HipGoNet:
         hooks = dict()
         for li, fn in self.grad_hooks:
             hooks.setdefault(li, []).append(fn)
+        if hooks.get(self.L - 1):
+            self.join_side()            # the head's gradients final (deferred reduce)
         for fn in hooks.get(self.L - 1, []):
             fn()
         for i in range(self.L - 2, -1, -1):
@@ -777,11 +783,22 @@ class HipGoNet:
         self.join_side()
 
     def head_reduce(self):
-        """The head's weight / bias gradient reduce over the fused head's per-board partials
-        (main stream: on the side stream, beside the backward-data stack it could not
-        co-schedule and the step measured 1% slower)."""
+        """The head's weight / bias gradient reduce over the fused head's per-board partials.
+        Nothing before the optimizer reads it.  With the side stream and grouped weight
+        gradients it is deferred (DG_HEAD_RED_DEFER=1): the first group's side-stream work
+        runs it beside the grouped wgrad launch, whose 2-per-CU grid leaves CUs free (it does
+        not co-schedule beside the backward-data stack: run there the step was 1% slower)."""
+        if self._head_red_defer:
+            self._head_red_pending = True
+            return
         f, a = self._head_red
         f(*a, stream_handle())
+
+    def _flush_head_reduce(self, stream):
+        if self._head_red_pending:
+            self._head_red_pending = False
+            f, a = self._head_red
+            f(*a, stream)
 
     def backward_layer(self, i: int, hooks=()):
         """Layer i's backward: bias grads + wgrad + slab reduce (final grads of layer i, then
@@ -802,6 +819,7 @@ class HipGoNet:
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
+                self._flush_head_reduce(side.cuda_stream)
                 self._run(ops[:1], side.cuda_stream)
                 ev = side.record_event()         # partials ready for the reduce
                 if l0_side:                      # then dZ_0 and the first layer's whole
@@ -815,6 +833,7 @@ class HipGoNet:
         self._run(ops[3:], main.cuda_stream)
 
     def join_side(self):
+        self._flush_head_reduce(stream_handle())
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
 
@@ -945,6 +964,7 @@ class SegmentedStep:
         emit(net.head_reduce)
         emit(lambda: net._run(net._bwd_pre, stream_handle()))
         if net.L - 1 in fire_after:
+            emit(net.join_side)               # the head's gradients final (deferred reduce)
             segs.append((cur, fire_after[net.L - 1]))
             cur = []
         for i in range(net.L - 2, -1, -1):
