@@ -37,9 +37,9 @@ hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void*
                                      float* loss, int* pred, void* dZ, float* gw_part,
                                      float* dzb, int head_relu, float grad_scale,
                                      hipStream_t stream);
-hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
+hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                           hipStream_t stream);
-hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
+hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int l1, int B,
                                    const float* w, const float* bias, const float* posb,
                                    const int* labels, float* loss, int* pred, void* dZ,
                                    float* gw_part, float* dzb, int head_relu, float grad_scale,
@@ -60,7 +60,7 @@ int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
 void dg_conv_l1_set_nw(int nw);
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
-                      void* mask, hipStream_t stream);
+                      void* mask, const void* pbias, hipStream_t stream);
 void dg_conv_wgrad_win_set_ablate(int mode);
 void dg_conv_wgrad_win_set_pd(int pd);
 void dg_conv_wgrad_win_set_nw(int nw);
@@ -175,20 +175,18 @@ PYBIND11_MODULE(_dghip, m) {
         },
         "conv_board + optional bf16 bias table (fwd) and ReLU bitmask (fwd writes, dgrad reads)");
   // conv_stack2.hip: weights streamed into VGPRs (fragment-ordered), no per-K-step barrier.
-  // Same signatures as conv_stack* (KP unused: the fragment layout is fixed for C = 128).
-  m.def("conv_stack2_fwd", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+  // l1 = 1: table row 0 is the network's first layer (5x5 over the 23x23x40 input frame X0)
+  m.def("conv_stack2_fwd", [](uintptr_t table, int nl, uintptr_t X0, int l1, int B,
                               uintptr_t stream) {
-    (void)KP;
-    check(dg_conv_stack2(1, P<long long>(table), nl, P<void>(X0), B, S(stream)),
+    check(dg_conv_stack2(1, P<long long>(table), nl, P<void>(X0), l1, B, S(stream)),
           "conv_stack2_fwd");
-  }, "conv_stack2 forward: table rows {A_frag, pbias_frag, Y, mask}");
-  m.def("conv_stack2_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+  }, "conv_stack2 forward: table rows {A_frag, pbias_frag, Y, mask}; l1: row 0 = first layer");
+  m.def("conv_stack2_fwd_head", [](uintptr_t table, int nl, uintptr_t X0, int l1, int B,
                                    uintptr_t w, uintptr_t bias, uintptr_t posb, uintptr_t labels,
                                    uintptr_t loss, uintptr_t pred, uintptr_t dZ, uintptr_t gw_part,
                                    uintptr_t dzb, int head_relu, float grad_scale,
                                    uintptr_t stream) {
-    (void)KP;
-    check(dg_conv_stack2_fwd_head(P<long long>(table), nl, P<void>(X0), B, P<float>(w),
+    check(dg_conv_stack2_fwd_head(P<long long>(table), nl, P<void>(X0), l1, B, P<float>(w),
                                   P<float>(bias), P<float>(posb), P<int>(labels), P<float>(loss),
                                   P<int>(pred), P<void>(dZ), P<float>(gw_part), P<float>(dzb),
                                   head_relu, grad_scale, S(stream)),
@@ -219,10 +217,9 @@ PYBIND11_MODULE(_dghip, m) {
         "conv_stack_f8 timing-ablation mode (0 = production)");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
         "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
-  m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int KP, int B,
+  m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int l1, int B,
                           uintptr_t stream) {
-    (void)KP;
-    check(dg_conv_stack2(epi, P<long long>(table), nl, P<void>(X0), B, S(stream)),
+    check(dg_conv_stack2(epi, P<long long>(table), nl, P<void>(X0), l1, B, S(stream)),
           "conv_stack2");
   }, "conv_stack2: EPI_FWD forward or EPI_DGRAD backward-data chain (fragment-ordered A)");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
@@ -354,11 +351,12 @@ PYBIND11_MODULE(_dghip, m) {
   }, "weight gradients of several same-shape layers in one three-slice launch");
   m.def("conv_l1", [](int kw, uintptr_t A, int KP, int M, int Mpad, uintptr_t X, int x_pad,
                       int x_C, int B, uintptr_t Y, int y_pad, uintptr_t bias, uintptr_t posb,
-                      uintptr_t mask, uintptr_t stream) {
+                      uintptr_t mask, uintptr_t pbias, uintptr_t stream) {
     check(dg_conv_l1(kw, P<void>(A), KP, M, Mpad, P<void>(X), x_pad, x_C, B, P<void>(Y), y_pad,
-                     P<float>(bias), P<float>(posb), P<void>(mask), S(stream)),
+                     P<float>(bias), P<float>(posb), P<void>(mask), P<void>(pbias), S(stream)),
           "conv_l1");
-  }, "board-resident first-layer forward (conv_l1.hip): bias + position bias + ReLU");
+  }, "board-resident first-layer forward (conv_l1.hip): bias + position bias (fp32, or the "
+     "bf16 pbias table when given) + ReLU");
   m.def("conv_l1_set_nw", [](int nw) { dg_conv_l1_set_nw(nw); },
         "conv_l1 workgroup: 4 waves / half a board, 2 per CU (default) or 8 waves / a board");
   m.def("conv_l1_ok", [](int kw, int x_pad, int x_C, int Mpad, int KP) {

@@ -37,6 +37,9 @@ struct L1Args {
   int img_bytes;       // LDS image bytes (whole KB)
   uint8_t* mask;       // optional ReLU bitmask [B][361][M/8] (bit k of byte q: channel 8q+k
                        // nonzero) — lets the backward-data stack reach layer 1
+  const bf16_t* pbias; // optional: bf16(bias + posb) [361][M] in place of bias / posb (the
+                       // other forward epilogues' table: the same values as the forward
+                       // stack's fused first layer)
 };
 
 // NW = 8: one workgroup (board x 128 co) per CU, 3-deep weight ring.  NW = 4: a workgroup
@@ -149,16 +152,24 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_l1_kernel(L1Args a) {
     const int co = m_tile + wm * 64 + i * 16 + lq * 4;
     const bool co_ok = co < a.M;
     const int coc = co_ok ? co : 0;
-    const f32x4 bv = *(const f32x4*)(a.bias + coc);
+    const f32x4 bv = a.pbias ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(a.bias + coc);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = px0 + j * 16 + lr;
       const bool ok = co_ok && p < NPTS;
       const int pc = p < NPTS ? p : 0;
-      const f32x4 pv = *(const f32x4*)(a.posb + (size_t)pc * a.M + coc);
       f32x4 v = acc[i][j];
+      if (a.pbias) {
+        const uint2 u = *(const uint2*)(a.pbias + (size_t)pc * a.M + coc);
+        v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
+        v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xFFFF0000u), 0.f);
+        v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
+        v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xFFFF0000u), 0.f);
+      } else {
+        const f32x4 pv = *(const f32x4*)(a.posb + (size_t)pc * a.M + coc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bv[r] + pv[r], 0.f);
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bv[r] + pv[r], 0.f);
+      }
       uint2 o;
       o.x = pack_bf16x2(v[0], v[1]);
       o.y = pack_bf16x2(v[2], v[3]);
@@ -212,13 +223,15 @@ int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP) {
 
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
-                      void* mask, hipStream_t stream) {
+                      void* mask, const void* pbias, hipStream_t stream) {
   if (!dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP) || B <= 0 || M % 4 != 0 || M > Mpad ||
       (mask && M % 8 != 0))
     return hipErrorInvalidValue;
   const int F = BOARD + 2 * x_pad;
   L1Args a{(const bf16_t*)A, (const char*)X, (char*)Y, bias, posb, KP, M, x_C, y_pad, B,
-           kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024, (uint8_t*)mask};
+           kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024, (uint8_t*)mask,
+           (const bf16_t*)pbias};
+  if (!pbias && (!bias || !posb)) return hipErrorInvalidValue;
   static bool env_done = false;
   if (!env_done) {
     const char* e = getenv("DG_L1_NW");

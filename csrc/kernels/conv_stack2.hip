@@ -75,14 +75,30 @@ struct StackLayer {
   uint8_t* mask;        // [B][361][16] ReLU bits: EPI_FWD writes (optional), EPI_DGRAD reads
 };
 struct StackArgs {
-  const char* X0;       // input frame [B][21][21][128] bf16 of the first layer
+  const char* X0;       // input frame [B][21][21][128] bf16 of the first layer (l1: the
+                        // network input frame [B][23][23][40])
   int nl;
   int fuse_head;        // EPI_FWD: run the policy head on the final image
+  int l1;               // EPI_FWD: row 0 is the network's first layer (5x5, 40 -> 128 channels)
   StackLayer L[MAXL];
   dghead::HeadMArgs head;  // (head_body.h; X unused: the image is resident)
 };
 
 DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+
+// The network's first layer fused in front of the forward stack (l1 mode): 5x5 over the
+// zero-bordered 23x23 frame of the 37 input planes padded to 40 channels (80 B per pixel),
+// staged linearly into the (still unused) image area.  K runs over the 125 8-channel
+// (tap, chunk) groups padded to 128 (K = 1024 = 16 K-steps; the padding chunks have zero
+// weights): a lane's 8 K values are one chunk, so a 32-wide k-half mixes taps — conv_l1.hip's
+// scheme, with the weights fragment-ordered like the hidden layers' ([16][2][2][4][64] x 8,
+// k linear).  Layer 0's output is written into the image by the usual epilogue (the frame is
+// dead by then: every read precedes the epilogue's first barrier).
+constexpr int L1F = 23;
+constexpr int L1XB = 80;                        // bytes per pixel (40 bf16)
+constexpr int L1_BYTES = L1F * L1F * L1XB;       // 42320
+constexpr int L1_STEPS = 16;
+constexpr int L1_CHUNKS = 125;
 
 // s_waitcnt lgkmcnt(0) (LDS writes of this wave done), vmcnt/expcnt untouched, then barrier:
 // unlike __syncthreads() this does not drain the weight loads already in flight
@@ -128,7 +144,14 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   char* sH = smem + SCRATCH;  // image c at sH + c * H_BYTES
 
   // ---- prologue: the first layer's input frame (both 64-channel images) by LDS-DMA ----
-  {
+  if (EPI == EPI_FWD && a.l1) {   // (l1: a linear copy of the 23x23x40 frame, whole 1-KB
+                                  // blocks; the last block's tail re-reads the last 16 B)
+    const char* Xb = a.X0 + (size_t)b * L1_BYTES;
+    for (int blk = wave; blk < (L1_BYTES + 1023) / 1024; blk += NW) {
+      const int off = blk * 1024 + lane * 16;
+      glds16(Xb + (off < L1_BYTES ? off : L1_BYTES - 16), (LDS_AS void*)(sH + blk * 1024));
+    }
+  } else {
     const char* Xb = a.X0 + (size_t)b * FF * C * 2;
     for (int j = wave; j < 2 * (HROWS / 8); j += NW) {
       const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
@@ -177,6 +200,20 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       const int off = (int)(pk[j] & 0xFFFFu) + toff * 128 +
                       ((lq ^ (((int)(pk[j] >> 16) + tsig) & 7)) * 16);
       bfr[j] = lds_read_b128(sHc + (off ^ (kk * 64)));
+    }
+  };
+  // l1 mode, layer 0: B fragments of k-half kk of K-step s from the staged input frame
+  auto read_B1 = [&](int s, int kk, bf16x8 (&bfr)[NF]) {
+    int kc = s * 8 + kk * 4 + lq;          // this lane group's chunk (tap, c8)
+    if (kc >= L1_CHUNKS) kc = 0;          // padding chunks: zero weights
+    const int t = kc / 5, c8 = kc - (kc / 5) * 5;
+    const int koff = ((t / 5 - 2) * L1F + (t % 5 - 2)) * L1XB + c8 * 16;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      int p = wn * NF * 16 + j * 16 + lr;
+      if (p >= NPTS) p = 0;
+      const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+      bfr[j] = lds_read_b128((const LDS_AS char*)(sH + ((h + 2) * L1F + (w + 2)) * L1XB + koff));
     }
   };
   auto mma = [&](const bf16x8 (&af)[MF], const bf16x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
@@ -262,10 +299,24 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     // (copy-out steps / the rest, MODE 16: fwd 229 -> 234 us, dgrad 216 -> 224 us) and
     // unrolled by 2 or 3 (267 / 279 us; profiles/r2_kbench_stack2.json).
     int s = 0;
-    if constexpr (!(MODE & 16)) {
+    if (EPI == EPI_FWD && l == 0 && a.l1) {
+      // the fused first layer: 16 K-steps over the staged input frame (nothing to copy out)
 #pragma unroll 1
-      for (; s < NSTEP; ++s) kstep(s, !(MODE & 4) && co_on && s < CO_STEPS);
-    } else {
+      for (; s < L1_STEPS; ++s) {
+        const char* An = s + 1 < L1_STEPS ? L.A + (s + 1) * STEP_BYTES : A_next;
+        bf16x8 bfr[NF];
+        read_B1(s, 0, bfr);
+        mma(Ak[0], bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        load_A(An, 0, Ak[0]);
+        read_B1(s, 1, bfr);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(Ak[1], bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        load_A(An, 1, Ak[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (!(MODE & 16)) {
       if (!(MODE & 4) && co_on) {
 #pragma unroll 1
         for (; s < CO_STEPS; ++s) {
@@ -298,6 +349,16 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       }
     }
     lds_barrier();  // every wave is past its last read of this layer's image
+    if (EPI == EPI_FWD && l == 0 && a.l1) {
+      // the image area held the first layer's input frame: zero the 21x21 frame's border
+      // rows / columns (the next layer's taps read them) and the padding rows 441..447
+      for (int u = tid; u < 87 * 8 * 2; u += NT) {
+        const int img = u / (87 * 8), k = (u >> 3) % 87, q = u & 7;
+        const int row = k < 21 ? k : k < 42 ? 420 + (k - 21) : k < 61 ? (k - 41) * 21
+                        : k < 80 ? (k - 60) * 21 + 20 : 441 + (k - 80);
+        *(uint4*)(sH + img * H_BYTES + row * 128 + q * 16) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = wn * NF * 16 + j * 16 + lr;
@@ -352,11 +413,14 @@ hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
 
 int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
 
-hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int B,
+hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                          const dghead::HeadMArgs* head, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || B <= 0) return hipErrorInvalidValue;
   if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
+  if (l1 && (epi != EPI_FWD || nl < 2)) return hipErrorInvalidValue;
+  static_assert(L1_BYTES <= 2 * H_BYTES, "l1 frame in the image area");
   StackArgs a;
+  a.l1 = l1 ? 1 : 0;
   a.fuse_head = 0;
   a.head = dghead::HeadMArgs{};
   a.X0 = (const char*)X0;
@@ -399,20 +463,22 @@ void dg_conv_stack2_set_mode(int m) { g_stack2_mode = m; }
 // table: nl rows of {A (fragment-ordered weights), pbias_frag, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)
 //   epi 2 (dgrad)  : mask required (read; ReLU bits of the layer below), pbias unused
-hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int B,
+// l1 (EPI_FWD only): row 0 is the network's first layer (5x5 over the [B][23][23][40] input
+// frame X0; its A = the [128][1024] weights in fragment order, k linear)
+hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                           hipStream_t stream) {
-  return stack2_launch(epi, table, nl, X0, B, nullptr, stream);
+  return stack2_launch(epi, table, nl, X0, l1, B, nullptr, stream);
 }
 
 // Forward stack + the 3x3 / 128-channel policy head fused after its last layer.
-hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int B,
+hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int l1, int B,
                                    const float* w, const float* bias, const float* posb,
                                    const int* labels, float* loss, int* pred, void* dZ,
                                    float* gw_part, float* dzb, int head_relu, float grad_scale,
                                    hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return stack2_launch(EPI_FWD, table, nl, X0, B, &h, stream);
+  return stack2_launch(EPI_FWD, table, nl, X0, l1, B, &h, stream);
 }
 
 }  // extern "C"

@@ -145,6 +145,10 @@ class HipGoNet:
         self.wf8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wd8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         for p in self.plans:
+            if p.index == 0 and self._stack_l1_ok(p):
+                # the first layer fused in front of the forward stack (conv_stack2.hip l1
+                # mode): [128][1024] weights in fragment order (k linear), no dgrad operand
+                self.wfrag[0] = torch.zeros(128 * 1024, dtype=torch.bfloat16, device=dev)
             if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
                 self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
                                                   device=dev)
@@ -180,7 +184,8 @@ class HipGoNet:
         # forward epilogue bias table (bf16 bias + pos_bias, rebuilt by every weight refresh)
         # and ReLU bitmasks of the board-kernel outputs consumed by a board dgrad
         self.pbias = [torch.zeros((NUM_POINTS, p.cout), dtype=torch.bfloat16, device=dev)
-                      if p.board and not p.fp8 else None for p in self.plans]
+                      if (p.board and not p.fp8) or self._l1_res_ok(p) else None
+                      for p in self.plans]
         # the same table in the forward stacks' accumulator-fragment order (coalesced
         # epilogue loads), for every 128-channel board layer (bf16 or fp8)
         self.pbias_frag = [torch.zeros((p.cout // 128) * 24 * 2 * 4 * 64 * 4, dtype=torch.bfloat16,
@@ -330,7 +335,8 @@ class HipGoNet:
                                               p.Mpad, xin.data_ptr(), x_pad, p.cinp, self.B,
                                               self.act[p.index].data_ptr(), y_pad,
                                               P + spec.b_off * f4, P + spec.pos_off * f4,
-                                              msk.data_ptr() if msk is not None else 0)))
+                                              msk.data_ptr() if msk is not None else 0,
+                                              self.pbias[p.index].data_ptr())))
             else:
                 msk = self.relu_mask[p.index]
                 self._fwd.append((h.conv_nt_ex, (h.EPI_FWD, p.k, p.bm, p.bn,
@@ -376,8 +382,9 @@ class HipGoNet:
                 and os.environ.get("DG_HEAD_MFMA", "1") != "0"):
             first = self.stack[0]
             fused = (h.conv_stack2_fwd_head, (
-                self._stack_table.ctypes.data, len(self.stack), self.act[first - 1].data_ptr(),
-                self.plans[first].KP, self.B, P + hd.w_off * f4, P + hd.b_off * f4,
+                self._stack_table.ctypes.data, len(self._stack_table),
+                self._stack_x0.data_ptr(), int(self.stack_l1), self.B,
+                P + hd.w_off * f4, P + hd.b_off * f4,
                 P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
                 self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
                 self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
@@ -435,6 +442,7 @@ class HipGoNet:
         stores; csrc/kernels/conv_stack2.hip).  DG_STACK=0 keeps per-layer kernels."""
         self.stack = []
         self.stack_fp8 = False
+        self.stack_l1 = False
         if os.environ.get("DG_STACK", "1") == "0":
             return
         L = self.layout.layers
@@ -470,8 +478,20 @@ class HipGoNet:
             else:
                 rows.append([self.wfrag[i].data_ptr(), self.pbias_frag[i].data_ptr(),
                              self.act[i].data_ptr(), m.data_ptr() if m is not None else 0])
-        self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
         first = best[0]
+        # the first layer in front of the stack (conv_stack2.hip l1 mode): its input frame is
+        # the expanded network input, its output act[0] leaves by the stack's copy-out
+        self.stack_l1 = (not fp8 and first == 1 and self.wfrag[0] is not None
+                         and self.relu_mask[0] is not None)
+        if self.stack_l1:
+            rows.insert(0, [self.wfrag[0].data_ptr(), self.pbias_frag[0].data_ptr(),
+                            self.act[0].data_ptr(), self.relu_mask[0].data_ptr()])
+        self._stack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+        self._stack_x0 = self.x0 if self.stack_l1 else self.act[first - 1]
+        if self.stack_l1:
+            members_l1 = {0}
+        else:
+            members_l1 = set()
         if fp8:
             # fp8 forward stack (conv_stack_f8.hip): quantizes its bf16 input frame itself
             # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out
@@ -483,11 +503,11 @@ class HipGoNet:
                                          self.B))
             self.stack_fp8 = True
         else:
-            op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(best),
-                                          self.act[first - 1].data_ptr(), self.plans[first].KP,
+            op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(rows),
+                                          self._stack_x0.data_ptr(), int(self.stack_l1),
                                           self.B))
         # every launch owned by a stack layer goes; the stack launch takes the first's place
-        members = set(best)
+        members = set(best) | members_l1
         keep, placed = [], False
         for fop, owner in zip(self._fwd, self._fwd_owner):
             if owner in members:
@@ -557,8 +577,7 @@ class HipGoNet:
             self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
             self._bwd_pre.append((self.h.conv_stack2, (self.h.EPI_DGRAD,
                                                       self._dstack_table.ctypes.data, len(run),
-                                                      self.dz[run[0]].data_ptr(),
-                                                      self.plans[run[0]].KPd, self.B)))
+                                                      self.dz[run[0]].data_ptr(), 0, self.B)))
         for i in run:  # per-layer dgrad dropped: ops = [bias partial, wgrad, reduce]
             self._bwd[i] = self._bwd[i][:3]
         # the remaining per-layer dgrads below the stack (layer 1 -> dZ_0) right after it, so
@@ -595,6 +614,16 @@ class HipGoNet:
         if moved:
             self._dgrad_first = True
             self._group_wgrads(set(range(len(self.plans))))
+
+    def _stack_l1_ok(self, p: ConvPlan) -> bool:
+        """The first layer can run inside the bf16 forward stack's launch (conv_stack2.hip l1
+        mode: 5x5 over the 23x23x40 input frame, 128 outputs, K = 1024; DG_STACK_L1=0: its
+        own conv_l1 launch)."""
+        lay = self.layout.layers
+        return (p.index == 0 and not self.fp8 and p.k == 5 and p.cinp == 40 and p.cout == 128
+                and p.KP == 1024 and lay[0].pad == 2 and len(lay) > 2 and lay[1].pad == 1
+                and os.environ.get("DG_STACK_L1", "1") != "0"
+                and os.environ.get("DG_STACK", "1") != "0" and self._l1_res_ok(p))
 
     def _l1_res_ok(self, p: ConvPlan) -> bool:
         """First layer on the board-resident kernel (conv_l1.hip; DG_L1_RES=0: pixel-tiled)."""
@@ -825,7 +854,8 @@ class HipGoNet:
                 if l0_side:                      # then dZ_0 and the first layer's whole
                     self._run(self._l0_dgrad, side.cuda_stream)   # chain, joined at layer 0
                     self._run(self._bwd[0][:3], side.cuda_stream)  # (measured: the other
-                self._run(ops[1:2], main.cuda_stream)              # order starves the 5x5 wgrad)
+                self._run(ops[1:2], main.cuda_stream)              # order starves the 5x5 wgrad;
+                # round 2 with the head reduce deferred: 293k vs 282k boards/s)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:

@@ -64,7 +64,7 @@ def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb, with_mask: bool = Fals
     posb = posb.float().contiguous().to(dev)
     mask = torch.zeros(B, NPTS, cout // 8, dtype=torch.uint8, device=dev) if with_mask else None
     h.conv_l1(k, A.data_ptr(), KP, cout, Mpad, xf.data_ptr(), pad, cinp, B, yf.data_ptr(), 1,
-              bias.data_ptr(), posb.data_ptr(), _ptr(mask), stream_handle())
+              bias.data_ptr(), posb.data_ptr(), _ptr(mask), 0, stream_handle())
     if with_mask:
         return LY.from_frame(yf, 1, cout), mask
     return LY.from_frame(yf, 1, cout)

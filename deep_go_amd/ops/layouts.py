@@ -76,6 +76,16 @@ def stack_frag(A: torch.Tensor) -> torch.Tensor:
     return a.permute(4, 3, 0, 5, 1, 6, 2, 7).reshape(-1).contiguous()
 
 
+def stack_frag_linear(A: torch.Tensor) -> torch.Tensor:
+    """conv_stack2's fused-first-layer A order (l1 mode) of a [128][1024] operand matrix with
+    LINEAR k (fwd_weight of the 5x5 40-channel first layer, k = tap*40 + c, zero-padded from
+    1000): flat [s 16][wm 2][kk 2][i 4][lane 64][e 8] with row wm*64 + i*16 + (lane & 15),
+    column s*64 + kk*32 + (lane >> 4)*8 + e."""
+    assert A.shape[0] >= 128 and A.shape[1] >= 1024
+    a = A[:128, :1024].reshape(2, 4, 16, 16, 2, 4, 8)     # wm i lr | s kk lq e
+    return a.permute(3, 0, 4, 1, 5, 2, 6).reshape(-1).contiguous()
+
+
 def stack_frag_f8(w8: torch.Tensor) -> torch.Tensor:
     """conv_stack_f8 A-operand order of e4m3 forward weights ``w8`` [C co][9 taps][C ci]
     (uint8 bytes, C = 128 | 256): flat [h C/128][tap 9][c C/128][wm 2][i 4][half 2][lane 64]

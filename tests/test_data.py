@@ -167,6 +167,22 @@ def test_concurrent_rank_loaders_are_deterministic(packed_fixture):
     assert not np.array_equal(got[0][0], got[1][0])
 
 
+def test_stack_frag_linear_indexing():
+    """layouts.stack_frag_linear (conv_stack2's fused first layer): A[row][col] lands at
+    [s][wm][kk][i][lane][e] with row = wm*64 + i*16 + (lane & 15), col = s*64 + kk*32 +
+    (lane >> 4)*8 + e (a CPU check of the index algebra the kernel and weight_refresh use)."""
+    import torch
+    from deep_go_amd.ops import layouts as LY
+    A = torch.arange(128 * 1024, dtype=torch.int64).reshape(128, 1024)
+    f = LY.stack_frag_linear(A).reshape(16, 2, 2, 4, 64, 8)
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        s_, wm, kk, i, lane, e = (int(rng.integers(n)) for n in (16, 2, 2, 4, 64, 8))
+        row = wm * 64 + i * 16 + (lane & 15)
+        col = s_ * 64 + kk * 32 + (lane >> 4) * 8 + e
+        assert f[s_, wm, kk, i, lane, e].item() == A[row, col].item()
+
+
 def test_stack_frag_layout_indexing():
     """layouts.stack_frag puts A[row][col] at the conv_stack2 fragment index (CPU check of the
     permutation the kernel and weight_refresh assume)."""

@@ -87,8 +87,9 @@ def test_model_matches_bf16_storage_oracle(layers, ch, B):
     """Flagship shapes (12x128, 12x256) end to end against the bf16-storage oracle.  The
     oracle rounds where the kernels round but cannot round the SAME values (its fp32 sums
     differ in order), so a few ReLU gates near zero flip and the difference compounds down the
-    backward: measured max per-tensor gradient error 3.6% (12x128) / 4.7% (12x256), 0.17% at
-    4 layers.  The per-layer, depth-independent bound is test_layerwise_teacher_forced."""
+    backward: measured max per-tensor gradient error 6.4% (12x128, since the first layer also
+    reads the bf16 bias table: the same flips, different ones) / 4.7% (12x256), 0.17% at 4
+    layers.  The per-layer, depth-independent bound is test_layerwise_teacher_forced."""
     cfg, net, data = _setup(layers, ch, B, seed=4)
     net.forward_backward()
     torch.cuda.synchronize()
@@ -106,7 +107,7 @@ def test_model_matches_bf16_storage_oracle(layers, ch, B):
     os.makedirs("gpurun_out", exist_ok=True)
     with open(f"gpurun_out/oracle_errs_{layers}x{ch}.json", "w") as f:
         json.dump(errs, f, indent=0)
-    assert errs[worst] < 6e-2, errs
+    assert errs[worst] < 7e-2, errs
 
 
 def _interior(frame, pad):
@@ -274,6 +275,32 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
     assert torch.equal(n0.loss, n1.loss)
     # (head_reduce folds board partials with atomics: last-bit order effects only)
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
+
+
+def test_first_layer_fused_into_forward_stack(monkeypatch):
+    """conv_stack2 l1 mode: the 5x5 first layer runs inside the forward stack's launch
+    (default) — its fragment-ordered weights are fwd_weight permuted by stack_frag_linear,
+    and activations, ReLU masks, loss and gradients are bit-identical to the standalone
+    conv_l1 launch (DG_STACK_L1=0; both add the same bf16 bias table)."""
+    from deep_go_amd.ops import layouts as LY
+    monkeypatch.setenv("DG_STACK_L1", "0")
+    _, n0, _ = _setup(5, 128, 5, seed=21)
+    monkeypatch.setenv("DG_STACK_L1", "1")
+    _, n1, _ = _setup(5, 128, 5, seed=21)
+    assert n1.stack_l1 and not n0.stack_l1
+    assert not any(f is n1.h.conv_l1 for f, _ in n1._fwd_train)
+    assert any(f is n0.h.conv_l1 for f, _ in n0._fwd_train)
+    assert torch.equal(n1.wfrag[0], LY.stack_frag_linear(n1.wf[0]))
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    for a0, a1 in zip(n0.act, n1.act):
+        assert torch.equal(a0, a1)
+    for m0, m1 in zip(n0.relu_mask, n1.relu_mask):
+        if m0 is not None:
+            assert torch.equal(m0, m1)
+    assert torch.equal(n0.loss, n1.loss)
+    assert torch.equal(n0.grads, n1.grads)
 
 
 @pytest.mark.parametrize("layers", [4, 7])

@@ -55,7 +55,7 @@ def test_stack_layers_match_fp32_oracle(epi):
                      ms[i].data_ptr()] for i in range(NL)], dtype=np.int64)
     masks_in = [m.clone() for m in ms]
     e = h.EPI_FWD if epi == "fwd" else h.EPI_DGRAD
-    h.conv_stack2(e, tab.ctypes.data, NL, x.data_ptr(), KP, B, stream_handle())
+    h.conv_stack2(e, tab.ctypes.data, NL, x.data_ptr(), 0, B, stream_handle())
     torch.cuda.synchronize()
     xin = x
     for l in range(NL):

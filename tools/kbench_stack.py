@@ -45,7 +45,7 @@ def main():
 
         def f():
             h.conv_stack2_set_mode(mode)
-            h.conv_stack2(epis[name], t.ctypes.data, NL, x.data_ptr(), KP, B, s)
+            h.conv_stack2(epis[name], t.ctypes.data, NL, x.data_ptr(), 0, B, s)
         return f
     abl = [2, 4, 6, 10, 14] if "--ablate" in sys.argv else []
     out = {}
