@@ -984,6 +984,8 @@ class SegmentedStep:
                 fire_after.setdefault(first_layer, []).append(bi)
         segs: List[Tuple[List[Callable[[], None]], List[int]]] = []
         cur: List[Callable[[], None]] = []
+        in_graph = (bucketer is not None and getattr(bucketer, "in_graph", False)
+                    and use_graphs)
 
         def emit(fn):
             cur.append(fn)
@@ -1000,7 +1002,14 @@ class SegmentedStep:
         for i in range(net.L - 2, -1, -1):
             emit(lambda i=i: net.backward_layer(i))
             if i in fire_after:
-                emit(net.join_side)           # bucket grads final on the main stream
+                # bucket grads final on the main stream: backward_layer already makes the
+                # main stream wait for a layer's (group's) side-stream bias partials (and the
+                # deferred head reduce before them); only layer 0's chain may still run on the
+                # side stream, so only layer 0's bucket joins it — the others' all-reduces
+                # overlap that chain (in-graph collectives only: a separately captured
+                # segment must join every stream it forked)
+                if i == 0 or net._l0_side_at is None or not in_graph:
+                    emit(net.join_side)
                 segs.append((cur, fire_after[i]))
                 cur = []
         if cur:
