@@ -66,6 +66,8 @@ void dg_conv_wgrad_win_set_pd(int pd);
 void dg_conv_wgrad_win_set_nw(int nw);
 void dg_conv_wgrad_win_set_swp(int on);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
+hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void* X, void* Y,
+                          void* mask, int C, int B, hipStream_t stream);
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                              int KP, int splits, hipStream_t stream);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
@@ -362,6 +364,13 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_l1_ok", [](int kw, int x_pad, int x_C, int Mpad, int KP) {
     return dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP);
   });
+  m.def("conv_layer2", [](int epi, uintptr_t A, uintptr_t pbias, uintptr_t X, uintptr_t Y,
+                         uintptr_t mask, int C, int B, uintptr_t stream) {
+    check(dg_conv_layer2(epi, P<void>(A), P<void>(pbias), P<void>(X), P<void>(Y), P<void>(mask),
+                         C, B, S(stream)),
+          "conv_layer2");
+  }, "one hidden 3x3 C -> C layer (C = 256 | 128) on conv_stack2's K loop: epi 1 forward "
+     "(fragment weights, pbias_frag, mask written), 2 backward-data (mask of the layer below)");
   m.def("conv_wgrad_win", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
                              int splits, uintptr_t stream) {
     check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),

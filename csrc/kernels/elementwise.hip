@@ -248,8 +248,9 @@ struct WRefreshLayer {
   bf16_t* pbias;       // [361][cout] or null
   uint2* pbias_frag;   // the same table in the board-resident stack's accumulator-fragment
                        // order (cout == 128): [24 px frags][2 co halves][4][64 lanes] x 4 bf16
-  uint4* wf_frag;      // conv_stack2 A operands (3x3, 128 -> 128 only), MFMA fragment order:
-  uint4* wd_frag;      //   [step 18][wm 2][kk 2][i 4][lane 64] x 8 bf16 (forward / dgrad)
+  uint4* wf_frag;      // conv_stack2 / conv_layer2 A operands (3x3, C -> C, C = 128 | 256),
+  uint4* wd_frag;      //   MFMA fragment order [h C/128][step 9 C/64][wm 2][kk 2][i 4][lane 64]
+                       //   x 8 bf16 (forward / dgrad)
   uint4* wf8_frag;     // conv_stack_f8 A operands (e4m3, quantized with s_w like wf8):
                        //   [h][tap 9][c][wm 2][i 4][half 2][lane 64] x 16 B (requires wf8)
   uint4* wd8_frag;     // the same for the backward-data operand (flipped taps, transposed)
@@ -342,8 +343,12 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
           f[e] = pack_bf16x2(tileS[r][k0 + 2 * e], tileS[r][k0 + 2 * e + 1]);
           d[e] = pack_bf16x2(tileS[k0 + 2 * e][r], tileS[k0 + 2 * e + 1][r]);
         }
-        L.wf_frag[((size_t)(cit * 9 + t) * 2 + cot) * 512 + u] = uint4{f[0], f[1], f[2], f[3]};
-        L.wd_frag[((size_t)(cot * 9 + (8 - t)) * 2 + cit) * 512 + u] = uint4{d[0], d[1], d[2], d[3]};
+        // (C = 256: [h = co half][36 steps] — h = cot / 2 (forward) / cit / 2 (dgrad rows))
+        const int nst = (L.cin / 64) * 9;
+        L.wf_frag[(((size_t)(cot >> 1) * nst + cit * 9 + t) * 2 + (cot & 1)) * 512 + u] =
+            uint4{f[0], f[1], f[2], f[3]};
+        L.wd_frag[(((size_t)(cit >> 1) * nst + cot * 9 + (8 - t)) * 2 + (cit & 1)) * 512 + u] =
+            uint4{d[0], d[1], d[2], d[3]};
       }
     }
     if (L.wf8_frag) {
@@ -555,7 +560,8 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
                             (a.L[i].cout != 128 && a.L[i].cout != 256)))
       return hipErrorInvalidValue;
     if (a.L[i].wf_frag && a.L[i].wd_frag &&
-        (a.L[i].cout != 128 || a.L[i].cin != 128 || a.L[i].taps != 9))
+        (a.L[i].cout != a.L[i].cin || (a.L[i].cout != 128 && a.L[i].cout != 256) ||
+         a.L[i].taps != 9))
       return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;

@@ -149,8 +149,10 @@ class HipGoNet:
                 # the first layer fused in front of the forward stack (conv_stack2.hip l1
                 # mode): [128][1024] weights in fragment order (k linear), no dgrad operand
                 self.wfrag[0] = torch.zeros(128 * 1024, dtype=torch.bfloat16, device=dev)
-            if p.index > 0 and p.k == 3 and p.cin == 128 and p.cout == 128 and p.cinp == 128:
-                self.wfrag[p.index] = torch.zeros(128 * 9 * 128, dtype=torch.bfloat16,
+            if (p.index > 0 and p.k == 3 and p.cin == p.cout == p.cinp
+                    and (p.cout == 128 or (p.cout == 256 and self._layer2_ok(p)))):
+                # 128: the layer stacks; 256: the per-layer conv_layer2 kernel
+                self.wfrag[p.index] = torch.zeros(p.cout * 9 * p.cin, dtype=torch.bfloat16,
                                                   device=dev)
                 self.wdfrag[p.index] = torch.zeros_like(self.wfrag[p.index])
             if (p.fp8 and p.index > 0 and p.k == 3 and p.cin == p.cout == p.cinp
@@ -319,6 +321,13 @@ class HipGoNet:
                     S + 2 * i * f4, S + (2 * i + 1) * f4,
                     self.fp8_amax.data_ptr() + i * 4 if y8 else 0,
                     self.relu_mask[i].data_ptr() if self.relu_mask[i] is not None else 0)))
+            elif p.board and p.cout == 256 and self.wfrag[p.index] is not None:
+                msk = self.relu_mask[p.index]
+                self._fwd.append((h.conv_layer2, (
+                    h.EPI_FWD, self.wfrag[p.index].data_ptr(),
+                    self.pbias_frag[p.index].data_ptr(), xin.data_ptr(),
+                    self.act[p.index].data_ptr(), msk.data_ptr() if msk is not None else 0,
+                    p.cout, self.B)))
             elif p.board:
                 msk = self.relu_mask[p.index]
                 self._fwd.append((h.conv_board_ex, (
@@ -419,7 +428,14 @@ class HipGoNet:
                                          G + spec.pos_off * f4, G + spec.b_off * f4)))
             if i > 0:
                 prev = lay.layers[i - 1]
-                if p.board_d:
+                if (p.board_d and self.wdfrag[i] is not None and p.cout == 256
+                        and self.relu_mask[i - 1] is not None and self.dzp[i] == 1
+                        and self.dzp[i - 1] == 1):
+                    ops.append((h.conv_layer2, (
+                        h.EPI_DGRAD, self.wdfrag[i].data_ptr(), 0, self.dz[i].data_ptr(),
+                        self.dz[i - 1].data_ptr(), self.relu_mask[i - 1].data_ptr(), p.cout,
+                        self.B)))
+                elif p.board_d:
                     msk = self.relu_mask[i - 1]
                     ops.append((h.conv_board_ex, (
                         h.EPI_DGRAD, p.k, p.bm_d, self.wd[i].data_ptr(), p.KPd, p.cin, p.Mpad_d,
@@ -452,6 +468,8 @@ class HipGoNet:
             if not (p.index > 0 and p.board and p.fp8 == fp8 and p.k == 3
                     and L[p.index].pad == 1 and L[p.index + 1].pad == 1):
                 return False
+            if not fp8 and p.cout != 128:
+                return False          # (bf16 d = 256: per-layer conv_layer2)
             # bf16: 128 channels (conv_stack2); fp8: 128 or 256 (conv_stack_f8)
             return self.wf8frag[p.index] is not None if fp8 else self.wfrag[p.index] is not None
         best, cur = [], []
@@ -614,6 +632,15 @@ class HipGoNet:
         if moved:
             self._dgrad_first = True
             self._group_wgrads(set(range(len(self.plans))))
+
+    def _layer2_ok(self, p: ConvPlan) -> bool:
+        """A hidden 3x3 256 -> 256 bf16 layer runs forward and backward-data on conv_layer2.hip
+        (weights streamed into VGPRs in fragment order, the board's input frame through two
+        64-channel chunk buffers; DG_LAYER2=0: the board kernel conv_board.hip)."""
+        lay = self.layout.layers
+        return (p.index > 0 and not p.fp8 and p.board and p.k == 3 and p.cin == p.cout == 256
+                and lay[p.index].pad == 1 and lay[p.index + 1].pad == 1
+                and os.environ.get("DG_LAYER2", "1") != "0")
 
     def _stack_l1_ok(self, p: ConvPlan) -> bool:
         """The first layer can run inside the bf16 forward stack's launch (conv_stack2.hip l1

@@ -277,6 +277,31 @@ def test_fused_forward_stack_matches_per_layer(layers, monkeypatch):
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
+def test_layer2_matches_board_kernel_at_256(monkeypatch):
+    """d = 256 bf16 hidden layers on conv_layer2.hip (fragment-ordered weights in VGPRs, chunk
+    images double-buffered in LDS) run the board kernel's exact MFMA sequence, bias table and
+    ReLU-mask gating: activations, masks, every dZ and the gradients are bit-identical to
+    DG_LAYER2=0 (conv_board.hip), forward and backward-data."""
+    monkeypatch.setenv("DG_LAYER2", "0")
+    _, n0, _ = _setup(5, 256, 4, seed=31)
+    monkeypatch.setenv("DG_LAYER2", "1")
+    _, n1, _ = _setup(5, 256, 4, seed=31)
+    assert any(f is n1.h.conv_layer2 for f, _ in n1._fwd)
+    assert not any(f is n0.h.conv_layer2 for f, _ in n0._fwd)
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    for a0, a1 in zip(n0.act, n1.act):
+        assert torch.equal(a0, a1)
+    for m0, m1 in zip(n0.relu_mask, n1.relu_mask):
+        if m0 is not None:
+            assert torch.equal(m0, m1)
+    for d0, d1 in zip(n0.dz, n1.dz):
+        assert torch.equal(d0, d1)
+    assert torch.equal(n0.loss, n1.loss)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
+
+
 def test_first_layer_fused_into_forward_stack(monkeypatch):
     """conv_stack2 l1 mode: the 5x5 first layer runs inside the forward stack's launch
     (default) — its fragment-ordered weights are fwd_weight permuted by stack_frag_linear,
