@@ -55,7 +55,6 @@ constexpr int HROWS = 448;                // halo rows padded to whole 8-wave DM
 constexpr int H_BYTES = HROWS * 128;      // one 64-channel image
 constexpr int T = 9;
 constexpr int NSTEP = 2 * T;              // chunks x taps
-constexpr int UNITS = NPTS * 16;          // 16-B output pieces of one board (5776)
 constexpr int MAXL = 24;
 constexpr int MF = 4;                     // 64 co per wave (4 fragments of 16)
 constexpr int NF = 6;                     // 96 px per wave (6 fragments of 16)
@@ -64,7 +63,7 @@ constexpr int NT = NW * 64;
 constexpr int SCRATCH = 12 * 1024;        // head_body scratch (fused head)
 constexpr int STEP_BYTES = 2 * 2 * MF * 64 * 16;   // one K-step of one layer: 16 KB
 constexpr int WM_BYTES = STEP_BYTES / 2;           // one co-half: 8 KB
-constexpr int CO_STEPS = (UNITS + NT - 1) / NT;    // 12
+constexpr int CO_STEPS = (NPTS * 8 + NT - 1) / NT;  // copy-out steps per 64-channel image (6)
 
 static_assert(dghead::scratch_bytes(C) <= SCRATCH, "head scratch");
 
@@ -131,10 +130,10 @@ DG_DEV uint32_t pair_mask(uint32_t nib) {
 }
 
 // MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop; 16 = two
-// branch-free K loops (exact waits; slower, kept for the A/B)
+// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop
 template <int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
+  constexpr bool TWO_GROUP = EPI == EPI_DGRAD;  // epilogue schedule (see the K loop)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -224,21 +223,26 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   };
 
   // Copy-out of the previous layer's output (resident in the image) to HBM, one 16-B piece
-  // (8 channels of one pixel) per thread and K-step over the first 12 K-steps: the piece
-  // of step s is READ from LDS during step s-1 and STORED in step s.  Thread tid always
-  // handles channel piece q = tid & 15 of pixels p = tid / 16 + 32 s.
-  const int co_q = tid & 15;
+  // (8 channels of one pixel) per thread and K-step: image 0 (channels 0..63) in K-steps
+  // 0..5, image 1 in K-steps 9..14 — each image only while the K loop is reading it, i.e.
+  // after the barrier that completes it and before the epilogue that overwrites it.  The
+  // piece of a step is read from LDS after the step's first k-half and stored at its end.
+  // Step s: half hf = s / 9, j = s % 9; thread tid handles channel piece q = tid & 7 of
+  // image hf at pixel p = tid / 8 + 64 j (128 contiguous bytes per pixel and image).
   auto co_read = [&](int s_) -> uint4 {
-    const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
+    const int hf = s_ >= T, j = s_ - hf * T;
+    const int p = min((tid >> 3) + 64 * j, NPTS - 1);
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    return *(const uint4*)(sH + (co_q >> 3) * H_BYTES + f * 128 + (((co_q & 7) ^ fsig(f)) * 16));
+    return *(const uint4*)(sH + hf * H_BYTES + f * 128 + (((tid & 7) ^ fsig(f)) * 16));
   };
   auto co_store = [&](int s_, const uint4& v, const StackLayer& Lo) {
     // lanes past the board re-store pixel 360 (same value): every wave issues the stores
-    const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
+    const int hf = s_ >= T, j = s_ - hf * T;
+    const int p = min((tid >> 3) + 64 * j, NPTS - 1);
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
+    const int co_q = hf * 8 + (tid & 7);
     *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
     if (EPI == EPI_FWD && Lo.mask) {
       // bit per nonzero bf16 half (post-ReLU: every half is in [0, 0x7fff]): h + 0x7fff has
@@ -293,11 +297,21 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       if (co) co_store(s, co_v, Lprev);
       __builtin_amdgcn_sched_barrier(0);
     };
-    // One rolled loop with a per-step copy-out branch.  The compiler's wait at its head is
+    // Rolled loops with a per-step copy-out branch.  The compiler's wait at their head is
     // then vmcnt(0) (the k-half-1 loads of the step before and its copy-out store drain
     // there); measured faster than every variant with exact waits: two branch-free loops
-    // (copy-out steps / the rest, MODE 16: fwd 229 -> 234 us, dgrad 216 -> 224 us) and
-    // unrolled by 2 or 3 (267 / 279 us; profiles/r2_kbench_stack2.json).
+    // (copy-out steps / the rest: fwd 229 -> 234 us, dgrad 216 -> 224 us) and unrolled by 2
+    // or 3 (267 / 279 us; profiles/r2_kbench_stack2.json).
+    //
+    // Two-group schedule of the backward-data chain (TWO_GROUP; the waves of co-half wm write
+    // image wm in the epilogue):
+    //   steps 0..8 (image 0) | barrier A | steps 9..17 (image 1) | wm 0: write image 0 |
+    //   barrier B | wm 1: write image 1 (beside wm 0's next steps 0..8, which read image 0)
+    // Barrier A: every wave is past its image-0 reads and image 1 holds the layer input
+    // (wm 1 wrote it before arriving); barrier B: image 0 holds the output and every wave is
+    // past its image-1 reads.  Same 2 barriers per layer as writing both images between two
+    // barriers, but half of the epilogue runs beside the other half's MFMAs (dgrad stack
+    // -0.9..-3% in the kernel bench; the forward keeps one write phase between two barriers).
     int s = 0;
     if (EPI == EPI_FWD && l == 0 && a.l1) {
       // the fused first layer: 16 K-steps over the staged input frame (nothing to copy out)
@@ -316,17 +330,21 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         load_A(An, 1, Ak[1]);
         __builtin_amdgcn_sched_barrier(0);
       }
-    } else if constexpr (!(MODE & 16)) {
-      if (!(MODE & 4) && co_on) {
+    } else {
 #pragma unroll 1
-        for (; s < CO_STEPS; ++s) {
-          int tt = s;
-          asm volatile("" : "+s"(tt));
-          kstep(tt, true);
+      for (int h2 = 0; h2 < 2; ++h2) {
+        if (h2 == 1 && TWO_GROUP) lds_barrier();  // A
+        if (!(MODE & 4) && co_on) {
+#pragma unroll 1
+          for (; s < h2 * T + CO_STEPS; ++s) {
+            int tt = s;
+            asm volatile("" : "+s"(tt));
+            kstep(tt, true);
+          }
         }
-      }
 #pragma unroll 1
-      for (; s < NSTEP; ++s) kstep(s, false);
+        for (; s < (h2 + 1) * T; ++s) kstep(s, false);
+      }
     }
 
     // ---- epilogue: write the layer's output back into the LDS image ----
@@ -348,7 +366,42 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         em[j] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8 + z0);
       }
     }
-    lds_barrier();  // every wave is past its last read of this layer's image
+    auto write_out = [&]() {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int p = wn * NF * 16 + j * 16 + lr;
+        const int f = (int)(pk[j] & 0xFFFFu) >> 7;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
+          const f32x4 v = acc[i][j];
+          uint2 o;
+          if constexpr (EPI == EPI_FWD) {
+            // packed fp32 bias add, bf16 pack, ReLU on the packed bf16 (max as int16: the
+            // same as relu before the rounding, -0 included)
+            o.x = relu_bf16x2(f32x2{v[0], v[1]} + bf16x2_f32(eb[j][i].x));
+            o.y = relu_bf16x2(f32x2{v[2], v[3]} + bf16x2_f32(eb[j][i].y));
+          } else {
+            // the 4 ReLU bits of these channels gate the bf16 pairs
+            const uint32_t word = (i < 2) ? em[j].x : em[j].y;
+            const uint32_t nib = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
+            o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
+            o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
+          }
+          const int slot = (cl >> 3) ^ (int)(pk[j] >> 16);
+          if (p < NPTS) *(uint2*)(sH + z0 + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
+        }
+      }
+    };
+    if constexpr (TWO_GROUP) {
+      if (wm == 0) write_out();  // image 0: dead since barrier A
+      lds_barrier();             // B
+      if (wm == 1) write_out();  // image 1 (the next layer's barrier A publishes it)
+      continue;
+    }
+    // forward: both groups write between two barriers (measured +0.9% over the two-group
+    // schedule in the step; the l1 layer's input frame fills image 0 for all 16 steps anyway)
+    lds_barrier();
     if (EPI == EPI_FWD && l == 0 && a.l1) {
       // the image area held the first layer's input frame: zero the 21x21 frame's border
       // rows / columns (the next layer's taps read them) and the padding rows 441..447
@@ -359,37 +412,15 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         *(uint4*)(sH + img * H_BYTES + row * 128 + q * 16) = uint4{0u, 0u, 0u, 0u};
       }
     }
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int p = wn * NF * 16 + j * 16 + lr;
-      const int f = (int)(pk[j] & 0xFFFFu) >> 7;
-#pragma unroll
-      for (int i = 0; i < MF; ++i) {
-        const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
-        const f32x4 v = acc[i][j];
-        uint2 o;
-        if constexpr (EPI == EPI_FWD) {
-          // packed fp32 bias add, bf16 pack, ReLU on the packed bf16 (max as int16: the
-          // same as relu before the rounding, -0 included)
-          o.x = relu_bf16x2(f32x2{v[0], v[1]} + bf16x2_f32(eb[j][i].x));
-          o.y = relu_bf16x2(f32x2{v[2], v[3]} + bf16x2_f32(eb[j][i].y));
-        } else {
-          // the 4 ReLU bits of these channels gate the bf16 pairs
-          const uint32_t word = (i < 2) ? em[j].x : em[j].y;
-          const uint32_t nib = word >> ((cl & 31) >> 3 << 3) >> (cl & 4);
-          o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
-          o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
-        }
-        const int slot = (cl >> 3) ^ (int)(pk[j] >> 16);
-        if (p < NPTS) *(uint2*)(sH + z0 + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
-      }
-    }
+    write_out();
     lds_barrier();  // the next layer's input is complete
   }
+  lds_barrier();  // C: image 1 of the last layer's output (wm 1) is complete
   // last layer's output: exposed copy-out
   {
     const StackLayer Ll = a.L[a.nl - 1];
     for (int s_ = 0; s_ < CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
+    for (int s_ = T; s_ < T + CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
   }
   // the policy head on the board image that is already in LDS (no re-staging, no launch)
   if constexpr (EPI == EPI_FWD) {
@@ -440,7 +471,6 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     a.head = *head;
   }
   if (epi == EPI_DGRAD) {
-    if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16>(a, B, stream);
     return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
   }
   switch (g_stack2_mode) {  // forward: the MODE ablations too (kbench_stack.py)
@@ -449,7 +479,6 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     case 14: return launch_stack2<EPI_FWD, 14>(a, B, stream);
     case 4: return launch_stack2<EPI_FWD, 4>(a, B, stream);
     case 10: return launch_stack2<EPI_FWD, 10>(a, B, stream);
-    case 16: return launch_stack2<EPI_FWD, 16>(a, B, stream);
     default: return launch_stack2<EPI_FWD, 0>(a, B, stream);
   }
 }

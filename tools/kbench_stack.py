@@ -74,7 +74,6 @@ def main():
     for _ in range(3):
         for name in ("fwd", "dgrad"):
             times.setdefault(name, []).append(round(timeit(run(name)), 1))
-            times.setdefault(name + "_mode16", []).append(round(timeit(run(name, 16)), 1))
         for m in abl:
             times.setdefault(f"fwd_mode{m}", []).append(round(timeit(run("fwd", m)), 1))
         times.setdefault("fp8_fwd", []).append(round(timeit(run8()), 1))
