@@ -35,6 +35,26 @@ def test_gpu_experiment_run_and_resume(tmp_path):
     assert torch.isfinite(r.backend.net.params).all()
 
 
+def test_fused_trainer_step_matches_unfused(tmp_path):
+    """nan_policy='skip' runs the non-validation iterations as the fused one-graph step
+    (forward/backward + SGD + refresh, experiment.py); 'raise' never does.  Same init, same
+    data stream across two validation points: the same parameters and validation costs up to
+    last-bit reduction-order effects (the graphs differ in stream placement), the same rate
+    (read before the step on both paths)."""
+    from deep_go_amd.train.experiment import Experiment
+    runs = {}
+    for pol in ("skip", "raise"):
+        e = Experiment(_cfg(tmp_path / pol, nan_policy=pol), id=pol)
+        e.run(25)
+        runs[pol] = e
+    a, b = runs["skip"], runs["raise"]
+    assert len(a.validation_costs) == 2
+    pa, pb = a.backend.net.params, b.backend.net.params
+    assert ((pa - pb).norm() / pb.norm()).item() < 1e-5
+    assert a.validation_costs == pytest.approx(b.validation_costs, rel=1e-4)
+    assert a.backend.rate == b.backend.rate
+
+
 def test_gpu_step_matches_cpu_step(tmp_path):
     """One SGD step through the HIP kernels vs the fp32 PyTorch oracle from the same init."""
     from deep_go_amd.data.synthetic import random_planes
