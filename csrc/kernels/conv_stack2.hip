@@ -370,7 +370,12 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int p = wn * NF * 16 + j * 16 + lr;
-        const int f = (int)(pk[j] & 0xFFFFu) >> 7;
+        // the LDS offsets below derive from an opaque copy of pk[j]: left visible, the
+        // compiler hoists all 24 (fragment, slot) offsets out of the layer loop, spills them
+        // (forward: 256 VGPRs) and reloads each with a full vmcnt(0) wait in every epilogue
+        uint32_t pkj = pk[j];
+        asm volatile("" : "+v"(pkj));
+        const int f = (int)(pkj & 0xFFFFu) >> 7;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           const int cl = i * 16 + lq * 4;  // channel within the wave's 64-channel image
@@ -388,7 +393,7 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
             o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
             o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
           }
-          const int slot = (cl >> 3) ^ (int)(pk[j] >> 16);
+          const int slot = (cl >> 3) ^ (int)(pkj >> 16);
           if (p < NPTS) *(uint2*)(sH + z0 + wm * H_BYTES + f * 128 + slot * 16 + (cl & 4) * 2) = o;
         }
       }
