@@ -395,8 +395,12 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int p = wn * NF * 16 + j * 16 + lr;
-        const int f = (int)(pk[j] & 0xFFFFFu) / ROWB;
-        const int sig = (int)(pk[j] >> 20);
+        // offsets from an opaque copy of pk[j]: visible, the compiler hoists every
+        // (fragment, slot) offset out of the layer loop and spills them (conv_stack2.hip)
+        uint32_t pkj = pk[j];
+        asm volatile("" : "+v"(pkj));
+        const int f = (int)(pkj & 0xFFFFFu) / ROWB;
+        const int sig = (int)(pkj >> 20);
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           f32x4 v = acc[i][j];
