@@ -312,6 +312,19 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     // past its image-1 reads.  Same 2 barriers per layer as writing both images between two
     // barriers, but half of the epilogue runs beside the other half's MFMAs (dgrad stack
     // -0.9..-3% in the kernel bench; the forward keeps one write phase between two barriers).
+    // dgrad: this wave's ReLU-bit words of the layer below (the epilogue's gates), loaded two
+    // K-steps before the end of the loop, so co-half 0's epilogue (first, right after the
+    // loop) does not wait for them (dgrad stack -1.7%, step +0.3%)
+    uint2 em[NF];
+    auto load_em = [&]() {
+      int z1 = 0;
+      asm volatile("" : "+v"(z1));
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
+        em[j] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8 + z1);
+      }
+    };
     int s = 0;
     if (EPI == EPI_FWD && l == 0 && a.l1) {
       // the fused first layer: 16 K-steps over the staged input frame (nothing to copy out)
@@ -343,7 +356,10 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
           }
         }
 #pragma unroll 1
-        for (; s < (h2 + 1) * T; ++s) kstep(s, false);
+        for (; s < (h2 + 1) * T; ++s) {
+          if (EPI == EPI_DGRAD && s == NSTEP - 2) load_em();
+          kstep(s, false);
+        }
       }
     }
 
@@ -354,7 +370,6 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     int z0 = 0;
     asm volatile("" : "+v"(z0));
     uint2 eb[NF][EPI == EPI_FWD ? MF : 1];
-    uint2 em[NF];
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
@@ -362,8 +377,6 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         const uint2* pf = (const uint2*)L.pbias + ((wn * NF + j) * 2 + wm) * 4 * 64 + lane + z0;
 #pragma unroll
         for (int i = 0; i < MF; ++i) eb[j][i] = pf[i * 64];
-      } else {  // 64 channel bits of this wave's image half
-        em[j] = *(const uint2*)(L.mask + ((size_t)b * NPTS + p) * 16 + wm * 8 + z0);
       }
     }
     auto write_out = [&]() {
