@@ -276,7 +276,11 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
   };
   auto co_store = [&](int s_, const uint4& v, const F8Layer& Lo, float s_prev) {
-    const int u = min(tid + NT * s_, G::PIECES - 1);
+    // (opaque piece index: visible, the compiler hoists the per-step 64-bit store offsets
+    // out of the layer loop and spills them — reloaded with vmcnt(0) in every layer)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int u = min(tq + NT * s_, G::PIECES - 1);
     const int p = u / G::SLOTS, q = u % G::SLOTS;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
@@ -447,14 +451,14 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
             uint2 o;
             o.x = pack_bf16x2(v[0], v[1]);
             o.y = pack_bf16x2(v[2], v[3]);
-            *(uint2*)(L.Y + ((size_t)(b * FF + f) * C + co) * 2) = o;
+            *(uint2*)(L.Y + ((size_t)(b * FF + f) * C + co) * 2 + z0) = o;
             if constexpr (EPI == EPI_FWD) {
             const uint32_t nib = (v[0] > 0.f ? 1u : 0u) | (v[1] > 0.f ? 2u : 0u) |
                                  (v[2] > 0.f ? 4u : 0u) | (v[3] > 0.f ? 8u : 0u);
             // 4 bits of one mask byte: the lane pair (lq even, odd) shares the byte
             const uint32_t other = __shfl_xor(nib, 16, 64);
             if ((lq & 1) == 0)
-              L.mask[((size_t)b * NPTS + p) * (C / 8) + (co >> 3)] = (uint8_t)(nib | (other << 4));
+              L.mask[((size_t)b * NPTS + p) * (C / 8) + (co >> 3) + z0] = (uint8_t)(nib | (other << 4));
             }
           }
         }
