@@ -17,7 +17,8 @@ sides; the MAX elapsed over ranks is used (per-rank min/max ms are reported too)
 prints ONE JSON line.
 
 What one step is (nothing skipped inside the timed region):
-  next batch (uint8 planes/labels) copied into the static input buffers ->
+  next batch (uint8 planes/labels) copied into the static input buffers (double-buffered:
+  the copy runs on a load stream beside the previous step) ->
   GPU feature expansion -> 11 conv layers fwd -> fused head (loss, argmax, head bwd) ->
   bias-grad + wgrad + dgrad for every layer -> [N>1: bucketed RCCL all-reduce overlapped
   with backward] -> SGD with per-step LR decay -> bf16 weight refresh.
@@ -54,6 +55,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic batches")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--host-pool", action="store_true",
+                    help="synthetic batches in pinned host memory (each step's copy is an H2D "
+                         "copy, as from the trainer's loader) instead of device memory")
     ap.add_argument("--bucket-mb", type=float, default=6.0,
                     help="DP gradient bucket size (6 MB: head + the grouped hidden layers in "
                          "one bucket, fired beside the first layer's gradient chain; the first "
@@ -239,6 +243,11 @@ def run_gpu(args) -> int:
                      batchSize=args.batch * world, seed=1234, dtype=args.dtype)
     B = args.batch
     net = HipGoNet(cfg, B, device=dev, global_batch=B * world)
+    # input prefetch (the next batch's copy on a load stream beside the previous step): on for
+    # the pinned host pool (SDMA copies, +1.1%), off for the device pool (its blit-kernel copy
+    # beside the step measured -1%; profiles/r2_input_prefetch_ab.txt); DG_PREFETCH=0/1 forces
+    pf = os.environ.get("DG_PREFETCH", "auto")
+    prefetch = (pf == "1" or (pf != "0" and args.host_pool)) and net.enable_prefetch()
     if world > 1:
         comm.broadcast_(net.params, 0)
         net.refresh_weights()
@@ -248,7 +257,8 @@ def run_gpu(args) -> int:
     # packed [planes | player | rank | labels] batches: one device copy per step
     pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
                                    rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
-                        for j in range(args.pool)]).to(dev)
+                        for j in range(args.pool)])
+    pool = pool.pin_memory() if args.host_pool else pool.to(dev)
 
     def load(i):
         net.set_batch_packed(pool[i % args.pool])
@@ -304,7 +314,8 @@ def run_gpu(args) -> int:
                              f"{[x.tolist() for x in sigs]}")
     if info.rank == 0:
         extra = {"last_loss": round(loss, 4), "graphs": not args.no_graph,
-                 "step_mode": step.mode, "spinup_steps": args.spinup_steps}
+                 "step_mode": step.mode, "spinup_steps": args.spinup_steps,
+                 "input_prefetch": bool(prefetch)}
         if use_dp:
             extra["comm"] = comm.kind
             extra["ranks_params_identical"] = consistent

@@ -249,6 +249,12 @@ class HipGoNet:
         self.planes, self.player, self.rank, self.labels = unpack_views(self.inbuf, B)
         self.player.fill_(1)
         self.rank.fill_(1)
+        # input prefetch (enable_prefetch): a second input buffer filled on a load stream
+        # while the previous step still runs; cur_in = the buffer the next step reads
+        self._inbufs = [self.inbuf]
+        self.cur_in = 0
+        self.load_stream = None
+        self._in_ops = None
         self.loss = torch.zeros(B, dtype=torch.float32, device=dev)
         self.pred = torch.zeros(B, dtype=torch.int32, device=dev)
         # evaluation writes its own outputs so it never clobbers the training step's loss
@@ -788,27 +794,101 @@ class HipGoNet:
         for f, a in ops:
             f(*a, s)
 
+    # ------------------------------------------------------------------ input prefetch
+    def enable_prefetch(self) -> bool:
+        """Double-buffered step inputs.  Every ``set_batch*`` copies into the buffer the
+        previous step does NOT read, on a load stream that waits only for the step before
+        that, so the copy (pinned H2D in the trainer, a D2D copy in the bench) runs beside the
+        previous step instead of in front of the next one.  The launches that read the inputs
+        (feature expansion, the heads: labels) exist once per buffer — the second set is the
+        first with the input pointers substituted — and SegmentedStep captures one step graph
+        per buffer.  Reference: the loader threads filling the next minibatch while the
+        current one trains (/root/reference/data.lua:11-27).  Call before SegmentedStep."""
+        if self.load_stream is not None:
+            return True
+        buf1 = torch.zeros_like(self.inbuf)
+        v0 = unpack_views(self.inbuf, self.B)
+        v1 = unpack_views(buf1, self.B)
+        v1[1].fill_(1)
+        v1[2].fill_(1)
+        m = {a.data_ptr(): b.data_ptr() for a, b in zip(v0, v1)}
+
+        def sub(op):
+            f, a = op
+            return (f, tuple(m.get(x, x) if type(x) is int else x for x in a))
+        names = ("_pre", "_fwd", "_fwd_train")
+        ops0 = {n: list(getattr(self, n)) for n in names}
+        ops0["_head_train"] = self._head_train
+        ops0["_head_eval"] = self._head_eval
+        ops1 = {n: [sub(op) for op in ops0[n]] for n in names}
+        ops1["_head_train"] = sub(self._head_train)
+        ops1["_head_eval"] = sub(self._head_eval)
+        self._in_ops = [ops0, ops1]
+        self._in_views = [v0, v1]
+        self._inbufs = [self.inbuf, buf1]
+        self.load_stream = torch.cuda.Stream(device=self.device)
+        self._rel_ev = [torch.cuda.Event(), torch.cuda.Event()]
+        return True
+
+    def select_inputs(self, k: int):
+        """Make input buffer k the one the (eager) launch lists read."""
+        self.cur_in = k
+        if self._in_ops is None:
+            return
+        for n, v in self._in_ops[k].items():
+            setattr(self, n, v)
+        self.inbuf = self._inbufs[k]
+        self.planes, self.player, self.rank, self.labels = self._in_views[k]
+
+    def _load(self, fill, device_src: bool):
+        """Run ``fill(buffer, views)`` for the next batch: in place without prefetch; with it,
+        into the other buffer on the load stream (after the step that last read it), and the
+        compute stream waits for the copy before the next step's launches.  A device source
+        may still be being written by work issued on the compute stream, so then the load
+        stream waits for all of it (the overlap is for host sources: the loader's pinned
+        slots, copied by the SDMA engines)."""
+        if self.load_stream is None:
+            fill(self.inbuf, (self.planes, self.player, self.rank, self.labels))
+        else:
+            main = torch.cuda.current_stream(self.device)
+            self._rel_ev[self.cur_in].record(main)       # all issued reads of the current one
+            t = 1 - self.cur_in
+            self.load_stream.wait_event(self._rel_ev[1 - t if device_src else t])
+            with torch.cuda.stream(self.load_stream):
+                fill(self._inbufs[t], self._in_views[t])
+                ready = torch.cuda.Event()
+                ready.record(self.load_stream)
+            main.wait_event(ready)
+            self.select_inputs(t)
+        if not self._fp8_calibrated:
+            self.calibrate_fp8()
+
     def set_batch(self, planes: torch.Tensor, player: torch.Tensor, rank: torch.Tensor,
                   labels: torch.Tensor, non_blocking: bool = True):
         """Copy one batch into the static input buffers (device or pinned host tensors)."""
-        self.planes.copy_(planes.reshape(self.B, 9, NUM_POINTS), non_blocking=non_blocking)
-        self.player.copy_(player, non_blocking=non_blocking)
-        self.rank.copy_(rank, non_blocking=non_blocking)
-        self.labels.copy_(labels, non_blocking=non_blocking)
-        if not self._fp8_calibrated:
-            self.calibrate_fp8()
+        def fill(_, v):
+            v[0].copy_(planes.reshape(self.B, 9, NUM_POINTS), non_blocking=non_blocking)
+            v[1].copy_(player, non_blocking=non_blocking)
+            v[2].copy_(rank, non_blocking=non_blocking)
+            v[3].copy_(labels, non_blocking=non_blocking)
+            if self.load_stream is not None:
+                for x in (planes, player, rank, labels):
+                    if x.is_cuda:
+                        x.record_stream(self.load_stream)
+        self._load(fill, any(x.is_cuda for x in (planes, player, rank, labels)))
 
     def set_batch_packed(self, packed: torch.Tensor, non_blocking: bool = True):
         """One copy of a ``pack_batch`` buffer (device or pinned host) into the inputs."""
-        self.inbuf.copy_(packed, non_blocking=non_blocking)
-        if not self._fp8_calibrated:
-            self.calibrate_fp8()
+        def fill(buf, _):
+            buf.copy_(packed, non_blocking=non_blocking)
+            if packed.is_cuda and self.load_stream is not None:
+                packed.record_stream(self.load_stream)
+        self._load(fill, packed.is_cuda)
 
     def set_batch_packed_from(self, loader):
-        """Next batch of a BatchLoader with pinned packed slots: one async copy."""
-        loader.next_packed_to(self.inbuf)
-        if not self._fp8_calibrated:
-            self.calibrate_fp8()
+        """Next batch of a BatchLoader with pinned packed slots: one async copy (the loader
+        releases the slot on an event recorded on the stream that copied it)."""
+        self._load(lambda buf, _: loader.next_packed_to(buf), False)
 
     def forward(self):
         s = stream_handle()
@@ -1055,8 +1135,22 @@ class SegmentedStep:
         self.opt_graph = None
         self.full_graph = None
         self.fb_graph = None
+        # one graph set per input buffer (HipGoNet.enable_prefetch): the replay picks the
+        # set of the buffer the last set_batch filled
+        self._gsets = {}
         if use_graphs:
-            self._capture(warmup)
+            cur = net.cur_in
+            for k in range(len(net._inbufs)):
+                net.select_inputs(k)
+                self._capture(warmup)
+                self._gsets[k] = (self.graphs, self.fb_graph, self.full_graph)
+                self.graphs = []
+            net.select_inputs(cur)
+            self.graphs, self.fb_graph, self.full_graph = self._gsets[cur]
+
+    def _pick(self):
+        if len(self._gsets) > 1:
+            self.graphs, self.fb_graph, self.full_graph = self._gsets[self.net.cur_in]
 
     @staticmethod
     def _call_all(fns):
@@ -1115,6 +1209,7 @@ class SegmentedStep:
 
     def forward_backward(self):
         """Gradients (all-reduced across ranks when DP) of the batch in the input buffers."""
+        self._pick()
         if self.fb_graph is not None:
             with trace.range("fwd_bwd_graph"):
                 self.fb_graph.replay()
@@ -1144,6 +1239,7 @@ class SegmentedStep:
                 self.net.optimizer_step()
 
     def __call__(self):
+        self._pick()
         if self.full_graph is not None:
             with trace.range("step_graph"):
                 self.full_graph.replay()

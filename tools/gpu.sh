@@ -18,7 +18,8 @@
 #   pmcx:C1,C2,..:SCRIPT  one rocprofv3 --pmc pass of the listed counters over python SCRIPT
 #   list             rocprofv3 -L -> gpurun_out/counters.txt
 #   py:SCRIPT ARGS   python SCRIPT ARGS (a tools/ script), stdout -> gpurun_out/py_<n>.log
-#   ab:R:A|B|...     R interleaved rounds of bench.py under env settings A, B, ... ("-" = none)
+#   ab:R:A|B|...     R interleaved rounds of bench.py under env settings A, B, ... ("-" = none;
+#                    extra bench.py arguments from $AB_ARGS)
 set -o pipefail
 mkdir -p gpurun_out
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -90,7 +91,7 @@ for step in "$@"; do
       for r in $(seq 1 $rounds); do
         for cfg in "${cfgs[@]}"; do
           e="$cfg"; [ "$e" = "-" ] && e=""
-          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 2>/dev/null \
+          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 ${AB_ARGS:-} 2>/dev/null \
                 | grep metric) || { rc=1; break 2; }
           echo "$cfg $(echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")" \
             | tee -a gpurun_out/ab.txt

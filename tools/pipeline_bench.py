@@ -3,7 +3,7 @@ packed slots -> one async H2D copy -> graphed step), on the packed reference fix
 flagship shape (12 layers x 128 channels, batch 256).  Compare with bench.py (synthetic,
 device-resident pool) to see what the input pipeline costs.
 
-Usage: python tools/pipeline_bench.py [--iters 400] [--threads 4] [--data data_cache/fixture]"""
+Usage: python tools/pipeline_bench.py [--iters 400] [--threads 4] [--data tests/fixtures]"""
 import argparse
 import json
 import os
@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--ch", type=int, default=128)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--data", default="data_cache/fixture")
+    ap.add_argument("--data", default="tests/fixtures")
     a = ap.parse_args()
     import torch
     from deep_go_amd.config import ExperimentConfig
