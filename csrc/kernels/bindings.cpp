@@ -68,6 +68,8 @@ void dg_conv_wgrad_win_set_swp(int on);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void* X, void* Y,
                           void* mask, int C, int B, hipStream_t stream);
+hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
+                                hipStream_t stream);
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                              int KP, int splits, hipStream_t stream);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
@@ -371,6 +373,12 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_layer2");
   }, "one hidden 3x3 C -> C layer (C = 256 | 128) on conv_stack2's K loop: epi 1 forward "
      "(fragment weights, pbias_frag, mask written), 2 backward-data (mask of the layer below)");
+  m.def("conv_layer2_multi", [](int epi, uintptr_t table, int nl, int C, int B,
+                               uintptr_t stream) {
+    check(dg_conv_layer2_multi(epi, P<long long>(table), nl, C, B, S(stream)),
+          "conv_layer2_multi");
+  }, "a run of nl conv_layer2 layers in one launch (one workgroup per board, the layers "
+     "chained through the board's own L2-resident output); table rows {A, pbias, X, Y, mask}");
   m.def("conv_wgrad_win", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
                              int splits, uintptr_t stream) {
     check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),

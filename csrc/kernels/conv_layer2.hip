@@ -227,6 +227,199 @@ hipError_t launch_layer2(const LayerArgs& a, int B, hipStream_t stream) {
   return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------------------------
+// conv_layer2_multi: a RUN of nl hidden layers (forward: X_l+1 = Y_l; backward-data: the
+// dZ chain top -> down) in ONE launch, one workgroup per board (grid B), on the same K loop.
+// A board's next layer only reads that board's own output, which this workgroup just wrote
+// (L2-resident; its stores drained with vmcnt(0) and a barrier before the next layer's
+// chunk DMA reads them), so the layers need no grid-wide synchronisation.  Per layer the
+// workgroup runs the C/128 output halves back to back; the second half reads the same input
+// frame, so its chunk 0 is staged into buffer 0 during the first half's last chunk (which
+// sits in buffer 1) and the epilogue stages in buffer 1 + a 35 KB extension: the half's
+// prologue (chunk-0 DMA latency) disappears and its epilogue stores drain under the next
+// half's MFMAs.  Per-item math is the single-layer kernel's, so outputs are bit-identical.
+constexpr int MAXL2 = 16;
+struct MultiArgs {
+  LayerArgs L[MAXL2];
+  int nl;
+};
+constexpr int STG_OFF = H_BYTES;                       // epilogue staging: buffer 1 + ext
+constexpr int LDS_MULTI = H_BYTES + NPTS * 256;        // 149760 B
+static_assert(LDS_MULTI <= 160 * 1024, "LDS");
+
+template <int EPI>
+__global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int b = blockIdx.x;
+  const int C = m.L[0].C, nch = C / 64, nsteps = nch * T, nh = C / 128;
+  const int nitems = m.nl * nh;
+
+  auto stage_H = [&](const char* Xb, int buf, int c, int j) {
+    const int rl = j * 8 + (lane >> 3);
+    const int r = rl < FF ? rl : FF - 1;
+    const int gs = (lane & 7) ^ fsig(rl);
+    glds16(Xb + ((size_t)r * C + c * 64 + gs * 8) * 2, (LDS_AS void*)(smem + buf * H_BYTES + j * 1024));
+  };
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  uint32_t pk[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int hh = p / BOARD, w = p - (p / BOARD) * BOARD;
+    pk[j] = (uint32_t)(((hh + 1) * F + (w + 1)) * 128) | ((uint32_t)(((w + 1) + 3 * (hh + 1)) & 7) << 16);
+  }
+  const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
+  auto load_A = [&](const char* A, int kk, bf16x8 (&r)[MF]) {
+    const char* p = A + a_lane + kk * MF * 1024;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) r[i] = *(const bf16x8*)(p + i * 1024);
+  };
+  auto read_B = [&](const char* sHc, int t, int kk, bf16x8 (&bfr)[NF]) {
+    const int toff = (t / 3 - 1) * F + (t % 3 - 1);
+    const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int off = (int)(pk[j] & 0xFFFFu) + toff * 128 +
+                      ((lq ^ (((int)(pk[j] >> 16) + tsig) & 7)) * 16);
+      bfr[j] = lds_read_b128((const LDS_AS char*)(sHc + (off ^ (kk * 64))));
+    }
+  };
+  auto mma = [&](const bf16x8 (&af)[MF], const bf16x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+  };
+
+  bool staged = false;   // buffer 0 already holds this item's chunk 0
+#pragma unroll 1
+  for (int it = 0; it < nitems; ++it) {
+    const int l = it / nh, h = it - (it / nh) * nh;
+    const bool next_same = h + 1 < nh;     // the next item reads the same input frame
+    const char* Xb = m.L[l].X + (size_t)b * FF * C * 2;
+    const char* Ah = m.L[l].A + (size_t)h * nsteps * STEP_BYTES;
+    if (!staged)
+      for (int j = wave; j < HROWS / 8; j += NW) stage_H(Xb, 0, 0, j);
+    __syncthreads();  // chunk 0 landed
+
+    bf16x8 Ak[2][MF];
+    load_A(Ah, 0, Ak[0]);
+    load_A(Ah, 1, Ak[1]);
+    f32x4 acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c = 0; c < nch; ++c) {
+      const char* sHc = smem + (c & 1) * H_BYTES;
+      const bool dma = c + 1 < nch || next_same;
+      const int cn = c + 1 < nch ? c + 1 : 0;       // chunk (of this or the next item) to stage
+#pragma unroll 1
+      for (int t = 0; t < T; ++t) {
+        const int s = c * T + t;
+        const char* An = s + 1 < nsteps ? Ah + (s + 1) * STEP_BYTES : Ah;
+        bf16x8 bfr[NF];
+        read_B(sHc, t, 0, bfr);
+        mma(Ak[0], bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        load_A(An, 0, Ak[0]);
+        read_B(sHc, t, 1, bfr);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(Ak[1], bfr, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        load_A(An, 1, Ak[1]);
+        if (dma && t < HROWS / 8 / NW) stage_H(Xb, (c + 1) & 1, cn, wave * (HROWS / 8 / NW) + t);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();  // the staged chunk landed; every wave is past chunk c's reads
+    }
+
+    // ---- epilogue (the single-layer kernel's, staged at STG_OFF) ----
+    const LayerArgs& a = m.L[l];
+    int z0 = 0;
+    asm volatile("" : "+v"(z0));
+    uint2 eb[NF][EPI == EPI_FWD ? MF : 1];
+    uint2 em[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = min(wn * NF * 16 + j * 16 + lr, NPTS - 1);
+      if constexpr (EPI == EPI_FWD) {
+        const uint2* pf = (const uint2*)a.pbias + (((h * 24 + wn * NF + j) * 2 + wm) * 4) * 64 + lane + z0;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) eb[j][i] = pf[i * 64];
+      } else {
+        em[j] = *(const uint2*)(a.mask + ((size_t)b * NPTS + p) * (C / 8) + h * 16 + wm * 8 + z0);
+      }
+    }
+    char* stg = smem + STG_OFF;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = wn * NF * 16 + j * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const int cl = wm * 64 + i * 16 + lq * 4;
+        const f32x4 v = acc[i][j];
+        uint2 o;
+        if constexpr (EPI == EPI_FWD) {
+          o.x = relu_bf16x2(f32x2{v[0], v[1]} + bf16x2_f32(eb[j][i].x));
+          o.y = relu_bf16x2(f32x2{v[2], v[3]} + bf16x2_f32(eb[j][i].y));
+        } else {
+          const int cw = i * 16 + lq * 4;
+          const uint32_t word = (i < 2) ? em[j].x : em[j].y;
+          const uint32_t nib = word >> ((cw & 31) >> 3 << 3) >> (cw & 4);
+          o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
+          o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
+        }
+        if (p < NPTS) *(uint2*)(stg + z0 + p * 256 + (((cl >> 3) ^ (p & 15)) * 16) + (cl & 4) * 2) = o;
+      }
+    }
+    lds_barrier();
+    char* Yb = a.Y + (size_t)b * FF * C * 2;
+    uint8_t* mk = a.mask ? a.mask + (size_t)b * NPTS * (C / 8) : nullptr;
+    for (int u = tid; u < NPTS * 16; u += NT) {
+      const int p = u >> 4, q = u & 15;
+      const uint4 v = *(const uint4*)(stg + p * 256 + ((q ^ (p & 15)) * 16));
+      const int hh = p / BOARD, w = p - (p / BOARD) * BOARD;
+      const int f = (hh + 1) * F + (w + 1);
+      *(uint4*)(Yb + ((size_t)f * C + h * 128 + q * 8) * 2) = v;
+      if (EPI == EPI_FWD && mk) {
+        const uint32_t mm = (((v.x + 0x7fff7fffu) >> 15) & 0x10001u) |
+                            (((v.y + 0x7fff7fffu) >> 13) & 0x40004u) |
+                            (((v.z + 0x7fff7fffu) >> 11) & 0x100010u) |
+                            (((v.w + 0x7fff7fffu) >> 9) & 0x400040u);
+        mk[(size_t)p * (C / 8) + h * 16 + q] = (uint8_t)(mm | (mm >> 15));
+      }
+    }
+    if (!next_same) {
+      // the next layer reads this layer's output: every wave's stores complete (vmcnt(0);
+      // this CU's own L2 lines, never read before in this launch) before the barrier
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    __syncthreads();  // staging reads done before the next item's chunk-1 DMA into buffer 1
+    staged = next_same;
+  }
+}
+
+template <int EPI>
+hipError_t launch_layer2_multi(const MultiArgs& m, int B, hipStream_t stream) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MULTI);
+    done = true;
+  }
+  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI>), dim3(B), dim3(NT), LDS_MULTI, stream, m);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -241,6 +434,28 @@ hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void*
   LayerArgs a{(const char*)A, (const bf16_t*)pbias, (const char*)X, (char*)Y, (uint8_t*)mask, C};
   if (epi == EPI_FWD) return launch_layer2<EPI_FWD>(a, B, stream);
   if (epi == EPI_DGRAD) return launch_layer2<EPI_DGRAD>(a, B, stream);
+  return hipErrorInvalidValue;
+}
+
+// nl layers in one launch: table = nl rows of {A, pbias, X, Y, mask} (int64); row l + 1's X
+// must be row l's Y (checked).  C = 256 | 128 as above.
+hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
+                                hipStream_t stream) {
+  if ((C != 128 && C != 256) || B <= 0 || nl <= 0 || nl > MAXL2) return hipErrorInvalidValue;
+  MultiArgs m{};
+  m.nl = nl;
+  for (int i = 0; i < nl; ++i) {
+    const long long* t = table + 5 * i;
+    LayerArgs& a = m.L[i];
+    a = LayerArgs{(const char*)t[0], (const bf16_t*)t[1], (const char*)t[2], (char*)t[3],
+                  (uint8_t*)t[4], C};
+    if (!a.A || !a.X || !a.Y) return hipErrorInvalidValue;
+    if (epi == EPI_FWD && !a.pbias) return hipErrorInvalidValue;
+    if (epi == EPI_DGRAD && !a.mask) return hipErrorInvalidValue;
+    if (i > 0 && a.X != m.L[i - 1].Y) return hipErrorInvalidValue;
+  }
+  if (epi == EPI_FWD) return launch_layer2_multi<EPI_FWD>(m, B, stream);
+  if (epi == EPI_DGRAD) return launch_layer2_multi<EPI_DGRAD>(m, B, stream);
   return hipErrorInvalidValue;
 }
 

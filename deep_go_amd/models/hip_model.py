@@ -370,6 +370,8 @@ class HipGoNet:
                     self.fp8_scales.data_ptr() + (2 * i + 1) * 4,
                     self.fp8_amax.data_ptr() + i * 4)))
         self._fuse_forward_stack()
+        self._l2_tables = []
+        self._fwd, self._fwd_owner = self._merge_layer2_runs(self._fwd, self._fwd_owner)
         hd = self.head
         hx = self.act[-1]
         self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
@@ -457,6 +459,47 @@ class HipGoNet:
                                             self.act[i - 1].data_ptr(), spec.pad)))
             self._bwd.append(ops)
         self._fuse_dgrad_stack()
+        self._bwd_pre, _ = self._merge_layer2_runs(self._bwd_pre)
+
+    def _merge_layer2_runs(self, ops, owners=None):
+        """Consecutive conv_layer2 launches of one kind whose layers chain (X of the next =
+        Y of the previous) become ONE conv_layer2_multi launch: one workgroup per board runs
+        the whole run, the second output half of a layer starts on a prefetched input chunk
+        and the epilogue stores drain under the next half's MFMAs (csrc/kernels/
+        conv_layer2.hip; bit-identical outputs).  DG_LAYER2_MULTI=0: per-layer launches."""
+        h = self.h
+        owners = list(owners) if owners is not None else [None] * len(ops)
+        if os.environ.get("DG_LAYER2_MULTI", "1") == "0":
+            return ops, owners
+        out, out_own, run = [], [], []
+
+        def flush():
+            if len(run) >= 2:
+                a0 = run[0][0][1]
+                rows = [[a[1], a[2], a[3], a[4], a[5]] for (_, a), _ in run]
+                tab = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+                self._l2_tables.append(tab)
+                out.append((h.conv_layer2_multi, (a0[0], tab.ctypes.data, len(run), a0[6],
+                                                  a0[7])))
+                out_own.append(run[0][1])
+            else:
+                for op, ow in run:
+                    out.append(op)
+                    out_own.append(ow)
+            run.clear()
+        for op, ow in zip(ops, owners):
+            f, a = op
+            if f is h.conv_layer2:
+                if run and (a[0] != run[-1][0][1][0] or a[3] != run[-1][0][1][4]
+                            or len(run) == 16):
+                    flush()
+                run.append((op, ow))
+            else:
+                flush()
+                out.append(op)
+                out_own.append(ow)
+        flush()
+        return out, out_own
 
     def _fuse_forward_stack(self):
         """Replace the per-layer forward launches of the longest run of hidden 128->128 3x3
@@ -722,7 +765,8 @@ class HipGoNet:
                             and 0 not in grouped
                             and all(i in grouped for i in range(1, groups[-1][0] + 1))
                             else None)
-        if self._l0_side_at is not None and 1 in self._pre_dgrads:
+        if (self._l0_side_at is not None and 1 in self._pre_dgrads
+                and os.environ.get("DG_L1_DGRAD_SIDE", "1") != "0"):
             # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
             drop = set(id(op) for op in self._pre_dgrads[1])
             self._bwd_pre = [op for op in self._bwd_pre if id(op) not in drop]

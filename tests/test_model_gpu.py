@@ -286,8 +286,9 @@ def test_layer2_matches_board_kernel_at_256(monkeypatch):
     _, n0, _ = _setup(5, 256, 4, seed=31)
     monkeypatch.setenv("DG_LAYER2", "1")
     _, n1, _ = _setup(5, 256, 4, seed=31)
-    assert any(f is n1.h.conv_layer2 for f, _ in n1._fwd)
-    assert not any(f is n0.h.conv_layer2 for f, _ in n0._fwd)
+    l2 = (n1.h.conv_layer2, n1.h.conv_layer2_multi)
+    assert any(f in l2 for f, _ in n1._fwd)
+    assert not any(f in l2 for f, _ in n0._fwd)
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
@@ -301,6 +302,34 @@ def test_layer2_matches_board_kernel_at_256(monkeypatch):
     assert torch.equal(n0.loss, n1.loss)
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
+
+@pytest.mark.parametrize("l1_side", ["1", "0"])
+def test_layer2_multi_matches_per_layer_launches(l1_side, monkeypatch):
+    """conv_layer2_multi (a run of d = 256 layers in one launch, one workgroup per board, the
+    second output half on a prefetched input chunk) is bit-identical to the per-layer
+    conv_layer2 launches at 12 layers: activations, masks, every dZ, loss and gradients."""
+    monkeypatch.setenv("DG_L1_DGRAD_SIDE", l1_side)
+    monkeypatch.setenv("DG_LAYER2_MULTI", "0")
+    _, n0, _ = _setup(12, 256, 6, seed=41)
+    monkeypatch.setenv("DG_LAYER2_MULTI", "1")
+    _, n1, _ = _setup(12, 256, 6, seed=41)
+    h = n1.h
+    assert sum(f is h.conv_layer2_multi for f, _ in n1._fwd) == 1
+    assert sum(f is h.conv_layer2_multi for f, _ in n1._bwd_pre) == 1
+    assert not any(f is h.conv_layer2 for f, _ in n1._fwd + n1._bwd_pre)
+    for _ in range(2):
+        n0.forward_backward()
+        n1.forward_backward()
+    torch.cuda.synchronize()
+    for a0, a1 in zip(n0.act, n1.act):
+        assert torch.equal(a0, a1)
+    for m0, m1 in zip(n0.relu_mask, n1.relu_mask):
+        if m0 is not None:
+            assert torch.equal(m0, m1)
+    for d0, d1 in zip(n0.dz, n1.dz):
+        assert torch.equal(d0, d1)
+    assert torch.equal(n0.loss, n1.loss)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 def test_first_layer_fused_into_forward_stack(monkeypatch):
     """conv_stack2 l1 mode: the 5x5 first layer runs inside the forward stack's launch
@@ -325,7 +354,7 @@ def test_first_layer_fused_into_forward_stack(monkeypatch):
         if m0 is not None:
             assert torch.equal(m0, m1)
     assert torch.equal(n0.loss, n1.loss)
-    assert torch.equal(n0.grads, n1.grads)
+    assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
 
 @pytest.mark.parametrize("layers", [4, 7])
