@@ -231,14 +231,15 @@ hipError_t launch_layer2(const LayerArgs& a, int B, hipStream_t stream) {
 // ------------------------------------------------------------------------------------
 // conv_layer2_multi: a RUN of nl hidden layers (forward: X_l+1 = Y_l; backward-data: the
 // dZ chain top -> down) in ONE launch, one workgroup per board (grid B), on the same K loop.
-// A board's next layer only reads that board's own output, which this workgroup just wrote
-// (L2-resident; its stores drained with vmcnt(0) and a barrier before the next layer's
-// chunk DMA reads them), so the layers need no grid-wide synchronisation.  Per layer the
-// workgroup runs the C/128 output halves back to back; the second half reads the same input
-// frame, so its chunk 0 is staged into buffer 0 during the first half's last chunk (which
-// sits in buffer 1) and the epilogue stages in buffer 1 + a 35 KB extension: the half's
-// prologue (chunk-0 DMA latency) disappears and its epilogue stores drain under the next
-// half's MFMAs.  Per-item math is the single-layer kernel's, so outputs are bit-identical.
+// A board's next layer only reads that board's own output, which this workgroup wrote
+// (L2-resident; every wave retires its stores with vmcnt(0) at the next item's chunk-0
+// barrier, before any DMA of the channels they hold), so the layers need no grid-wide
+// synchronisation.  Per layer the workgroup runs the C/128 output halves back to back.  The
+// next item's chunk 0 is staged into buffer 0 during the current item's last chunk (which
+// sits in buffer 1): the same frame for the second half, the next layer's channels 0..63
+// (written by the first half) at a layer change; the epilogue stages in buffer 1 + a 35 KB
+// extension.  No item after the first waits for a chunk-0 DMA, and the epilogue stores drain
+// under the next item's MFMAs.  Per-item math is the single-layer kernel's (bit-identical).
 constexpr int MAXL2 = 16;
 struct MultiArgs {
   LayerArgs L[MAXL2];
@@ -305,9 +306,16 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
     const bool next_same = h + 1 < nh;     // the next item reads the same input frame
     const char* Xb = m.L[l].X + (size_t)b * FF * C * 2;
     const char* Ah = m.L[l].A + (size_t)h * nsteps * STEP_BYTES;
-    if (!staged)
+    // the next item's chunk 0 (channels 0..63) is staged during this item's last chunk: the
+    // same frame, or — at a layer change with two output halves — the next layer's input,
+    // whose channels 0..63 the FIRST half of this layer wrote (its stores completed at this
+    // item's chunk-0 barrier)
+    const bool pf_next = next_same || (nh > 1 && l + 1 < m.nl);
+    const char* Xn = next_same ? Xb : (l + 1 < m.nl ? m.L[l + 1].X + (size_t)b * FF * C * 2 : Xb);
+    if (!staged) {
       for (int j = wave; j < HROWS / 8; j += NW) stage_H(Xb, 0, 0, j);
-    __syncthreads();  // chunk 0 landed
+      __syncthreads();  // chunk 0 landed
+    }  // (else it landed at the previous item's last-chunk barrier)
 
     bf16x8 Ak[2][MF];
     load_A(Ah, 0, Ak[0]);
@@ -320,8 +328,9 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
 
     for (int c = 0; c < nch; ++c) {
       const char* sHc = smem + (c & 1) * H_BYTES;
-      const bool dma = c + 1 < nch || next_same;
+      const bool dma = c + 1 < nch || pf_next;
       const int cn = c + 1 < nch ? c + 1 : 0;       // chunk (of this or the next item) to stage
+      const char* Xs = c + 1 < nch ? Xb : Xn;
 #pragma unroll 1
       for (int t = 0; t < T; ++t) {
         const int s = c * T + t;
@@ -336,9 +345,12 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
         mma(Ak[1], bfr, acc);
         __builtin_amdgcn_sched_barrier(0);
         load_A(An, 1, Ak[1]);
-        if (dma && t < HROWS / 8 / NW) stage_H(Xb, (c + 1) & 1, cn, wave * (HROWS / 8 / NW) + t);
+        if (dma && t < HROWS / 8 / NW) stage_H(Xs, (c + 1) & 1, cn, wave * (HROWS / 8 / NW) + t);
         __builtin_amdgcn_sched_barrier(0);
       }
+      // chunk 0's barrier also retires the previous item's epilogue stores (vmcnt(0) in every
+      // wave): chunk 2+ of a new layer read them, and their DMAs issue after this barrier
+      if (c == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();  // the staged chunk landed; every wave is past chunk c's reads
     }
 
@@ -398,13 +410,10 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
         mk[(size_t)p * (C / 8) + h * 16 + q] = (uint8_t)(mm | (mm >> 15));
       }
     }
-    if (!next_same) {
-      // the next layer reads this layer's output: every wave's stores complete (vmcnt(0);
-      // this CU's own L2 lines, never read before in this launch) before the barrier
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-    }
-    __syncthreads();  // staging reads done before the next item's chunk-1 DMA into buffer 1
-    staged = next_same;
+    // staging reads done (LDS only) before the next item's chunk-1 DMA into buffer 1; the
+    // global stores keep draining under the next item's MFMAs
+    lds_barrier();
+    staged = pf_next;
   }
 }
 
