@@ -597,6 +597,7 @@ class HipGoNet:
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
+        self._l0_first_at = None   # ... runs it on the main stream first (DG_L0_FIRST)
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
         if os.environ.get("DG_DSTACK", "1") == "0":
@@ -727,6 +728,7 @@ class HipGoNet:
         self.wgroups: List[List[int]] = []
         self.win_groups = set()
         self._l0_side_at = None
+        self._l0_first_at = None
         G = int(os.environ.get("DG_WGRAD_GROUP", "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
         if G < 2 or self.side_mode not in ("none", "bias"):
@@ -761,10 +763,16 @@ class HipGoNet:
         # shared slab / bias-partial buffers while layer 0's chain still uses them on the
         # side stream (e.g. 8 layers under DP: groups [6..2] and [1] -> [1] is dropped).
         grouped = set(i for g in groups for i in g)
-        self._l0_side_at = (groups[-1][0] if self.side_mode == "bias" and self._dgrad_first
-                            and 0 not in grouped
-                            and all(i in grouped for i in range(1, groups[-1][0] + 1))
-                            else None)
+        l0_ok = (self.side_mode == "bias" and self._dgrad_first and 0 not in grouped
+                 and all(i in grouped for i in range(1, groups[-1][0] + 1)))
+        # DG_L0_FIRST=1: layer 0's gradient chain runs on the main stream BEFORE the last
+        # group's weight-gradient launch instead of on the side stream after the group's bias
+        # partials (which stretch over the whole window kernel beside it, leaving the side
+        # chain in the step's tail).  Measured slower at both widths (12x128 -2.1%, 12x256
+        # -0.4%: profiles/r2_l0_first_ab.txt), so off by default
+        first = os.environ.get("DG_L0_FIRST", "0") == "1"
+        self._l0_first_at = groups[-1][0] if l0_ok and first else None
+        self._l0_side_at = groups[-1][0] if l0_ok and not first else None
         if (self._l0_side_at is not None and 1 in self._pre_dgrads
                 and os.environ.get("DG_L1_DGRAD_SIDE", "1") != "0"):
             # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
@@ -995,7 +1003,11 @@ class HipGoNet:
         elif self.side_mode == "bias":
             side = self.side
             l0_side = self._l0_side_at == i
-            if i == 0 and self._l0_side_at is not None:
+            if i == self._l0_first_at:
+                self._run(self._bwd[0][:3], main.cuda_stream)   # layer 0's chain, main first
+            if i == 0 and self._l0_first_at is not None:
+                pass                                 # ran before the last group's launch
+            elif i == 0 and self._l0_side_at is not None:
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final

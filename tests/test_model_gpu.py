@@ -331,6 +331,27 @@ def test_layer2_multi_matches_per_layer_launches(l1_side, monkeypatch):
     assert torch.equal(n0.loss, n1.loss)
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
+@pytest.mark.parametrize("ch", [128, 256])
+def test_layer0_chain_first_matches_side_chain(ch, monkeypatch):
+    """DG_L0_FIRST=1 (layer 0's gradient chain on the main stream before the last group's
+    weight-gradient launch) and =0 (on the side stream after the group's bias partials)
+    produce the same gradients, through the one-graph step too."""
+    from deep_go_amd.models.hip_model import SegmentedStep
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DG_L0_FIRST", mode)
+        _, net, _ = _setup(12, ch, 6, seed=43)
+        assert (net._l0_first_at is not None) == (mode == "1")
+        net.forward_backward()
+        torch.cuda.synchronize()
+        g = net.grads.clone()
+        step = SegmentedStep(net, None, use_graphs=True)
+        step()
+        torch.cuda.synchronize()
+        res.append((g, net.params.clone()))
+    assert torch.allclose(res[0][0], res[1][0], rtol=1e-6, atol=1e-9)
+    assert torch.allclose(res[0][1], res[1][1], rtol=1e-6, atol=1e-9)
+
 def test_first_layer_fused_into_forward_stack(monkeypatch):
     """conv_stack2 l1 mode: the 5x5 first layer runs inside the forward stack's launch
     (default) — its fragment-ordered weights are fwd_weight permuted by stack_frag_linear,
