@@ -18,6 +18,8 @@
 // backward (train.lua:10).
 #include "dg_common.h"
 
+#include <cstdlib>
+
 using namespace dg;
 
 namespace {
@@ -249,7 +251,7 @@ constexpr int STG_OFF = H_BYTES;                       // epilogue staging: buff
 constexpr int LDS_MULTI = H_BYTES + NPTS * 256;        // 149760 B
 static_assert(LDS_MULTI <= 160 * 1024, "LDS");
 
-template <int EPI>
+template <int EPI, int BPF>
 __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -335,14 +337,27 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
       for (int t = 0; t < T; ++t) {
         const int s = c * T + t;
         const char* An = s + 1 < nsteps ? Ah + (s + 1) * STEP_BYTES : Ah;
-        bf16x8 bfr[NF];
-        read_B(sHc, t, 0, bfr);
-        mma(Ak[0], bfr, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        load_A(An, 0, Ak[0]);
-        read_B(sHc, t, 1, bfr);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(Ak[1], bfr, acc);
+        if constexpr (BPF == 1) {
+          // k-half 1's B fragments read before k-half 0's MFMAs (+24 VGPRs): their LDS
+          // latency hides under this wave's own MFMAs, not only the SIMD partner's
+          bf16x8 bfr[NF], bfr1[NF];
+          read_B(sHc, t, 0, bfr);
+          read_B(sHc, t, 1, bfr1);
+          mma(Ak[0], bfr, acc);
+          __builtin_amdgcn_sched_barrier(0);
+          load_A(An, 0, Ak[0]);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(Ak[1], bfr1, acc);
+        } else {
+          bf16x8 bfr[NF];
+          read_B(sHc, t, 0, bfr);
+          mma(Ak[0], bfr, acc);
+          __builtin_amdgcn_sched_barrier(0);
+          load_A(An, 0, Ak[0]);
+          read_B(sHc, t, 1, bfr);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(Ak[1], bfr, acc);
+        }
         __builtin_amdgcn_sched_barrier(0);
         load_A(An, 1, Ak[1]);
         if (dma && t < HROWS / 8 / NW) stage_H(Xs, (c + 1) & 1, cn, wave * (HROWS / 8 / NW) + t);
@@ -417,16 +432,29 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
   }
 }
 
-template <int EPI>
+template <int EPI, int BPF>
 hipError_t launch_layer2_multi(const MultiArgs& m, int B, hipStream_t stream) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI>,
+    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI, BPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MULTI);
     done = true;
   }
-  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI>), dim3(B), dim3(NT), LDS_MULTI, stream, m);
+  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI, BPF>), dim3(B), dim3(NT), LDS_MULTI, stream,
+                     m);
   return hipGetLastError();
+}
+
+// DG_L2_BPF (B-fragment read-ahead in the K loop): 1 (default) k-half 1 read before k-half
+// 0's MFMAs (+0.5% at 12x256), 0 none.  (Also reading the next step's k-half 0 under k-half
+// 1's MFMAs, 242-252 VGPRs, measured -4.5%: profiles/r2_layer2_multi_ab.txt.)
+int layer2_bpf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DG_L2_BPF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
 }
 
 }  // namespace
@@ -463,8 +491,13 @@ hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, 
     if (epi == EPI_DGRAD && !a.mask) return hipErrorInvalidValue;
     if (i > 0 && a.X != m.L[i - 1].Y) return hipErrorInvalidValue;
   }
-  if (epi == EPI_FWD) return launch_layer2_multi<EPI_FWD>(m, B, stream);
-  if (epi == EPI_DGRAD) return launch_layer2_multi<EPI_DGRAD>(m, B, stream);
+  const int bpf = layer2_bpf();
+  if (epi == EPI_FWD)
+    return bpf ? launch_layer2_multi<EPI_FWD, 1>(m, B, stream)
+               : launch_layer2_multi<EPI_FWD, 0>(m, B, stream);
+  if (epi == EPI_DGRAD)
+    return bpf ? launch_layer2_multi<EPI_DGRAD, 1>(m, B, stream)
+               : launch_layer2_multi<EPI_DGRAD, 0>(m, B, stream);
   return hipErrorInvalidValue;
 }
 
