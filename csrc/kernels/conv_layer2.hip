@@ -251,7 +251,7 @@ constexpr int STG_OFF = H_BYTES;                       // epilogue staging: buff
 constexpr int LDS_MULTI = H_BYTES + NPTS * 256;        // 149760 B
 static_assert(LDS_MULTI <= 160 * 1024, "LDS");
 
-template <int EPI, int BPF, bool DIRECT>
+template <int EPI, int BPF>
 __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -390,50 +390,6 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
         em[j] = *(const uint2*)(a.mask + ((size_t)b * NPTS + p) * (C / 8) + h * 16 + wm * 8 + z0);
       }
     }
-    if constexpr (DIRECT) {
-      // no staging: each lane stores its 8-B (4-channel) pieces straight from the
-      // accumulators (a pixel's 4 lq lanes cover 32 contiguous bytes; the 4 i fragments of
-      // the wave fill its 128-B lines in L2), the forward's mask byte (8 channels) from the
-      // lane's nibble and its lq-partner's (lane ^ 16).  No LDS traffic and no barrier: the
-      // next item starts while the stores drain.
-      char* Yb = a.Y + (size_t)b * FF * C * 2;
-#pragma unroll
-      for (int j = 0; j < NF; ++j) {
-        const int p = wn * NF * 16 + j * 16 + lr;
-        const int hh = p / BOARD, w = p - (p / BOARD) * BOARD;
-        const int f = (hh + 1) * F + (w + 1);
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          const int cl = wm * 64 + i * 16 + lq * 4;
-          const f32x4 v = acc[i][j];
-          uint2 o;
-          if constexpr (EPI == EPI_FWD) {
-            o.x = relu_bf16x2(f32x2{v[0], v[1]} + bf16x2_f32(eb[j][i].x));
-            o.y = relu_bf16x2(f32x2{v[2], v[3]} + bf16x2_f32(eb[j][i].y));
-          } else {
-            const int cw = i * 16 + lq * 4;
-            const uint32_t word = (i < 2) ? em[j].x : em[j].y;
-            const uint32_t nib = word >> ((cw & 31) >> 3 << 3) >> (cw & 4);
-            o.x = bf16x2_bits(f32x2{v[0], v[1]}) & pair_mask(nib);
-            o.y = bf16x2_bits(f32x2{v[2], v[3]}) & pair_mask(nib >> 2);
-          }
-          if (p < NPTS) *(uint2*)(Yb + ((size_t)f * C + h * 128 + cl) * 2 + z0) = o;
-          if constexpr (EPI == EPI_FWD) {
-            if (a.mask) {
-              const uint32_t m4 = (((o.x + 0x7fff7fffu) >> 15) & 0x10001u) |
-                                  (((o.y + 0x7fff7fffu) >> 13) & 0x40004u);
-              const uint32_t nb = (m4 | (m4 >> 15)) & 0xFu;
-              const uint32_t pn = (uint32_t)__shfl_xor((int)nb, 16);
-              if (p < NPTS && !(lq & 1))
-                a.mask[((size_t)b * NPTS + p) * (C / 8) + h * 16 + (cl >> 3)] =
-                    (uint8_t)(nb | (pn << 4));
-            }
-          }
-        }
-      }
-      staged = pf_next;
-      continue;
-    }
     char* stg = smem + STG_OFF;
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
@@ -480,33 +436,17 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
   }
 }
 
-template <int EPI, int BPF, bool DIRECT>
+template <int EPI, int BPF>
 hipError_t launch_layer2_multi(const MultiArgs& m, int B, hipStream_t stream) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI, BPF, DIRECT>,
+    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI, BPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MULTI);
     done = true;
   }
-  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI, BPF, DIRECT>), dim3(B), dim3(NT), LDS_MULTI,
-                     stream, m);
+  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI, BPF>), dim3(B), dim3(NT), LDS_MULTI, stream,
+                     m);
   return hipGetLastError();
-}
-
-template <int EPI, bool DIRECT>
-hipError_t launch_layer2_multi_b(const MultiArgs& m, int B, int bpf, hipStream_t stream) {
-  return bpf ? launch_layer2_multi<EPI, 1, DIRECT>(m, B, stream)
-             : launch_layer2_multi<EPI, 0, DIRECT>(m, B, stream);
-}
-
-// DG_L2_DIRECT: 1 = epilogue stores straight from the accumulators (no LDS staging)
-int layer2_direct() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DG_L2_DIRECT");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v;
 }
 
 // DG_L2_BPF (B-fragment read-ahead in the K loop): 1 (default) k-half 1 read before k-half
@@ -556,13 +496,12 @@ hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, 
     if (i > 0 && a.X != m.L[i - 1].Y) return hipErrorInvalidValue;
   }
   const int bpf = layer2_bpf();
-  const bool direct = layer2_direct();
   if (epi == EPI_FWD)
-    return direct ? launch_layer2_multi_b<EPI_FWD, true>(m, B, bpf, stream)
-                  : launch_layer2_multi_b<EPI_FWD, false>(m, B, bpf, stream);
+    return bpf ? launch_layer2_multi<EPI_FWD, 1>(m, B, stream)
+               : launch_layer2_multi<EPI_FWD, 0>(m, B, stream);
   if (epi == EPI_DGRAD)
-    return direct ? launch_layer2_multi_b<EPI_DGRAD, true>(m, B, bpf, stream)
-                  : launch_layer2_multi_b<EPI_DGRAD, false>(m, B, bpf, stream);
+    return bpf ? launch_layer2_multi<EPI_DGRAD, 1>(m, B, stream)
+               : launch_layer2_multi<EPI_DGRAD, 0>(m, B, stream);
   return hipErrorInvalidValue;
 }
 
