@@ -17,8 +17,7 @@ sides; the MAX elapsed over ranks is used (per-rank min/max ms are reported too)
 prints ONE JSON line.
 
 What one step is (nothing skipped inside the timed region):
-  next batch (uint8 planes/labels) copied into the static input buffers (double-buffered:
-  the copy runs on a load stream beside the previous step) ->
+  next batch (uint8 planes/labels) copied into the static input buffers ->
   GPU feature expansion -> 11 conv layers fwd -> fused head (loss, argmax, head bwd) ->
   bias-grad + wgrad + dgrad for every layer -> [N>1: bucketed RCCL all-reduce overlapped
   with backward] -> SGD with per-step LR decay -> bf16 weight refresh.
@@ -26,7 +25,20 @@ Weak scaling: 256 boards per GPU per step (BASELINE.json config "12-layer d=128 
 on one MI355X, batch=256"; global batch = 256*N).  Synthetic 19x19 positions, random-init
 weights (BASELINE.json: no datasets/checkpoints available).  Top-1 accuracy on synthetic
 random labels is meaningless and is not reported here; held-out top-1 on the real fixture
-comes from ``tools/fixture_accuracy.py`` (profiles/).
+comes from ``tools/real_data_run.py`` (profiles/).
+
+After the headline timing (never inside it) the same process measures:
+  * ``secondary``: the d=256 configs (BASELINE configs 3-5 per GPU: 12x256 bf16 and fp8) with
+    the same K/W and the same communicator (under N > 1 that is config 3/5's DP=N step);
+  * ``dp`` (N > 1 or --force-dp): communicator kind and RCCL version, per-rank devices, bytes
+    all-reduced per step, the step's bucket collectives timed alone (us/step, bus GB/s), the
+    same network's step without collectives, and from those the exposed communication time
+    and the fraction of it hidden behind compute.
+
+Multi-rank safety: every rank arms a phase guard (``utils/faults.PhaseGuard``: comm set-up,
+capture, warmup, timed, report; exit 42 and a status file on expiry) and the launcher bounds
+the whole child run.  If the native in-graph communicator (``--comm auto``) hangs, the
+launcher re-runs ONCE with ``--comm torch`` and says so in the JSON (``comm_fallback``).
 
 ``--cpu-dry-run``: the same launcher / rank / timing / JSON path on the CPU over gloo with
 the fp32 oracle at BASELINE config 1 size (tests/test_bench_launcher.py drives it at N=2, 4).
@@ -36,9 +48,12 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
+import signal
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 METRIC = "board-positions/sec (whole node) 12-layer d=128 CNN; top-1 move accuracy"
@@ -58,15 +73,23 @@ def parse(argv=None):
     ap.add_argument("--host-pool", action="store_true",
                     help="synthetic batches in pinned host memory (each step's copy is an H2D "
                          "copy, as from the trainer's loader) instead of device memory")
-    ap.add_argument("--bucket-mb", type=float, default=6.0,
-                    help="DP gradient bucket size (6 MB: head + the grouped hidden layers in "
-                         "one bucket, fired beside the first layer's gradient chain; the first "
-                         "layer in a second one)")
+    ap.add_argument("--bucket-mb", type=float, default=3.0,
+                    help="DP gradient bucket size; with --wgrad-group splitting the hidden "
+                         "layers, 3 MB gives one bucket per weight-gradient group (head + top "
+                         "group | bottom group | first layer)")
+    ap.add_argument("--wgrad-group", type=int, default=0,
+                    help="DP: hidden layers per grouped weight-gradient launch (0 = half of "
+                         "them, so the top group's all-reduce runs beside the bottom group's "
+                         "launch; >= the layer count = one launch)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
                          "torch = torch.distributed between graph segments, proxy = world-1 "
-                         "stand-in kernel on the comm stream (overlap measurement)")
+                         "RCCL-shaped stand-in kernel on the comm stream (overlap measurement)")
+    ap.add_argument("--proxy-world", type=int, default=8)
+    ap.add_argument("--proxy-gbps", type=float, default=300.0,
+                    help="proxy: ring bus rate it is paced to (GB/s)")
+    ap.add_argument("--proxy-blocks", type=int, default=32)
     ap.add_argument("--profile", type=int, default=0, metavar="N",
                     help="after the timed run, N extra steps with roctx ranges (load / segments"
                          " / allreduce / optimizer) and a host phase breakdown; run under "
@@ -76,12 +99,19 @@ def parse(argv=None):
                          "overhead")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
+    ap.add_argument("--secondary", default="256:bf16,256:fp8",
+                    help="after the headline: other configs as CHANNELS:DTYPE,... ('' = none)")
+    ap.add_argument("--no-report", action="store_true",
+                    help="skip the post-timing DP report (isolated collectives, no-comm step)")
     ap.add_argument("--spinup-steps", type=int, default=300,
                     help="untimed steps BEFORE the W warmup steps (a fixed count: every rank "
                          "must run the same number of collectives): "
                          "the GPU leaves its idle clock state over the first ~25 ms of load, so "
                          "without it a 20-step (20 ms) timed window measures the DVFS ramp "
                          "(20/5 steps: 0.97 ms/step, 200/50: 0.90 on the same box)")
+    ap.add_argument("--phase-timeout", type=float, default=300.0,
+                    help="N > 1: per-rank limit of each phase (comm set-up, capture, warmup, "
+                         "timed, report) in seconds")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/timing/JSON path on CPU over gloo (BASELINE config 1 "
                          "model); no GPU")
@@ -94,27 +124,79 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch(args, argv) -> int:
-    """Parent of an N-rank run: torch.distributed.run as a child process (never exec: the
-    parent must not replace itself, and it touches no GPU), relay rank 0's JSON line."""
+def _run_ranks(args, argv, status_dir, limit_s):
+    """One torch.distributed.run child (its own process group, so a wedged run can be ended
+    as a whole); returns (rc, json lines)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
+    env["DG_BENCH_STATUS_DIR"] = status_dir
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env,
-                         cwd=HERE)
+                         cwd=HERE, start_new_session=True)
+    t_end = time.monotonic() + limit_s
+
+    def on_alarm(*_):
+        sys.stderr.write(f"bench: the {args.gpus}-rank run exceeded {limit_s:.0f} s: "
+                         "ending its process group\n")
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+    old = signal.signal(signal.SIGALRM, on_alarm)
+    signal.alarm(max(1, int(t_end - time.monotonic())))
     lines = []
-    for line in p.stdout:
-        s = line.strip()
-        if s.startswith("{") and '"metric"' in s:
-            lines.append(s)
-        else:
-            sys.stderr.write(line)
-    rc = p.wait()
+    try:
+        for line in p.stdout:
+            s = line.strip()
+            if s.startswith("{") and '"metric"' in s:
+                lines.append(s)
+            else:
+                sys.stderr.write(line)
+        rc = p.wait()
+    finally:
+        signal.alarm(0)
+        signal.signal(signal.SIGALRM, old)
+    return rc, lines
+
+
+def _hangs(status_dir):
+    out = {}
+    for f in sorted(os.listdir(status_dir)):
+        try:
+            txt = open(os.path.join(status_dir, f)).read().strip()
+        except OSError:
+            continue
+        if txt.startswith("hang:"):
+            out[f] = txt[5:]
+    return out
+
+
+def launch(args, argv) -> int:
+    """Parent of an N-rank run: torch.distributed.run as a child process (never exec: the
+    parent must not replace itself, and it touches no GPU), relay rank 0's JSON line.
+    If a rank's phase guard reports a hang while the native communicator was in use
+    (--comm auto), re-run once with torch.distributed collectives."""
+    limit = 6 * args.phase_timeout + 120
+    status_dir = tempfile.mkdtemp(prefix="dg_bench_")
+    fallback = None
+    try:
+        rc, lines = _run_ranks(args, argv, status_dir, limit)
+        hangs = _hangs(status_dir)
+        if (rc != 0 and hangs and args.comm == "auto" and not args.cpu_dry_run):
+            fallback = f"native communicator run hung ({hangs}); re-run with --comm torch"
+            sys.stderr.write(f"bench: {fallback}\n")
+            for f in os.listdir(status_dir):
+                os.remove(os.path.join(status_dir, f))
+            rc, lines = _run_ranks(args, argv + ["--comm", "torch"], status_dir, limit)
+            hangs = _hangs(status_dir)
+    finally:
+        shutil.rmtree(status_dir, ignore_errors=True)
     if rc != 0:
-        sys.stderr.write(f"bench: {args.gpus}-rank run failed (rc={rc})\n")
+        sys.stderr.write(f"bench: {args.gpus}-rank run failed (rc={rc})"
+                         + (f"; hung phases {hangs}" if hangs else "") + "\n")
         return rc if rc > 0 else 1
     if len(lines) != 1:
         sys.stderr.write(f"bench: expected one JSON line from rank 0, got {len(lines)}\n")
@@ -123,7 +205,11 @@ def launch(args, argv) -> int:
     if rec.get("n_gpus") != args.gpus:
         sys.stderr.write(f"bench: ranks report n_gpus={rec.get('n_gpus')} != {args.gpus}\n")
         return 1
-    print(lines[0], flush=True)
+    if fallback:
+        rec["comm_fallback"] = fallback
+        print(json.dumps(rec), flush=True)
+    else:
+        print(lines[0], flush=True)
     return 0
 
 
@@ -138,12 +224,16 @@ def _gather_times(elapsed: float, dev) -> list:
     return [float(x.item()) for x in out]
 
 
+def _model_name(layers, channels):
+    return (f"{layers}-layer d={channels} CNN (5x5 first, 3x3 hidden, 3x3 head, "
+            "untied biases)")
+
+
 def _record(args, world, elapsed_all, flops_per_board, extra) -> dict:
     elapsed = max(elapsed_all)
     B = args.batch
     value = B * world * args.steps / elapsed
     ms = 1000.0 * elapsed / args.steps
-    model = f"{args.layers}-layer d={args.channels} CNN (5x5 first, 3x3 hidden, 3x3 head, untied biases)"
     rec = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -158,14 +248,36 @@ def _record(args, world, elapsed_all, flops_per_board, extra) -> dict:
         "dtype": args.dtype,
         "data": "synthetic (random 19x19 uint8 feature planes, GPU-expanded to 37 planes; "
                 "random-init weights)",
-        "config": {"model": model, "global_batch": B * world, "seq_len": 361,
-                   "parallelism": f"dp{world}"},
+        "config": {"model": _model_name(args.layers, args.channels), "global_batch": B * world,
+                   "seq_len": 361, "parallelism": f"dp{world}"},
         "achieved_tflops": round(flops_per_board * B * world * args.steps / elapsed / 1e12, 2),
         "rank_ms_per_step_min": round(1000.0 * min(elapsed_all) / args.steps, 4),
         "rank_ms_per_step_max": round(1000.0 * elapsed / args.steps, 4),
     }
     rec.update(extra)
     return rec
+
+
+class _NoGuard:
+    def phase(self, *_):
+        pass
+
+    def stop(self):
+        pass
+
+
+def _guard(rank, world, args):
+    if world <= 1:
+        return _NoGuard()
+    from deep_go_amd.utils.faults import PhaseGuard
+    return PhaseGuard(rank, os.environ.get("DG_BENCH_STATUS_DIR"))
+
+
+def _test_hang(rank, phase):
+    """Test hook (tests/test_bench_launcher.py): DG_BENCH_HANG=RANK:PHASE sleeps there."""
+    spec = os.environ.get("DG_BENCH_HANG", "")
+    if spec and spec == f"{rank}:{phase}":
+        time.sleep(3600)
 
 
 def run_cpu_dry(args) -> int:
@@ -183,22 +295,28 @@ def run_cpu_dry(args) -> int:
         raise SystemExit(f"rank {info.rank}: injected failure")
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
+    guard = _guard(info.rank, world, args)
     torch.set_num_threads(1)
     cfg = get_preset("cpu-1layer-k16", batchSize=args.batch * world, seed=1234)
     be = CPUBackend(cfg, args.batch, world=world)
     if world > 1:
         dp.broadcast_(be.params.data, 0)
     pool = [random_planes(args.batch, seed=1000 + 97 * info.rank + j) for j in range(4)]
+    guard.phase("warmup", args.phase_timeout)
+    _test_hang(info.rank, "warmup")
     for i in range(args.warmup):
         be.set_batch(*pool[i % 4])
         be.train_step()
     dp.barrier()
+    guard.phase("timed", args.phase_timeout)
+    _test_hang(info.rank, "timed")
     t0 = time.perf_counter()
     for i in range(args.steps):
         be.set_batch(*pool[i % 4])
         be.train_step()
     dp.barrier()
     elapsed_all = _gather_times(time.perf_counter() - t0, "cpu")
+    guard.stop()
     if info.rank == 0:
         args.layers, args.channels = cfg.numLayers, cfg.channelSize
         rec = _record(args, world, elapsed_all, cfg.train_flops_per_board(),
@@ -210,12 +328,157 @@ def run_cpu_dry(args) -> int:
     return 0
 
 
+class _Case:
+    """One configuration's network, input pool, optional DP bucketer and step graph."""
+
+    def __init__(self, args, channels, dtype, world, info, dev, comm, use_dp):
+        import torch
+        from deep_go_amd.config import get_preset
+        from deep_go_amd.data.synthetic import random_planes
+        from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep, pack_batch
+        from deep_go_amd.parallel import dp
+        self.args, self.channels, self.dtype = args, channels, dtype
+        B = args.batch
+        self.cfg = get_preset("12x128-bf16", numLayers=args.layers, channelSize=channels,
+                              batchSize=B * world, seed=1234, dtype=dtype)
+        n_hidden = args.layers - 2
+        wg = None
+        if use_dp:
+            wg = args.wgrad_group or max(1, (n_hidden + 1) // 2)
+        self.net = net = HipGoNet(self.cfg, B, device=dev, global_batch=B * world,
+                                  wgrad_group=wg)
+        # input prefetch (the next batch's copy on a load stream beside the previous step):
+        # on for the pinned host pool (SDMA copies, +1.1%), off for the device pool (its
+        # blit-kernel copy beside the step measured -1%; profiles/r2_input_prefetch_ab.txt)
+        pf = os.environ.get("DG_PREFETCH", "auto")
+        self.prefetch = (pf == "1" or (pf != "0" and args.host_pool)) and net.enable_prefetch()
+        if world > 1:
+            comm.broadcast_(net.params, 0)
+            net.refresh_weights()
+        # synthetic data pool (different per rank), packed [planes | player | rank | labels]
+        # batches: one copy per step
+        planes, player, rank, labels = random_planes(B * args.pool, seed=1000 + info.rank)
+        pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
+                                       rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
+                            for j in range(args.pool)])
+        self.pool = pool.pin_memory() if args.host_pool else pool.to(dev)
+        self.bucketer = None
+        if use_dp:
+            lay = net.layout
+            ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
+            buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20), groups=net.wgroups)
+            self.bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=args.grad_dtype,
+                                            comm=comm)
+        self.load(0)
+        self.step = SegmentedStep(net, self.bucketer, use_graphs=not args.no_graph)
+
+    def load(self, i):
+        self.net.set_batch_packed(self.pool[i % self.args.pool])
+
+    def run(self, n):
+        for i in range(n):
+            self.load(i)
+            self.step()
+
+    def timed(self, n, dev):
+        import torch
+        from deep_go_amd.parallel import dp
+        dp.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        self.run(n)
+        dp.barrier()
+        torch.cuda.synchronize()
+        return _gather_times(time.perf_counter() - t0, dev)
+
+    def params_identical(self, world) -> bool:
+        """Every rank must hold bit-identical parameters after the run (same init, same
+        all-reduced gradients): a silent collective bug fails the bench."""
+        import torch
+        if world == 1:
+            return True
+        p = self.net.params.double()
+        sig = torch.stack([p.sum(), (p ** 2).sum()])
+        sigs = [torch.zeros_like(sig) for _ in range(world)]
+        torch.distributed.all_gather(sigs, sig)
+        return all(torch.equal(x, sigs[0]) for x in sigs)
+
+
+def _dp_report(case, comm, world, dev, args, step_ms) -> dict:
+    """Post-timing DP evidence: the step's bucket collectives alone, and the same network's
+    step without collectives (so exposed comm = step - step without comm)."""
+    import torch
+    from deep_go_amd.models.hip_model import SegmentedStep
+    from deep_go_amd.parallel import dp
+    bk = case.bucketer
+    esize = 2 if args.grad_dtype == "bf16" else 4
+    nbytes = sum(e - s for s, e, _ in bk.buckets) * esize
+    rep = {"comm": comm.kind, "buckets": len(bk.buckets),
+           "bucket_mb": [round((e - s) * esize / 2 ** 20, 3) for s, e, _ in bk.buckets],
+           "wgrad_groups": [len(g) for g in case.net.wgroups],
+           "allreduce_bytes_per_step": nbytes, "grad_dtype": args.grad_dtype}
+    if comm.kind == "native":
+        rep["rccl_version"] = comm.version()
+    else:
+        try:
+            rep["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
+        except Exception:  # noqa: BLE001
+            pass
+    if comm.kind == "proxy":
+        rep["proxy"] = {"world": comm.proxy_world, "gbps": comm.gbps, "blocks": comm.blocks}
+    devs = {"rank": dp.env_info().rank, "device": dev.index,
+            "pci_bus_id": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None)}
+    if world > 1:
+        allv = [None] * world
+        torch.distributed.all_gather_object(allv, devs)
+        rep["devices"] = allv
+    else:
+        rep["devices"] = [devs]
+    # (a) the bucket collectives alone, back to back on the comm stream (same count on every
+    # rank): us per step and the ring bus bandwidth 2(n-1)/n * bytes / time
+    reps = 20
+    n = max(world, comm.proxy_world if comm.kind == "proxy" else world)
+    for _ in range(3):
+        for b in range(len(bk.buckets)):
+            bk.fire(b)
+        bk.wait()
+    dp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for b in range(len(bk.buckets)):
+            bk.fire(b)
+        bk.wait()
+    torch.cuda.synchronize()
+    t_iso = _gather_times(time.perf_counter() - t0, dev)
+    us = 1e6 * max(t_iso) / reps
+    rep["comm_isolated_us_per_step"] = round(us, 2)
+    if n > 1:
+        rep["bus_gbps"] = round(2.0 * (n - 1) / n * nbytes / (us * 1e-6) / 1e9, 1)
+    # (b) the same network's step without collectives (one graph), timed like the headline
+    plain = SegmentedStep(case.net, None, use_graphs=not args.no_graph)
+    for i in range(max(20, args.warmup)):
+        case.load(i)
+        plain()
+    dp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        case.load(i)
+        plain()
+    torch.cuda.synchronize()
+    t_plain = _gather_times(time.perf_counter() - t0, dev)
+    ms_plain = 1000.0 * max(t_plain) / args.steps
+    exposed = max(0.0, (step_ms - ms_plain) * 1000.0)
+    rep["step_nocomm_ms"] = round(ms_plain, 4)
+    rep["comm_exposed_us_per_step"] = round(exposed, 2)
+    rep["overlap_frac"] = round(max(0.0, min(1.0, 1.0 - exposed / us)), 3) if us > 0 else None
+    return rep
+
+
 def run_gpu(args) -> int:
     import torch
     sys.path.insert(0, HERE)
-    from deep_go_amd.config import get_preset
-    from deep_go_amd.data.synthetic import random_planes
-    from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep, pack_batch
     from deep_go_amd.parallel import dp
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -226,67 +489,32 @@ def run_gpu(args) -> int:
     world = info.world
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
+    guard = _guard(info.rank, world, args)
     dev = torch.device("cuda", info.local_rank if world > 1 else 0)
     torch.cuda.set_device(dev)
     use_dp = world > 1 or args.force_dp
     comm = None
+    guard.phase("comm", args.phase_timeout)
+    _test_hang(info.rank, "comm")
     if use_dp and world == 1 and args.comm == "torch" and not torch.distributed.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
         torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     if use_dp:
-        comm = dp.make_communicator(args.comm, dev)
+        comm = dp.make_communicator(args.comm, dev, world=args.proxy_world,
+                                    gbps=args.proxy_gbps, blocks=args.proxy_blocks)
         if comm.world != world:
             raise SystemExit(f"communicator world {comm.world} != {world}")
 
-    cfg = get_preset("12x128-bf16", numLayers=args.layers, channelSize=args.channels,
-                     batchSize=args.batch * world, seed=1234, dtype=args.dtype)
-    B = args.batch
-    net = HipGoNet(cfg, B, device=dev, global_batch=B * world)
-    # input prefetch (the next batch's copy on a load stream beside the previous step): on for
-    # the pinned host pool (SDMA copies, +1.1%), off for the device pool (its blit-kernel copy
-    # beside the step measured -1%; profiles/r2_input_prefetch_ab.txt); DG_PREFETCH=0/1 forces
-    pf = os.environ.get("DG_PREFETCH", "auto")
-    prefetch = (pf == "1" or (pf != "0" and args.host_pool)) and net.enable_prefetch()
-    if world > 1:
-        comm.broadcast_(net.params, 0)
-        net.refresh_weights()
-
-    # synthetic data pool on device (different per rank)
-    planes, player, rank, labels = random_planes(B * args.pool, seed=1000 + info.rank)
-    # packed [planes | player | rank | labels] batches: one device copy per step
-    pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
-                                   rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
-                        for j in range(args.pool)])
-    pool = pool.pin_memory() if args.host_pool else pool.to(dev)
-
-    def load(i):
-        net.set_batch_packed(pool[i % args.pool])
-
-    bucketer = None
-    if use_dp:
-        lay = net.layout
-        ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
-        buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20), groups=net.wgroups)
-        bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=args.grad_dtype, comm=comm)
-    load(0)
-    step = SegmentedStep(net, bucketer, use_graphs=not args.no_graph)
-
-    for i in range(args.spinup_steps):    # untimed: clock ramp (see --help)
-        load(i)
-        step()
-    for i in range(args.warmup):
-        load(i)
-        step()
-    dp.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        load(i)
-        step()
-    dp.barrier()
-    torch.cuda.synchronize()
-    elapsed_all = _gather_times(time.perf_counter() - t0, dev)
+    guard.phase("capture", args.phase_timeout)
+    case = _Case(args, args.channels, args.dtype, world, info, dev, comm, use_dp)
+    guard.phase("warmup", args.phase_timeout)
+    case.run(args.spinup_steps)     # untimed: clock ramp (see --help)
+    case.run(args.warmup)
+    guard.phase("timed", args.phase_timeout)
+    _test_hang(info.rank, "timed")
+    elapsed_all = case.timed(args.steps, dev)
+    guard.phase("report", args.phase_timeout)
     phases = None
     if args.profile > 0:
         from deep_go_amd.utils import trace
@@ -295,35 +523,62 @@ def run_gpu(args) -> int:
         for i in range(args.profile):
             with trace.range("step"):
                 with trace.range("load"):
-                    load(i)
-                step()
+                    case.load(i)
+                case.step()
         torch.cuda.synchronize()
         phases = {k: round(1e3 * v / args.profile, 4) for k, v in trace.totals(True).items()}
         trace.enable(False)
-    loss = net.mean_loss().item()  # sanity: finite
-    consistent = None
-    if world > 1:
-        # every rank must hold bit-identical parameters after the run (same init, same
-        # all-reduced gradients): a silent collective bug fails the bench here
-        sig = torch.stack([net.params.double().sum(), (net.params.double() ** 2).sum()])
-        sigs = [torch.zeros_like(sig) for _ in range(world)]
-        torch.distributed.all_gather(sigs, sig)
-        consistent = all(torch.equal(x, sigs[0]) for x in sigs)
-        if not consistent:
-            raise SystemExit(f"rank {info.rank}: parameters diverged across ranks: "
-                             f"{[x.tolist() for x in sigs]}")
+    loss = case.net.mean_loss().item()  # sanity: finite
+    consistent = case.params_identical(world)
+    if not consistent:
+        raise SystemExit(f"rank {info.rank}: parameters diverged across ranks")
+    extra = {"last_loss": round(loss, 4), "graphs": not args.no_graph,
+             "step_mode": case.step.mode, "spinup_steps": args.spinup_steps,
+             "input_prefetch": bool(case.prefetch)}
+    step_ms = 1000.0 * max(elapsed_all) / args.steps
+    if use_dp:
+        extra["comm"] = comm.kind
+        extra["ranks_params_identical"] = consistent
+        extra["grad_dtype"] = args.grad_dtype
+        if not args.no_report:
+            extra["dp"] = _dp_report(case, comm, world, dev, args, step_ms)
+    if phases:
+        extra["profile_host_ms_per_step"] = phases
+    headline = _record(args, world, elapsed_all, case.cfg.train_flops_per_board(), extra)
+    del case
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+    # secondary configurations (never inside the headline's timed region)
+    sec = {}
+    for item in [x for x in args.secondary.split(",") if x]:
+        ch, dt = item.split(":")
+        if int(ch) == args.channels and dt == args.dtype:
+            continue
+        c2 = _Case(args, int(ch), dt, world, info, dev, comm, use_dp)
+        c2.run(100)
+        c2.run(args.warmup)
+        t = c2.timed(args.steps, dev)
+        ok = c2.params_identical(world)
+        if not ok:
+            raise SystemExit(f"rank {info.rank}: parameters diverged across ranks ({item})")
+        el = max(t)
+        sec[f"12x{ch}-{dt}" if args.layers == 12 else f"{args.layers}x{ch}-{dt}"] = {
+            "value": round(args.batch * world * args.steps / el, 1), "unit": "boards/s",
+            "ms_per_step": round(1000.0 * el / args.steps, 4), "steps": args.steps,
+            "warmup": args.warmup, "spinup_steps": 100, "dtype": dt,
+            "model": _model_name(args.layers, int(ch)), "global_batch": args.batch * world,
+            "parallelism": f"dp{world}", "step_mode": c2.step.mode,
+            "achieved_tflops": round(c2.cfg.train_flops_per_board() * args.batch * world
+                                     * args.steps / el / 1e12, 2)}
+        del c2
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    if sec:
+        headline["secondary"] = sec
+    guard.stop()
     if info.rank == 0:
-        extra = {"last_loss": round(loss, 4), "graphs": not args.no_graph,
-                 "step_mode": step.mode, "spinup_steps": args.spinup_steps,
-                 "input_prefetch": bool(prefetch)}
-        if use_dp:
-            extra["comm"] = comm.kind
-            extra["ranks_params_identical"] = consistent
-            extra["grad_dtype"] = args.grad_dtype
-        if phases:
-            extra["profile_host_ms_per_step"] = phases
-        print(json.dumps(_record(args, world, elapsed_all, cfg.train_flops_per_board(), extra)),
-              flush=True)
+        print(json.dumps(headline), flush=True)
     if comm is not None:
         comm.close()
     if torch.distributed.is_initialized():

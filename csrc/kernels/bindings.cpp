@@ -14,6 +14,8 @@
 namespace py = pybind11;
 
 extern "C" {
+hipError_t dg_comm_proxy(void* buf, long long nbytes, int world, double gbps, int blocks,
+                         hipStream_t s);
 hipError_t dg_conv_nt_ex(int epi, int kw, int bm, int bn, const void* A, int KP, int M,
                          int Mpad, const void* X, int x_pad, int x_C, int Npix, void* Y,
                          int y_pad, const float* bias, const float* posb, const void* aux,
@@ -306,6 +308,10 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_bias_grad_partial(P<void>(dZ), B, C, pad, P<float>(part), S(stream)),
           "bias_grad_partial");
   });
+  m.def("comm_proxy", [](uintptr_t buf, long long nbytes, int world, double gbps, int blocks,
+                         uintptr_t stream) {
+    check(dg_comm_proxy(P<void>(buf), nbytes, world, gbps, blocks, S(stream)), "comm_proxy");
+  });
   m.def("bias_chunks", [](int B) { return dg_bias_chunks(B); });
   m.def("bias_chunks_multi", [](int B) { return dg_bias_chunks_multi(B); });
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
@@ -346,7 +352,7 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
   m.def("conv_wgrad_set_t3", [](int on) { dg_conv_wgrad_set_t3(on); },
-        "three-slice (128 x 384) wgrad tiles on/off (default on; env DG_WGRAD_T3)");
+        "three-slice (128 x 384) wgrad tiles on/off (default on)");
   m.def("conv_wgrad_multi", [](int kw, uintptr_t table, int nl, int dz_pad, int M, int Mpad,
                                int x_pad, int x_C, int B, int KP, int splits, uintptr_t stream) {
     check(dg_conv_wgrad_multi(kw, P<long long>(table), nl, dz_pad, M, Mpad, x_pad, x_C, B, KP,

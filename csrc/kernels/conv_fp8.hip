@@ -239,24 +239,30 @@ __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w,
                                          unsigned* gamax) {
   const int l = threadIdx.x;
   if (l >= n) return;
+  // a non-finite amax (an inf / NaN reached a quantized tensor: amax is an atomicMax over
+  // float bits, so NaN bits win too) never becomes a scale — exp2f(inf) = inf would zero
+  // every later quantized input and freeze the delayed scaling of the layers below — it
+  // counts as a saturation event and the previous scale stays
   if (gscales) {
     const float mg = __uint_as_float(gamax[l]);
-    if (sat && mg > 57344.f * gscales[l]) sat[2 * n + l] += 1;
-    if (mg > 0.f) gscales[l] = exp2f(ceilf(log2f(1.25f * mg / 57344.f)));
+    const bool ok = __builtin_isfinite(mg);
+    if (sat && (!ok || mg > 57344.f * gscales[l])) sat[2 * n + l] += 1;
+    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(1.25f * mg / 57344.f)));
     gamax[l] = 0u;
   }
   const float mw = __uint_as_float(amax_w[l]);
-  if (sat) {
-    if (mw > FP8_MAX * scales[2 * l]) sat[2 * l] += 1;
-    if (__uint_as_float(amax_y[l]) > FP8_MAX * scales[2 * l + 1]) sat[2 * l + 1] += 1;
-  }
-  if (mw > 0.f) scales[2 * l] = mw * w_margin / FP8_MAX;
   const float my = __uint_as_float(amax_y[l]);
+  const bool okw = __builtin_isfinite(mw), oky = __builtin_isfinite(my);
+  if (sat) {
+    if (!okw || mw > FP8_MAX * scales[2 * l]) sat[2 * l] += 1;
+    if (!oky || my > FP8_MAX * scales[2 * l + 1]) sat[2 * l + 1] += 1;
+  }
+  if (okw && mw > 0.f) scales[2 * l] = mw * w_margin / FP8_MAX;
   // activation scales are powers of two (the smallest with 1.25 amax / s <= 448: headroom
   // for the next step's growth — without it 0.8% of layer-steps saturated in the 1000-step
   // stress test); e4m3 <-> bf16 conversions then scale exactly (conv_stack_f8's
   // v_cvt_scalef32_pk_bf16_fp8 copy-out)
-  if (my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(1.25f * my / FP8_MAX)));
+  if (oky && my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(1.25f * my / FP8_MAX)));
   amax_w[l] = 0u;
   amax_y[l] = 0u;
 }

@@ -232,12 +232,6 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
            kw * kw * x_C / 8, (F * F * x_C * 2 + 1023) / 1024 * 1024, (uint8_t*)mask,
            (const bf16_t*)pbias};
   if (!pbias && (!bias || !posb)) return hipErrorInvalidValue;
-  static bool env_done = false;
-  if (!env_done) {
-    const char* e = getenv("DG_L1_NW");
-    if (e) g_l1_nw = atoi(e) == 8 ? 8 : 4;
-    env_done = true;
-  }
   // 4-wave half-board workgroups when two fit on a CU
   const bool w4 = g_l1_nw == 4 && 2 * (a.img_bytes + 2 * A_BYTES) <= 160 * 1024;
   if (kw == 5) return w4 ? launch_l1<5, 4>(a, Mpad, stream) : launch_l1<5, 8>(a, Mpad, stream);

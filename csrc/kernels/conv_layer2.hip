@@ -449,17 +449,10 @@ hipError_t launch_layer2_multi(const MultiArgs& m, int B, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// DG_L2_BPF (B-fragment read-ahead in the K loop): 1 (default) k-half 1 read before k-half
-// 0's MFMAs (+0.5% at 12x256), 0 none.  (Also reading the next step's k-half 0 under k-half
-// 1's MFMAs, 242-252 VGPRs, measured -4.5%: profiles/r2_layer2_multi_ab.txt.)
-int layer2_bpf() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DG_L2_BPF");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v;
-}
+// BPF = 1 (the only instantiation): the K loop reads k-half 1's B fragments before k-half
+// 0's MFMAs (+0.5% at 12x256 over no read-ahead, which round 3 removed).  (Also reading the
+// next step's k-half 0 under k-half 1's MFMAs, 242-252 VGPRs, measured -4.5%:
+// profiles/r2_layer2_multi_ab.txt.)
 
 }  // namespace
 
@@ -495,13 +488,8 @@ hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, 
     if (epi == EPI_DGRAD && !a.mask) return hipErrorInvalidValue;
     if (i > 0 && a.X != m.L[i - 1].Y) return hipErrorInvalidValue;
   }
-  const int bpf = layer2_bpf();
-  if (epi == EPI_FWD)
-    return bpf ? launch_layer2_multi<EPI_FWD, 1>(m, B, stream)
-               : launch_layer2_multi<EPI_FWD, 0>(m, B, stream);
-  if (epi == EPI_DGRAD)
-    return bpf ? launch_layer2_multi<EPI_DGRAD, 1>(m, B, stream)
-               : launch_layer2_multi<EPI_DGRAD, 0>(m, B, stream);
+  if (epi == EPI_FWD) return launch_layer2_multi<EPI_FWD, 1>(m, B, stream);
+  if (epi == EPI_DGRAD) return launch_layer2_multi<EPI_DGRAD, 1>(m, B, stream);
   return hipErrorInvalidValue;
 }
 

@@ -833,10 +833,7 @@ void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
 int dg_conv_wgrad_wgs_per_cu() { return 2; }
 static int g_wgrad_t3 = -1;
 static bool wgrad_t3_enabled() {
-  if (g_wgrad_t3 < 0) {
-    const char* e = getenv("DG_WGRAD_T3");
-    g_wgrad_t3 = e ? atoi(e) : 1;
-  }
+  if (g_wgrad_t3 < 0) g_wgrad_t3 = 1;
   return g_wgrad_t3 != 0;
 }
 void dg_conv_wgrad_set_t3(int on) { g_wgrad_t3 = on; }

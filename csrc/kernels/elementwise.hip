@@ -423,6 +423,37 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// Stand-in for a ring all-reduce on ONE GPU (bench.py --force-dp --comm proxy; the real
+// collective needs peers): a small grid (RCCL drives a ring with a few channel workgroups)
+// streams 2(n-1)/n x the bucket's bytes through HBM (read + write back, values unchanged),
+// paced by s_memrealtime (100 MHz) so it lasts as long as the wire transfer would at the
+// given link rate.  Its kernel trace shows whether such a comm-stream kernel co-schedules
+// beside the step's compute launches (tools/overlap_report.py).
+__global__ void __launch_bounds__(256) comm_proxy_kernel(float4* __restrict__ buf, long long n4,
+                                                         long long moves,
+                                                         long long dur_ticks) {
+  const long long per = (moves + gridDim.x - 1) / gridDim.x;
+  const long long lo = (long long)blockIdx.x * per;
+  const long long hi = lo + per < moves ? lo + per : moves;
+  if (lo >= hi) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (long long base = lo; base < hi; base += blockDim.x) {
+    if (dur_ticks > 0) {
+      const unsigned long long due =
+          t0 + (unsigned long long)((double)(base - lo) / (double)(hi - lo) * (double)dur_ticks);
+      while (__builtin_amdgcn_s_memrealtime() < due) __builtin_amdgcn_s_sleep(4);
+    }
+    const long long i = base + threadIdx.x;
+    if (i < hi) {
+      const long long j = i % n4;
+      float4 v = buf[j];
+      asm volatile("" : "+v"(v.x));
+      buf[j] = v;
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -568,6 +599,21 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   }
   const int blocks = maxtotal < 512 ? maxtotal : 512;
   hipLaunchKernelGGL(weight_refresh_kernel, dim3(blocks, n), dim3(256), 0, s, a, lr, decay, step);
+  return hipGetLastError();
+}
+
+// nbytes of a bucket (multiple of 16), world = the ring size it stands in for, gbps = link
+// rate (GB/s; 0 = unpaced), blocks = channel workgroups
+hipError_t dg_comm_proxy(void* buf, long long nbytes, int world, double gbps, int blocks,
+                         hipStream_t s) {
+  if (!buf || nbytes < 16 || nbytes % 16 != 0 || world < 2 || blocks < 1 || blocks > 1024)
+    return hipErrorInvalidValue;
+  const long long n4 = nbytes / 16;
+  const long long moves = (long long)((double)n4 * 2.0 * (world - 1) / world);
+  const double wire = (double)nbytes * 2.0 * (world - 1) / world;
+  const long long ticks = gbps > 0 ? (long long)(wire / (gbps * 1e9) * 1e8) : 0;
+  hipLaunchKernelGGL(comm_proxy_kernel, dim3(blocks), dim3(256), 0, s, (float4*)buf, n4,
+                     moves, ticks);
   return hipGetLastError();
 }
 

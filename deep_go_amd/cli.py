@@ -55,12 +55,15 @@ def cmd_train(args):
                 e.cfg = e.cfg.replace(useCuda=False)
             iters = max(0, args.iters - e.iterations)
             print(json.dumps({"auto_resume": path, "from_iteration": e.iterations}), flush=True)
-    res = e.run(iters) if iters > 0 else {"iterations": e.iterations}
-    if e.info.is_main:
-        e.save()
-        if args.export_t7:
-            e.export_t7(args.export_t7)
-        print(json.dumps({"id": e.id, "checkpoint": e.checkpoint_path(), **res}))
+    try:
+        res = e.run(iters) if iters > 0 else {"iterations": e.iterations}
+        if e.info.is_main:
+            e.save()
+            if args.export_t7:
+                e.export_t7(args.export_t7)
+            print(json.dumps({"id": e.id, "checkpoint": e.checkpoint_path(), **res}))
+    finally:
+        e.close()
     return 0
 
 
@@ -73,10 +76,13 @@ def cmd_resume(args):
         e.id = args.id
     if args.device == "cpu":
         e.cfg = e.cfg.replace(useCuda=False)
-    res = e.run(args.iters)
-    if e.info.is_main:
-        e.save()
-        print(json.dumps({"id": e.id, "checkpoint": e.checkpoint_path(), **res}))
+    try:
+        res = e.run(args.iters)
+        if e.info.is_main:
+            e.save()
+            print(json.dumps({"id": e.id, "checkpoint": e.checkpoint_path(), **res}))
+    finally:
+        e.close()
     return 0
 
 
@@ -85,7 +91,10 @@ def cmd_eval(args):
     e = Experiment.load(args.checkpoint)
     if args.device == "cpu":
         e.cfg = e.cfg.replace(useCuda=False)
-    cost, acc = e.evaluate_split(args.split, args.n)
+    try:
+        cost, acc = e.evaluate_split(args.split, args.n)
+    finally:
+        e.close()
     print(json.dumps({"split": args.split, "cost": cost, "accuracy": acc}))
     return 0
 

@@ -56,6 +56,11 @@ class ExperimentConfig:
     rmsprop_decay: float = 0.9
     bucket_mb: float = 6.0         # DP gradient bucket size (12x128: head + hidden layers | layer 0)
     grad_dtype: str = "fp32"       # all-reduce dtype: fp32 | bf16
+    # DP gradient collectives in the trainer: torch (torch.distributed between graph
+    # segments) | auto (native in-graph RCCL when every rank's self-test passes, else torch)
+    # | native.  bench.py uses auto; the trainer stays on torch by default until a
+    # multi-GPU hardware run has confirmed the in-graph mode (README, DP section)
+    comm: str = "torch"
     reference_validation_quirks: bool = False  # train.lua:23-44 floor/off-by-one
     sampling: str = "game"         # game (reference, data.lua:29-37) | position
     loader_threads: int = 8

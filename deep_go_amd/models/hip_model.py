@@ -68,12 +68,16 @@ class HipGoNet:
 
     def __init__(self, cfg: ExperimentConfig, batch: int, device="cuda",
                  flat_params: Optional[torch.Tensor] = None, num_cus: Optional[int] = None,
-                 global_batch: Optional[int] = None):
+                 global_batch: Optional[int] = None, wgrad_group: Optional[int] = None):
         if cfg.numLayers < 2:
             raise ValueError("HIP executor needs >= 2 layers (conv stack + head)")
         self.cfg = cfg
         self.B = batch
         self.global_batch = global_batch or batch
+        # layers per grouped weight-gradient launch (None: DG_WGRAD_GROUP, default all);
+        # data parallelism splits the hidden layers into groups so the top group's
+        # all-reduce runs beside the next group's launch (bench.py --wgrad-group)
+        self._wgrad_group = wgrad_group
         self.device = torch.device(device)
         self.h = hip()
         self.layout = ParamLayout(cfg)
@@ -270,9 +274,9 @@ class HipGoNet:
         self._head_red_defer = False
         self._head_red_pending = False
         self._refresh_table = self._build_refresh_table()
+        self.launches = 0     # native launches issued through _run (SegmentedStep counts them)
         self._build_plans()
-        self._head_red_defer = (self.side_mode == "bias" and bool(self.wgroups)
-                                and os.environ.get("DG_HEAD_RED_DEFER", "1") != "0")
+        self._head_red_defer = self.side_mode == "bias" and bool(self.wgroups)
         self.refresh_weights()
         self.grad_hooks: List[Tuple[int, Callable[[], None]]] = []  # (after bwd layer i, fn)
 
@@ -597,7 +601,6 @@ class HipGoNet:
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
-        self._l0_first_at = None   # ... runs it on the main stream first (DG_L0_FIRST)
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
         if os.environ.get("DG_DSTACK", "1") == "0":
@@ -703,9 +706,9 @@ class HipGoNet:
                 and os.environ.get("DG_STACK", "1") != "0" and self._l1_res_ok(p))
 
     def _l1_res_ok(self, p: ConvPlan) -> bool:
-        """First layer on the board-resident kernel (conv_l1.hip; DG_L1_RES=0: pixel-tiled)."""
+        """First layer on the board-resident kernel (conv_l1.hip) where its shape checks
+        pass; otherwise the pixel-tiled implicit GEMM (conv_nt_ex)."""
         return (p.index == 0 and not p.board and not p.fp8
-                and os.environ.get("DG_L1_RES", "1") != "0"
                 and bool(self.h.conv_l1_ok(p.k, self.layout.layers[0].pad, p.cinp, p.Mpad, p.KP)))
 
     @staticmethod
@@ -728,8 +731,7 @@ class HipGoNet:
         self.wgroups: List[List[int]] = []
         self.win_groups = set()
         self._l0_side_at = None
-        self._l0_first_at = None
-        G = int(os.environ.get("DG_WGRAD_GROUP", "16"))
+        G = self._wgrad_group or int(os.environ.get("DG_WGRAD_GROUP", "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
         if G < 2 or self.side_mode not in ("none", "bias"):
             return
@@ -765,16 +767,11 @@ class HipGoNet:
         grouped = set(i for g in groups for i in g)
         l0_ok = (self.side_mode == "bias" and self._dgrad_first and 0 not in grouped
                  and all(i in grouped for i in range(1, groups[-1][0] + 1)))
-        # DG_L0_FIRST=1: layer 0's gradient chain runs on the main stream BEFORE the last
-        # group's weight-gradient launch instead of on the side stream after the group's bias
-        # partials (which stretch over the whole window kernel beside it, leaving the side
-        # chain in the step's tail).  Measured slower at both widths (12x128 -2.1%, 12x256
-        # -0.4%: profiles/r2_l0_first_ab.txt), so off by default
-        first = os.environ.get("DG_L0_FIRST", "0") == "1"
-        self._l0_first_at = groups[-1][0] if l0_ok and first else None
-        self._l0_side_at = groups[-1][0] if l0_ok and not first else None
-        if (self._l0_side_at is not None and 1 in self._pre_dgrads
-                and os.environ.get("DG_L1_DGRAD_SIDE", "1") != "0"):
+        # layer 0's gradient chain runs on the side stream after the last group's bias
+        # partials (on the main stream before that group's launch measured -2.1% at 12x128,
+        # -0.4% at 12x256: profiles/r2_l0_first_ab.txt; removed in round 3)
+        self._l0_side_at = groups[-1][0] if l0_ok else None
+        if self._l0_side_at is not None and 1 in self._pre_dgrads:
             # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
             drop = set(id(op) for op in self._pre_dgrads[1])
             self._bwd_pre = [op for op in self._bwd_pre if id(op) not in drop]
@@ -841,10 +838,11 @@ class HipGoNet:
             ]
 
     # ------------------------------------------------------------------ execution
-    @staticmethod
-    def _run(ops, s):
+    def _run(self, ops, s):
         for f, a in ops:
             f(*a, s)
+            if f is not HipGoNet._noop:
+                self.launches += 1
 
     # ------------------------------------------------------------------ input prefetch
     def enable_prefetch(self) -> bool:
@@ -955,8 +953,7 @@ class HipGoNet:
         # slab reduces and the deterministic head reduce)
         self._run(self._pre, s)
         self._run(self._fwd_train, s)
-        f, a = self._head_train
-        f(*a, s)
+        self._run([self._head_train], s)
         self.head_reduce()
         self._run(self._bwd_pre, s)
         hooks = dict()
@@ -973,20 +970,18 @@ class HipGoNet:
     def head_reduce(self):
         """The head's weight / bias gradient reduce over the fused head's per-board partials.
         Nothing before the optimizer reads it.  With the side stream and grouped weight
-        gradients it is deferred (DG_HEAD_RED_DEFER=1): the first group's side-stream work
+        gradients it is deferred: the first group's side-stream work
         runs it beside the grouped wgrad launch, whose 2-per-CU grid leaves CUs free (it does
         not co-schedule beside the backward-data stack: run there the step was 1% slower)."""
         if self._head_red_defer:
             self._head_red_pending = True
             return
-        f, a = self._head_red
-        f(*a, stream_handle())
+        self._run([self._head_red], stream_handle())
 
     def _flush_head_reduce(self, stream):
         if self._head_red_pending:
             self._head_red_pending = False
-            f, a = self._head_red
-            f(*a, stream)
+            self._run([self._head_red], stream)
 
     def backward_layer(self, i: int, hooks=()):
         """Layer i's backward: bias grads + wgrad + slab reduce (final grads of layer i, then
@@ -1003,11 +998,7 @@ class HipGoNet:
         elif self.side_mode == "bias":
             side = self.side
             l0_side = self._l0_side_at == i
-            if i == self._l0_first_at:
-                self._run(self._bwd[0][:3], main.cuda_stream)   # layer 0's chain, main first
-            if i == 0 and self._l0_first_at is not None:
-                pass                                 # ran before the last group's launch
-            elif i == 0 and self._l0_side_at is not None:
+            if i == 0 and self._l0_side_at is not None:
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
@@ -1155,7 +1146,7 @@ class SegmentedStep:
 
         emit(lambda: net._run(net._pre, stream_handle()))
         emit(lambda: net._run(net._fwd_train, stream_handle()))
-        emit(lambda: net._head_train[0](*net._head_train[1], stream_handle()))
+        emit(lambda: net._run([net._head_train], stream_handle()))
         emit(net.head_reduce)
         emit(lambda: net._run(net._bwd_pre, stream_handle()))
         if net.L - 1 in fire_after:
@@ -1184,7 +1175,7 @@ class SegmentedStep:
         if not use_graphs:
             self.mode = "eager"
         elif bucketer is None:
-            self.mode = "graph" if os.environ.get("DG_ONE_GRAPH", "1") != "0" else "segments"
+            self.mode = "graph"
         else:
             self.mode = "dp-graph" if self.in_graph_comm else "dp-segments"
         self.graphs = []
@@ -1224,13 +1215,17 @@ class SegmentedStep:
     def _capture(self, warmup: int):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        net = self.net
+        self.seg_launches = [0] * len(self.segments)
         with torch.cuda.stream(s):
-            for _ in range(warmup):
+            for _ in range(max(1, warmup)):
                 if self.in_graph_comm:
                     self._fb_in_stream()       # also connects the communicator eagerly
                 else:
-                    for fns, _ in self.segments:
+                    for si, (fns, _) in enumerate(self.segments):
+                        n0 = net.launches
                         self._call_all(fns)
+                        self.seg_launches[si] = net.launches - n0
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         if self.mode == "dp-graph":
@@ -1245,10 +1240,19 @@ class SegmentedStep:
                 self.net.optimizer_step()
             self.full_graph = g
         else:
-            for fns, _ in self.segments:
+            for si, (fns, _) in enumerate(self.segments):
+                # a segment whose launches were all grouped away (e.g. the layers of a
+                # grouped weight-gradient launch issued by the group's top layer) is not
+                # captured: an empty capture is what a wrong-stream capture looks like, so
+                # none may be produced on purpose (tests treat that warning as an error)
+                if self.seg_launches[si] == 0:
+                    self.graphs.append(None)
+                    continue
                 g = torch.cuda.CUDAGraph()
+                n0 = net.launches
                 with torch.cuda.graph(g):
                     self._call_all(fns)
+                assert net.launches > n0, "segment capture recorded no launch"
                 self.graphs.append(g)
             if self.mode == "graph":
                 g = torch.cuda.CUDAGraph()
@@ -1276,7 +1280,8 @@ class SegmentedStep:
         for si, (fns, fire) in enumerate(self.segments):
             with trace.range(f"segment{si}"):
                 if self.use_graphs:
-                    self.graphs[si].replay()
+                    if self.graphs[si] is not None:
+                        self.graphs[si].replay()
                 else:
                     self._call_all(fns)
             if self.bucketer is not None:

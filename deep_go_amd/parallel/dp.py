@@ -146,26 +146,34 @@ class NativeComm:
     in_graph = True
     _seq = 0
 
-    def __init__(self, device):
-        from ..ops.native import comm as _comm_mod
-        mod = _comm_mod()
+    def __init__(self, device, mod=None, stream=None):
+        if mod is None:
+            from ..ops.native import comm as _comm_mod
+            mod = _comm_mod()
+        self.mod = mod
         device = torch.device(device)
         self.device = device
         if dist.is_initialized():
             self.world, self.rank = dist.get_world_size(), dist.get_rank()
         else:
             self.world, self.rank = 1, 0
+        # every rank constructs its communicators in the same order, so the n-th one of
+        # each rank meets under the same store key
+        self.key = f"dg_rccl_uid_{NativeComm._seq}"
+        NativeComm._seq += 1
         if self.world > 1:
             store = dist.distributed_c10d._get_default_store()
-            key = f"dg_rccl_uid_{NativeComm._seq}"
             if self.rank == 0:
-                store.set(key, mod.unique_id().hex())
-            uid = bytes.fromhex(store.get(key).decode())
+                store.set(self.key, mod.unique_id().hex())
+            uid = bytes.fromhex(store.get(self.key).decode())
         else:
             uid = mod.unique_id()
-        NativeComm._seq += 1
+        self.uid = uid
         self.c = mod.Comm(uid, self.world, self.rank, device.index or 0)
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=device)
+
+    def version(self) -> int:
+        return int(self.mod.version())
 
     @staticmethod
     def _dt(t: torch.Tensor) -> str:
@@ -202,21 +210,28 @@ class NativeComm:
 
 class ProxyComm:
     """World-1 stand-in for an in-graph collective (``bench.py --force-dp --comm proxy``):
-    ``all_reduce_`` launches a bandwidth-bound elementwise kernel (read + write the bucket,
-    x *= 1) on the comm stream, where the RCCL all-reduce kernel would run.  Its kernel trace
-    shows whether comm-stream kernels co-schedule with the step's full-machine compute kernels
+    ``all_reduce_`` launches an RCCL-shaped kernel on the comm stream, where the ring
+    all-reduce would run: ``blocks`` channel workgroups stream 2(n-1)/n x the bucket's bytes
+    (values unchanged), paced to the wire time at ``gbps`` (csrc/kernels/elementwise.hip
+    comm_proxy_kernel).  The step time with it vs without prices the comm kernels'
+    co-scheduling beside the compute launches; its kernel trace shows the overlap
     (tools/overlap_report.py).  Not a collective: world must be 1."""
     kind = "proxy"
     in_graph = True
 
-    def __init__(self, device):
+    def __init__(self, device, world: int = 8, gbps: float = 300.0, blocks: int = 32):
+        from ..ops.native import hip
+        self.h = hip()
         self.device = torch.device(device)
         self.world, self.rank = 1, 0
+        self.proxy_world, self.gbps, self.blocks = world, gbps, blocks
         self.stream = torch.cuda.Stream(device=self.device)
 
     def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
-        with torch.cuda.stream(stream if stream is not None else self.stream):
-            t.mul_(1.0)
+        s = stream if stream is not None else self.stream
+        nbytes = t.numel() * t.element_size() // 16 * 16
+        self.h.comm_proxy(t.data_ptr(), nbytes, self.proxy_world, self.gbps, self.blocks,
+                          int(s.cuda_stream))
         return t
 
     def broadcast_(self, t: torch.Tensor, root: int = 0):
@@ -229,42 +244,93 @@ class ProxyComm:
         pass
 
 
-def make_communicator(kind: str, device):
-    """``native`` | ``torch`` | ``auto``.  ``auto`` takes the native in-graph communicator and
-    falls back to torch.distributed if the native module is missing or its self-test (a
-    graph-captured all-reduce whose result is checked) fails — the fallback is reported by
-    ``comm.kind`` (bench JSON "comm")."""
+def agree(ok: bool, device=None) -> bool:
+    """True iff ``ok`` holds on EVERY rank (MIN all-reduce over the default process group;
+    world 1 / no process group: ``ok`` itself).  Used so that a per-rank decision (native
+    communicator or fallback) is taken by all ranks together: a rank that silently chose
+    differently would issue collectives its peers never pair with."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(ok)
+    dev = device if (dist.get_backend() == "nccl" and device is not None) else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def make_communicator(kind: str, device, selftest: Optional[Callable] = None,
+                      load_module: Optional[Callable] = None,
+                      native_factory: Optional[Callable] = None, **proxy_kw):
+    """``native`` | ``torch`` | ``auto`` (| ``proxy``, world 1 only).
+
+    ``auto`` takes the native in-graph communicator when EVERY rank can: the choice is made
+    collectively in three phases, each closed by an ``agree`` (MIN all-reduce of an ok flag)
+    so no rank ever waits in a collective its peers skipped:
+      1. local prerequisites (the ``_dgcomm`` module loads) — agreed BEFORE any rank enters
+         the collective ``ncclCommInitRank``;
+      2. ``ncclCommInitRank`` (unique id through the c10d store) and ``selftest`` (an eager
+         and a graph-captured all-reduce, the same collective sequence on every rank, the
+         sums checked only after all of them ran);
+      3. if any rank failed 1 or 2, the ranks whose native communicator came up abort it and
+         ALL ranks return a ``TorchComm`` (reported by ``comm.kind``; bench JSON "comm").
+    ``native``: the same, but a failure on any rank raises on every rank.
+    A rank that hangs inside RCCL is not recoverable here: bench.py's per-rank hang guard
+    and the trainer's StepWatchdog bound that case.
+
+    ``selftest`` / ``load_module`` / ``native_factory(module)`` are injectable so the
+    protocol runs under a CPU gloo world with a stub module (tests/test_dist_cpu.py)."""
     if kind == "torch":
         return TorchComm()
     if kind == "proxy":
         if dist.is_initialized() and dist.get_world_size() > 1:
             raise ValueError("the proxy communicator is world-1 only")
-        return ProxyComm(device)
+        return ProxyComm(device, **proxy_kw)
+    if kind not in ("auto", "native"):
+        raise ValueError(f"unknown communicator kind {kind!r}")
+    import sys
+    selftest = selftest_in_graph if selftest is None else selftest
+    if load_module is None:
+        from ..ops.native import comm as load_module
+    factory = native_factory or (lambda mod: NativeComm(device, mod=mod))
+    err = None
+    mod = None
     try:
-        c = NativeComm(device)
-        if kind == "auto":
-            selftest_in_graph(c)
-        return c
+        mod = load_module()
     except Exception as e:  # noqa: BLE001
-        if kind == "native":
-            raise
-        import sys
-        print(f"[dp] native communicator unavailable ({e}); using torch.distributed",
-              file=sys.stderr, flush=True)
-        return TorchComm()
+        err = e
+    if agree(err is None, device):
+        c = None
+        try:
+            c = factory(mod)
+            if kind == "auto":
+                selftest(c)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if agree(err is None, device):
+            return c
+        if c is not None:
+            try:
+                c.abort()
+            except Exception:  # noqa: BLE001
+                pass
+    why = err if err is not None else "another rank failed its native communicator set-up"
+    if kind == "native":
+        raise RuntimeError(f"native communicator unavailable on some rank: {why}")
+    print(f"[dp] native communicator unavailable ({why}); every rank uses torch.distributed",
+          file=sys.stderr, flush=True)
+    return TorchComm()
 
 
 def selftest_in_graph(c: NativeComm, n: int = 4096):
     """Capture ONE all-reduce on the comm stream into a hipGraph forked from / joined to the
-    capturing stream (the step graph's structure), replay it twice, check the sums."""
+    capturing stream (the step graph's structure), replay it twice, check the sums.  Every
+    collective runs before any check raises, so all ranks issue the same sequence."""
     dev = c.device
     x = torch.empty(n, dtype=torch.float32, device=dev)
     x.fill_(float(c.rank + 1))
     c.all_reduce_(x, stream=torch.cuda.current_stream(dev))   # eager: connects the comm
     torch.cuda.synchronize(dev)
     want = float(c.world * (c.world + 1) // 2)
-    if not bool((x == want).all()):
-        raise RuntimeError("native all-reduce self-test: wrong eager sum")
+    eager_ok = bool((x == want).all())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
         cur = torch.cuda.current_stream(dev)
@@ -276,9 +342,12 @@ def selftest_in_graph(c: NativeComm, n: int = 4096):
     for _ in range(2):
         g.replay()
     torch.cuda.synchronize(dev)
-    if not bool((x == 2 * want).all()):
-        raise RuntimeError("native all-reduce self-test: wrong in-graph sum")
+    graph_ok = bool((x == 2 * want).all())
     del g
+    if not eager_ok:
+        raise RuntimeError("native all-reduce self-test: wrong eager sum")
+    if not graph_ok:
+        raise RuntimeError("native all-reduce self-test: wrong in-graph sum")
 
 
 class GradBucketer:

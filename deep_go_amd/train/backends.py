@@ -248,6 +248,12 @@ class HIPBackend:
             d["optimizer"]["ms"] = self.net.ms.detach().cpu()
         return d
 
+    def close(self):
+        if self.comm is not None:
+            torch.cuda.synchronize(self.device)
+            self.comm.close()
+            self.comm = None
+
     def load_state_dict(self, d):
         o = d["optimizer"]
         self.net.lr.fill_(float(o["rate"]))

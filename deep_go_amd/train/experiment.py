@@ -33,6 +33,10 @@ from ..utils import checkpoint as ckpt
 from ..utils.faults import StepWatchdog, check_finite, maybe_inject, parse_fault
 from ..utils.metrics import MetricsSink
 
+# step timeout (seconds) armed under the native RCCL communicator when DG_STEP_TIMEOUT is
+# unset: a hung in-graph collective of a live-but-stuck peer raises no async error
+DEFAULT_NATIVE_STEP_TIMEOUT = 600.0
+
 
 def synthetic_dataset(n: int, seed: int) -> PackedDataset:
     from ..data.synthetic import engine_positions
@@ -83,7 +87,7 @@ class Experiment:
             from .backends import HIPBackend
             self.backend = HIPBackend(cfg, self.local_batch, flat=self._restore_params,
                                       world=world, bucket_mb=cfg.bucket_mb,
-                                      grad_dtype=cfg.grad_dtype)
+                                      grad_dtype=cfg.grad_dtype, comm=cfg.comm)
         else:
             from .backends import CPUBackend
             self.backend = CPUBackend(cfg, self.local_batch, flat=self._restore_params,
@@ -157,11 +161,17 @@ class Experiment:
         loader = self._train_loader()
         fault = parse_fault()
         # step timeout (DG_STEP_TIMEOUT seconds) and, with the native RCCL communicator,
-        # ncclCommGetAsyncError polling (always on under DP)
+        # ncclCommGetAsyncError polling.  RCCL reports no async error for a peer that is
+        # alive but stuck, so under the native communicator a step timeout is always armed
+        # (default DEFAULT_NATIVE_STEP_TIMEOUT s: generous against any step, validation or
+        # checkpoint between two beats)
         comm = getattr(be, "comm", None)
         comm = comm if comm is not None and comm.kind == "native" else None
-        watchdog = (StepWatchdog(float(os.environ.get("DG_STEP_TIMEOUT", "0")), comm=comm)
-                    if os.environ.get("DG_STEP_TIMEOUT") or comm is not None else None)
+        timeout = os.environ.get("DG_STEP_TIMEOUT")
+        if timeout is None and comm is not None:
+            timeout = str(DEFAULT_NATIVE_STEP_TIMEOUT)
+        watchdog = (StepWatchdog(float(timeout or 0), comm=comm)
+                    if timeout or comm is not None else None)
         ema = self.train_costs[-1] if self.train_costs else None
         t_start = time.perf_counter()
         t_log = t_start
@@ -253,6 +263,13 @@ class Experiment:
             self.init()
         data = self.draw_validation(n or self.cfg.validationSize, split=split, seed_offset=99)
         return self.eval_batch_set(data)
+
+    def close(self):
+        """Release the backend's communicator (ncclCommDestroy after a device sync) while
+        every peer is still alive, instead of in a destructor at interpreter teardown."""
+        be = self.backend
+        if be is not None and hasattr(be, "close"):
+            be.close()
 
     # ------------------------------------------------------------------ checkpoint
     def state(self):

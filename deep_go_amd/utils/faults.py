@@ -104,3 +104,54 @@ class StepWatchdog:
 
     def stop(self):
         self._stop.set()
+
+
+class PhaseGuard:
+    """Per-rank hang guard for a run made of named phases (bench.py: ``comm`` set-up,
+    ``capture``, ``warmup``, ``timed``, ``report``).  ``phase(name, limit_s)`` arms a
+    deadline; a thread that outlives it writes ``hang:<name>`` to ``<status_dir>/rank<r>``
+    (read by the launcher), reports on stderr and ends the process with ``os._exit(42)``,
+    so a rank stuck in a collective of a dead or stuck peer exits non-zero within the bound
+    instead of holding the node until an outer timeout."""
+
+    EXIT_CODE = 42
+
+    def __init__(self, rank: int, status_dir: Optional[str] = None, poll_s: float = 0.5):
+        self.rank = rank
+        self.status_dir = status_dir
+        self.poll = poll_s
+        self.name = "start"
+        self.deadline = None
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def phase(self, name: str, limit_s: float):
+        with self._lock:
+            self.name = name
+            self.deadline = time.monotonic() + limit_s
+
+    def _write_status(self, text: str):
+        if self.status_dir:
+            try:
+                with open(os.path.join(self.status_dir, f"rank{self.rank}"), "w") as f:
+                    f.write(text)
+            except OSError:
+                pass
+
+    def _run(self):
+        import sys
+        while not self._stop.wait(self.poll):
+            with self._lock:
+                name, dl = self.name, self.deadline
+            if dl is not None and time.monotonic() > dl:
+                self._write_status(f"hang:{name}")
+                sys.stderr.write(f"[guard] rank {self.rank}: phase '{name}' exceeded its "
+                                 f"time limit: exiting {self.EXIT_CODE}\n")
+                sys.stderr.flush()
+                os._exit(self.EXIT_CODE)
+
+    def stop(self):
+        self._stop.set()
+        self._write_status("ok")

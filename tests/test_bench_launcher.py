@@ -49,3 +49,18 @@ def test_world_size_mismatch_is_an_error():
     r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "1", "--warmup", "0",
                env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1 != --gpus 2" in r.stderr
+
+
+def test_hung_rank_is_bounded_by_the_phase_guard():
+    # rank 1 sleeps inside the timed phase (DG_BENCH_HANG hook): its PhaseGuard ends it with
+    # exit 42 after --phase-timeout, it records hang:timed, and the launcher fails loudly
+    import time
+    t0 = time.monotonic()
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "2", "--warmup", "1",
+               "--phase-timeout", "5", env={"DG_BENCH_HANG": "1:timed"}, timeout=240)
+    wall = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "phase 'timed' exceeded" in r.stderr
+    assert "'rank1': 'timed'" in r.stderr   # (rank 0, waiting in the barrier, may trip too)
+    assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert wall < 150

@@ -116,3 +116,87 @@ def _exp_worker(rank, world, port, ref_data, ckdir):
 def test_experiment_runs_under_gloo_world2(tmp_path, ref_data):
     mp.spawn(_exp_worker, args=(2, _free_port(), ref_data, str(tmp_path)), nprocs=2, join=True)
     assert os.path.exists(tmp_path / "dist.model")  # rank 0 checkpoint only
+
+
+# ---------------------------------------------------------------- native communicator set-up
+class _StubDgcomm:
+    """Stands in for the ``_dgcomm`` module (csrc/comm/comm.cpp) on the CPU: unique ids are
+    random bytes, ``Comm`` records what it was built with."""
+    aborted = []
+
+    @staticmethod
+    def unique_id():
+        return os.urandom(128)
+
+    @staticmethod
+    def version():
+        return 21801
+
+    class Comm:
+        def __init__(self, uid, world, rank, device):
+            self.uid, self.world, self.rank, self.device = uid, world, rank, device
+
+        def abort(self):
+            _StubDgcomm.aborted.append(self.rank)
+
+
+def _native_worker(rank, world, port, out_path, mode):
+    import json
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deep_go_amd.parallel import dp
+
+    def load():
+        if mode == "no-module" and rank == 1:
+            raise ImportError("_dgcomm missing on this rank")
+        return _StubDgcomm
+
+    def selftest(c):
+        if mode == "bad-selftest" and rank == 1:
+            raise RuntimeError("native all-reduce self-test: wrong in-graph sum")
+
+    factory = lambda mod: dp.NativeComm("cpu", mod=mod, stream="comm-stream")  # noqa: E731
+    made = []
+
+    def counting_factory(mod):
+        made.append(1)
+        return factory(mod)
+    comms = [dp.make_communicator("auto", "cpu", selftest=selftest, load_module=load,
+                                  native_factory=counting_factory) for _ in range(2)]
+    rec = {"kinds": [c.kind for c in comms], "made": len(made),
+           "aborted": list(_StubDgcomm.aborted),
+           "uids": [c.uid.hex() if c.kind == "native" else None for c in comms],
+           "keys": [getattr(c, "key", None) for c in comms]}
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(rec, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["ok", "bad-selftest", "no-module"])
+def test_native_comm_rendezvous_and_collective_fallback(tmp_path, mode):
+    """World 2 over gloo with a stub _dgcomm: every rank's n-th communicator meets under the
+    same store key and gets rank 0's unique id; if ANY rank fails its module load or
+    self-test, EVERY rank falls back to torch.distributed (and the ranks whose native
+    communicator came up abort it) — never a split decision."""
+    import json
+    out = str(tmp_path / "rec")
+    mp.spawn(_native_worker, args=(2, _free_port(), out, mode), nprocs=2, join=True)
+    recs = [json.load(open(f"{out}.{r}")) for r in (0, 1)]
+    if mode == "ok":
+        for r in recs:
+            assert r["kinds"] == ["native", "native"]
+            assert r["keys"] == ["dg_rccl_uid_0", "dg_rccl_uid_1"]
+        assert recs[0]["uids"] == recs[1]["uids"]          # rank 0's id reached rank 1
+        assert recs[0]["uids"][0] != recs[0]["uids"][1]    # a fresh id per communicator
+    else:
+        for r in recs:
+            assert r["kinds"] == ["torch", "torch"]
+        if mode == "bad-selftest":
+            # both ranks built a native comm (init is collective); both aborted it
+            assert recs[0]["made"] == recs[1]["made"] == 2
+            assert recs[0]["aborted"] == [0, 0] and recs[1]["aborted"] == [1, 1]
+        else:
+            # agreed BEFORE the collective init: no rank entered ncclCommInitRank
+            assert recs[0]["made"] == recs[1]["made"] == 0

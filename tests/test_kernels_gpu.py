@@ -1,7 +1,8 @@
 """HIP kernel numerics vs plain PyTorch fp32 oracles (SURVEY.md §4.3 'Kernel unit tests').
 
 Inputs are rounded to bf16 first so the oracle sees exactly what the MFMA sees; the
-remaining error is fp32-accumulation order + the bf16 rounding of the output.
+remaining error is fp32-accumulation order + the bf16 rounding of the output.  The conv
+oracle itself is computed on the CPU (conv_ref).
 """
 import numpy as np
 import pytest
@@ -22,7 +23,12 @@ def rel_err(a, b):
 
 
 def conv_ref(x, w_ohwi, k):
-    return F.conv2d(x, w_ohwi.permute(0, 3, 1, 2), padding=(k - 1) // 2)
+    """The fp32 oracle runs on the CPU (a CPU F.conv2d, not a GPU library
+    conv); the result comes back to x's device.  Differentiable through the device moves,
+    so autograd gives the CPU dgrad / wgrad oracles too."""
+    y = F.conv2d(x.cpu().float(), w_ohwi.cpu().float().permute(0, 3, 1, 2),
+                 padding=(k - 1) // 2)
+    return y.to(x.device)
 
 
 @pytest.mark.parametrize("B,cin,cout,k,tiles", [
@@ -370,3 +376,34 @@ def test_weight_refresh_stack_fragments():
     assert torch.equal(ff, LY.stack_frag(wf))
     assert torch.equal(fd, LY.stack_frag(wd))
     assert torch.equal(ff, LY.stack_frag(LY.fwd_weight(w, 128, KP, Mpad)))
+
+
+def test_fp8_scale_update_ignores_non_finite_amax():
+    """Delayed fp8 scaling never adopts a non-finite amax (an inf |dz| or a NaN activation):
+    the previous scale stays and the event counts as a saturation (otherwise exp2f(inf)
+    would zero every later quantized tensor and freeze the scales of the layers below)."""
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    n = 3
+    f = lambda vals: torch.tensor(vals, dtype=torch.float32, device=DEV)  # noqa: E731
+    bits = lambda vals: f(vals).view(torch.int32).clone()                 # noqa: E731
+    scales = f([0.5, 2.0, 0.25, 4.0, 1.0, 8.0])       # [2l] = s_w, [2l + 1] = s_y
+    gscales = f([16.0, 32.0, 64.0])
+    amax_w = bits([100.0, float("inf"), 10.0])
+    amax_y = bits([float("nan"), 64.0, 5.0])
+    gamax = bits([float("inf"), 1000.0, float("nan")])
+    sat = torch.zeros(3 * n, dtype=torch.int32, device=DEV)
+    s0, g0 = scales.clone(), gscales.clone()
+    h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), amax_y.data_ptr(), 1.05,
+                        sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(), stream_handle())
+    torch.cuda.synchronize()
+    assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
+    assert scales[3].item() == s0[3].item()          # layer 1 s_w: amax_w inf -> unchanged
+    assert scales[1].item() == s0[1].item()          # layer 0 s_y: amax_y NaN -> unchanged
+    assert gscales[0].item() == g0[0].item() and gscales[2].item() == g0[2].item()
+    assert abs(scales[0].item() - 100.0 * 1.05 / 448.0) < 1e-6      # finite ones update
+    assert gscales[1].item() == 2.0 ** np.ceil(np.log2(1.25 * 1000.0 / 57344.0))
+    s = sat.tolist()
+    assert s[2 * 1] == 1 and s[2 * 0 + 1] == 1        # weights l1, activations l0
+    assert s[2 * n + 0] == 1 and s[2 * n + 2] == 1    # gradients l0 (inf), l2 (NaN)
+    assert (amax_w == 0).all() and (amax_y == 0).all() and (gamax == 0).all()

@@ -27,7 +27,7 @@ def _oracle(A, x_frame, mask, epi):
     from deep_go_amd.ops import layouts as LY
     x = LY.frame_interior(x_frame, 1).float().permute(0, 3, 1, 2)          # B C 19 19
     w = A[:C, :9 * C].float().reshape(C, 3, 3, C).permute(0, 3, 1, 2)    # r c kh kw
-    out = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)                   # B 19 19 r
+    out = F.conv2d(x.cpu(), w.cpu(), padding=1).to(DEV).permute(0, 2, 3, 1)  # CPU fp32 oracle
     if epi == "fwd":
         return out.relu()
     bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1)  # B 361 16 8
@@ -137,7 +137,8 @@ def test_fp8_stack_matches_emulated_oracle(C, nl, epi):
         s_x, s_w, s_y = s[l], ws[l], s[l + 1]
         xq = q(LY.frame_interior(xin, 1).float() / s_x).permute(0, 3, 1, 2)
         wq = W8[l].float().reshape(C, 3, 3, C).permute(0, 3, 1, 2)
-        v = (F.conv2d(xq, wq, padding=1) * (s_x * s_w)).permute(0, 2, 3, 1)
+        v = (F.conv2d(xq.cpu(), wq.cpu(), padding=1).to(DEV)            # CPU fp32 oracle
+             * (s_x * s_w)).permute(0, 2, 3, 1)
         if epi == "fwd":
             v = v.relu()
         else:
