@@ -78,9 +78,12 @@ def parse(argv=None):
                          "layers, 3 MB gives one bucket per weight-gradient group (head + top "
                          "group | bottom group | first layer)")
     ap.add_argument("--wgrad-group", type=int, default=0,
-                    help="DP: hidden layers per grouped weight-gradient launch (0 = half of "
-                         "them, so the top group's all-reduce runs beside the bottom group's "
-                         "launch; >= the layer count = one launch)")
+                    help="DP: hidden layers per grouped weight-gradient launch.  0 = auto: at "
+                         "d >= 256 half of them (the top group's all-reduce runs beside the "
+                         "bottom group's launch: 3.138 vs 3.178 ms/step with the RCCL-shaped "
+                         "proxy), at d = 128 one launch (the split doubles the split-K slab "
+                         "traffic: +6%% compute for ~5 us less exposed comm); "
+                         "profiles/r3_dp_overlap_proxy.txt")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
@@ -344,7 +347,7 @@ class _Case:
         n_hidden = args.layers - 2
         wg = None
         if use_dp:
-            wg = args.wgrad_group or max(1, (n_hidden + 1) // 2)
+            wg = args.wgrad_group or (max(1, (n_hidden + 1) // 2) if channels >= 256 else 16)
         self.net = net = HipGoNet(self.cfg, B, device=dev, global_batch=B * world,
                                   wgrad_group=wg)
         # input prefetch (the next batch's copy on a load stream beside the previous step):

@@ -1005,11 +1005,13 @@ class HipGoNet:
                 self._flush_head_reduce(side.cuda_stream)
                 self._run(ops[:1], side.cuda_stream)
                 ev = side.record_event()         # partials ready for the reduce
-                if l0_side:                      # then dZ_0 and the first layer's whole
-                    self._run(self._l0_dgrad, side.cuda_stream)   # chain, joined at layer 0
-                    self._run(self._bwd[0][:3], side.cuda_stream)  # (measured: the other
-                self._run(ops[1:2], main.cuda_stream)              # order starves the 5x5 wgrad;
-                # round 2 with the head reduce deferred: 293k vs 282k boards/s)
+                # then dZ_0 and the first layer's whole chain, joined at layer 0.  Measured
+                # (profiles/r3_l0_chain_stream_ab.txt): the chain before the partials, or on a
+                # third stream beside the grouped launch, is 5-6% slower at 12x128 and
+                # 0.3-1.6% at 12x256 — compute beside the window kernel slows it
+                if l0_side:
+                    self._run(self._l0_dgrad + self._bwd[0][:3], side.cuda_stream)
+                self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:

@@ -398,7 +398,8 @@ def test_fp8_scale_update_ignores_non_finite_amax():
                         sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(), stream_handle())
     torch.cuda.synchronize()
     assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
-    assert scales[3].item() == s0[3].item()          # layer 1 s_w: amax_w inf -> unchanged
+    assert scales[2].item() == s0[2].item()          # layer 1 s_w: amax_w inf -> unchanged
+    assert scales[3].item() == 0.25                  # layer 1 s_y from amax_y 64: 2^-2
     assert scales[1].item() == s0[1].item()          # layer 0 s_y: amax_y NaN -> unchanged
     assert gscales[0].item() == g0[0].item() and gscales[2].item() == g0[2].item()
     assert abs(scales[0].item() - 100.0 * 1.05 / 448.0) < 1e-6      # finite ones update
