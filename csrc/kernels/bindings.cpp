@@ -32,13 +32,17 @@ void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
 void dg_conv_stack_f8_set_mode(int m);
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
-                            const float* s_x0, unsigned* amax_x0, int B, hipStream_t stream);
+                            const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
+                            hipStream_t stream);
+hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
+                              int KP, int splits, hipStream_t stream);
+int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
                                      float* dzb, int head_relu, float grad_scale,
-                                     hipStream_t stream);
+                                     const long long* y8, hipStream_t stream);
 hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                           hipStream_t stream);
 hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int l1, int B,
@@ -202,10 +206,27 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_stack_f8", [](int C, int epi, uintptr_t table, int nl, uintptr_t X0,
                             uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t stream) {
     check(dg_conv_stack_f8(C, epi, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
-                           P<unsigned>(amax_x0), B, S(stream)),
+                           P<unsigned>(amax_x0), B, nullptr, S(stream)),
           "conv_stack_f8");
   }, "fp8 layer stack (C = 128 | 256; epi 1 forward e4m3, 2 backward-data e5m2): table rows "
      "{A8_frag, pbias_frag, Y, mask, s_in, s_w, s_out, amax_out}; X0 quantized with *s_x0");
+  m.def("conv_stack_f8_y8", [](int C, int epi, uintptr_t table, int nl, uintptr_t X0,
+                               uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t y8,
+                               uintptr_t stream) {
+    check(dg_conv_stack_f8(C, epi, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+                           P<unsigned>(amax_x0), B, P<long long>(y8), S(stream)),
+          "conv_stack_f8_y8");
+  }, "conv_stack_f8 + fp8 copy-out: y8 = nl + 1 int64 {X8_0, Y8 of each layer} (448-row "
+     "frames; the last layer's 0)");
+  m.def("conv_wgrad_win8", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
+                              int splits, uintptr_t stream) {
+    check(dg_conv_wgrad_win8(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
+          "conv_wgrad_win8");
+  }, "MX-fp8 sliding-window weight gradients: table rows {dZ8 (e5m2), X8 (e4m3), slab, s_dz, "
+     "s_x} (448-row fp8 frames)");
+  m.def("conv_wgrad_win8_splits", [](int nl, int M, int Cx, int B, int num_cus) {
+    return dg_conv_wgrad_win8_splits(nl, M, Cx, B, num_cus);
+  });
   m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0,
                                      uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t w,
                                      uintptr_t bias, uintptr_t posb, uintptr_t labels,
@@ -216,9 +237,22 @@ PYBIND11_MODULE(_dghip, m) {
                                     P<unsigned>(amax_x0), B, P<float>(w), P<float>(bias),
                                     P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
                                     P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
-                                    grad_scale, S(stream)),
+                                    grad_scale, nullptr, S(stream)),
           "conv_stack_f8_fwd_head");
   }, "fp8 forward stack + the fused 3x3/128 policy head");
+  m.def("conv_stack_f8_fwd_head_y8", [](uintptr_t table, int nl, uintptr_t X0,
+                                     uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t w,
+                                     uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                     uintptr_t loss, uintptr_t pred, uintptr_t dZ,
+                                     uintptr_t gw_part, uintptr_t dzb, int head_relu,
+                                     float grad_scale, uintptr_t y8, uintptr_t stream) {
+    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+                                    P<unsigned>(amax_x0), B, P<float>(w), P<float>(bias),
+                                    P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
+                                    P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
+                                    grad_scale, P<long long>(y8), S(stream)),
+          "conv_stack_f8_fwd_head_y8");
+  }, "conv_stack_f8_fwd_head + fp8 copy-out (y8 as conv_stack_f8_y8)");
   m.def("conv_stack_f8_set_mode", [](int m) { dg_conv_stack_f8_set_mode(m); },
         "conv_stack_f8 timing-ablation mode (0 = production)");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },

@@ -22,6 +22,10 @@
 //     the bf16 stack;
 //   * prologue: the bf16 input frame (conv_l1's output) is quantized into the image with
 //     its scale; its amax is folded in as well.
+// fp8 copy-out (optional y8 table, the MX-fp8 weight gradient's operands, conv_wgrad_win8.hip):
+// the raw e4m3 / e5m2 image bytes — the quantized input (X8_0) and every non-last layer's
+// quantized output (Y8) — are stored beside the bf16 frames, in frames of 448 rows per board
+// (441 + 7 zero rows, never written).
 // Scales are device scalars named per layer in the launch table (s_in, s_w, s_out, amax_out):
 // HipGoNet points them into its fp8_scales / fp8_gscales arrays (delayed scaling).
 // EPI_DGRAD runs the backward-data chain the same way: e5m2 gradient image (the wider range),
@@ -68,6 +72,7 @@ constexpr float FP8_MAX = 448.f;      // e4m3
 constexpr float BF8_MAX = 57344.f;    // e5m2
 constexpr int EPI_FWD = 1;
 constexpr int EPI_DGRAD = 2;
+constexpr int FP8P = 448;             // fp8 copy-out frames: rows per board
 
 static_assert(dghead::scratch_bytes(128) + 64 <= SCRATCH, "head scratch");
 
@@ -99,11 +104,13 @@ struct F8Layer {
   const float* s_w;     // scale of its e4m3 weights
   const float* s_out;   // scale its output is quantized with (the next layer's s_in)
   unsigned* amax_out;   // |output| max folded in here (float bits; delayed scaling)
+  uint8_t* Y8;          // optional fp8 copy of the quantized output [B][448][C] (non-last)
 };
 struct F8Args {
   const char* X0;       // bf16 input frame of the first layer
   const float* s_x0;    // its quantization scale
   unsigned* amax_x0;    // its |x| max (folded in by the prologue)
+  uint8_t* X8_0;        // optional fp8 copy of the quantized input [B][448][C]
   int nl;
   int fuse_head;        // C = 128, EPI_FWD only
   F8Layer L[MAXL];
@@ -275,7 +282,10 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const int f = (h + 1) * F + (w + 1);
     return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
   };
-  auto co_store = [&](int s_, const uint4& v, const F8Layer& Lo, float s_prev) {
+  // (Y: the bf16 frame or null — layer 0's copy-out of the quantized input is fp8 only;
+  // y8: the fp8 copy or null)
+  auto co_store = [&](int s_, const uint4& v, char* Y, uint8_t* mask, uint8_t* y8,
+                      float s_prev) {
     // (opaque piece index: visible, the compiler hoists the per-step 64-bit store offsets
     // out of the layer loop and spills them — reloaded with vmcnt(0) in every layer)
     int tq = tid;
@@ -284,6 +294,8 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const int p = u / G::SLOTS, q = u % G::SLOTS;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
+    if (y8) *(uint4*)(y8 + ((size_t)(b * FP8P + f) * C + q * 16)) = v;
+    if (!Y) return;
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
     uint32_t bits = 0;
@@ -295,11 +307,11 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (EPI == EPI_FWD)
         bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
     }
-    char* yp = Lo.Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
+    char* yp = Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
     *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
     *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
     if constexpr (EPI == EPI_FWD)
-      *(uint16_t*)(Lo.mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
+      *(uint16_t*)(mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
   };
 
   i32x8 Ak[MF];
@@ -310,7 +322,12 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const F8Layer L = a.L[l];
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
-    const bool co_on = l > 0;
+    // the copy-out target of this layer's K loop: the previous layer's output (bf16 + mask
+    // + optional fp8), or at layer 0 the quantized input's fp8 copy only
+    char* coY = l > 0 ? Lprev.Y : nullptr;
+    uint8_t* coM = l > 0 ? Lprev.mask : nullptr;
+    uint8_t* coY8 = l > 0 ? Lprev.Y8 : a.X8_0;
+    const bool co_on = l > 0 || a.X8_0 != nullptr;
     const bool last = l + 1 == a.nl;
     const float s_x = *L.s_in;
     const float deq = s_x * *L.s_w;
@@ -342,7 +359,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         mma(Ak, 2, bfr, acc);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(MODE & 2)) load_A(An, 2, Ak);
-        if (co) co_store(cs, co_v, Lprev, s_x);
+        if (co) co_store(cs, co_v, coY, coM, coY8, s_x);
         __builtin_amdgcn_sched_barrier(0);
       };
       // the copy-out steps (the first CO_STEPS of pass 0) and the rest as separate loops
@@ -532,9 +549,11 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
 }
 
 // table: nl rows of 8 int64 {A8, pbias, Y, mask, s_in, s_w, s_out, amax_out}
+// y8 (optional): nl + 1 int64 {X8_0, Y8 of layer 0 .. nl - 1} (0 = none; the last layer's
+// must be 0)
 hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void* X0,
                      const float* s_x0, unsigned* amax_x0, int B, const dghead::HeadMArgs* head,
-                     hipStream_t stream) {
+                     const long long* y8, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || B <= 0 || !s_x0 || !amax_x0) return hipErrorInvalidValue;
   if ((C != 128 && C != 256) || (epi != EPI_FWD && epi != EPI_DGRAD)) return hipErrorInvalidValue;
   if (head && (C != 128 || epi != EPI_FWD)) return hipErrorInvalidValue;
@@ -542,6 +561,7 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
   a.X0 = (const char*)X0;
   a.s_x0 = s_x0;
   a.amax_x0 = amax_x0;
+  a.X8_0 = y8 ? (uint8_t*)y8[0] : nullptr;
   a.nl = nl;
   a.fuse_head = head ? 1 : 0;
   a.head = head ? *head : dghead::HeadMArgs{};
@@ -556,6 +576,8 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
     L.s_w = (const float*)t[5];
     L.s_out = (const float*)t[6];
     L.amax_out = (unsigned*)t[7];
+    L.Y8 = y8 ? (uint8_t*)y8[1 + i] : nullptr;
+    if (L.Y8 && i + 1 == nl) return hipErrorInvalidValue;
     if (!L.A8 || !L.Y || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
       return hipErrorInvalidValue;
     if (epi == EPI_FWD && !L.pbias) return hipErrorInvalidValue;
@@ -572,8 +594,9 @@ void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 // table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask, s_in, s_w,
 // s_out, amax_out} (int64); epi 1 forward, 2 backward-data
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
-                            const float* s_x0, unsigned* amax_x0, int B, hipStream_t stream) {
-  return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, stream);
+                            const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
+                            hipStream_t stream) {
+  return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, y8, stream);
 }
 
 hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
@@ -581,10 +604,10 @@ hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void*
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
                                      float* dzb, int head_relu, float grad_scale,
-                                     hipStream_t stream) {
+                                     const long long* y8, hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return f8_launch(128, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, stream);
+  return f8_launch(128, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, y8, stream);
 }
 
 }  // extern "C"

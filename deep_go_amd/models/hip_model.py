@@ -39,6 +39,9 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+FP8_PITCH = 448   # rows per board of the fp8 copy-out frames (441 + 7 zero rows)
+
+
 @dataclass
 class ConvPlan:
     index: int
@@ -212,6 +215,14 @@ class HipGoNet:
                     and os.environ.get("DG_RELU_MASK", "1") == "1"):
                 self.relu_mask[p.index] = torch.zeros((B, NUM_POINTS, p.cout // 8),
                                                       dtype=torch.uint8, device=dev)
+        # MX-fp8 weight gradients of the hidden layers (conv_wgrad_win8.hip, fp8 models;
+        # DG_FP8_WGRAD=0: bf16 window kernel): x8q[l] / dz8q[l] = the fp8 copies of layer l's
+        # input activation (e4m3) and gradient (e5m2) that the fp8 stacks write beside the
+        # bf16 frames (448 rows per board); allocated by _fuse_forward_stack /
+        # _fuse_dgrad_stack for the layers they cover
+        self.fp8_wgrad = self.fp8 and os.environ.get("DG_FP8_WGRAD", "1") != "0"
+        self.x8q: List[Optional[torch.Tensor]] = [None] * len(self.plans)
+        self.dz8q: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
         self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
@@ -415,10 +426,13 @@ class HipGoNet:
                     self._stack_table.ctypes.data, len(self.stack),
                     self.act[first - 1].data_ptr(), S + 4 * (2 * (first - 1) + 1),
                     AM + 4 * (first - 1), self.B) + fused[1][5:])
-            self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8) else (f, a)
+                if self.fp8_wgrad:
+                    fused = (h.conv_stack_f8_fwd_head_y8, fused[1] + (self._fwd_y8.ctypes.data,))
+            self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8,
+                                              h.conv_stack_f8_y8) else (f, a)
                                for f, a in self._fwd]
-            if any(f in (h.conv_stack2_fwd_head, h.conv_stack_f8_fwd_head)
-                   for f, _ in self._fwd_train):
+            if any(f in (h.conv_stack2_fwd_head, h.conv_stack_f8_fwd_head,
+                         h.conv_stack_f8_fwd_head_y8) for f, _ in self._fwd_train):
                 self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -565,13 +579,22 @@ class HipGoNet:
             members_l1 = set()
         if fp8:
             # fp8 forward stack (conv_stack_f8.hip): quantizes its bf16 input frame itself
-            # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out
+            # (amax -> fp8_amax[first - 1]), dequantized bf16 activations + ReLU bits out;
+            # with the fp8 weight gradients also the raw e4m3 input of every stack layer
+            # (x8q[l], l in the stack: the quantized input, then each non-last output)
             S, AM = self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr()
-            op = (self.h.conv_stack_f8, (self.plans[first].cout, self.h.EPI_FWD,
-                                         self._stack_table.ctypes.data, len(best),
-                                         self.act[first - 1].data_ptr(),
-                                         S + 4 * (2 * (first - 1) + 1), AM + 4 * (first - 1),
-                                         self.B))
+            args = (self.plans[first].cout, self.h.EPI_FWD, self._stack_table.ctypes.data,
+                    len(best), self.act[first - 1].data_ptr(), S + 4 * (2 * (first - 1) + 1),
+                    AM + 4 * (first - 1), self.B)
+            op = (self.h.conv_stack_f8, args)
+            if self.fp8_wgrad:
+                for i in best:
+                    self.x8q[i] = torch.zeros(self.B * FP8_PITCH * self.plans[i].cin,
+                                              dtype=torch.uint8, device=self.device)
+                y8 = [self.x8q[first].data_ptr()] + [
+                    self.x8q[i + 1].data_ptr() if i != best[-1] else 0 for i in best]
+                self._fwd_y8 = np.ascontiguousarray(np.array(y8, dtype=np.int64))
+                op = (self.h.conv_stack_f8_y8, args + (self._fwd_y8.ctypes.data,))
             self.stack_fp8 = True
         else:
             op = (self.h.conv_stack2_fwd, (self._stack_table.ctypes.data, len(rows),
@@ -638,10 +661,22 @@ class HipGoNet:
                      self.relu_mask[i - 1].data_ptr(), GS + 4 * i, S + 4 * 2 * i,
                      GS + 4 * (i - 1), GA + 4 * (i - 1)] for i in run]
             self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-            self._bwd_pre.append((self.h.conv_stack_f8, (
-                self.plans[run[0]].cout, self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
-                len(run), self.dz[run[0]].data_ptr(), GS + 4 * run[0], GA + 4 * run[0],
-                self.B)))
+            args = (self.plans[run[0]].cout, self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+                    len(run), self.dz[run[0]].data_ptr(), GS + 4 * run[0], GA + 4 * run[0],
+                    self.B)
+            if self.fp8_wgrad:
+                # the raw e5m2 gradient of every run layer for the fp8 weight gradients:
+                # dz8q[top] = the quantized input, dz8q[i - 1] = each non-last output
+                for i in run:
+                    self.dz8q[i] = torch.zeros(self.B * FP8_PITCH * self.plans[i].cout,
+                                               dtype=torch.uint8, device=self.device)
+                y8 = [self.dz8q[run[0]].data_ptr()] + [
+                    self.dz8q[i - 1].data_ptr() if i != run[-1] else 0 for i in run]
+                self._dstack_y8 = np.ascontiguousarray(np.array(y8, dtype=np.int64))
+                self._bwd_pre.append((self.h.conv_stack_f8_y8,
+                                      args + (self._dstack_y8.ctypes.data,)))
+            else:
+                self._bwd_pre.append((self.h.conv_stack_f8, args))
         else:
             rows = [[self.wdfrag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
                      self.relu_mask[i - 1].data_ptr()] for i in run]
@@ -730,6 +765,7 @@ class HipGoNet:
         profiles/r2_comm_overlap_proxy.txt), so the split only costs."""
         self.wgroups: List[List[int]] = []
         self.win_groups = set()
+        self.win8_groups = set()
         self._l0_side_at = None
         G = self._wgrad_group or int(os.environ.get("DG_WGRAD_GROUP", "16"))
         G = min(G, 16)                # MAXWL / RD_MAXL / BG_MAXL of the multi-layer kernels
@@ -785,9 +821,17 @@ class HipGoNet:
             if (win_ok and p.k == 3 and lay[g[0]].pad == 1 and self.dzp[g[0]] == 1
                     and p.cout % 64 == 0 and p.cinp % 64 == 0 and p.KPw >= 9 * p.cinp):
                 # sliding-window kernel (conv_wgrad_win.hip): one X window per K-step for
-                # all 9 taps, 43 instead of 171 B of LDS-DMA per MFMA
+                # all 9 taps, 43 instead of 171 B of LDS-DMA per MFMA; fp8 models whose
+                # stacks write the fp8 copies of every layer of the group: its MX-fp8 form
+                # (conv_wgrad_win8.hip, one 4-wave workgroup per CU)
                 self.win_groups.add(tuple(g))
-                S = h.conv_wgrad_win_splits(len(g), p.cout, p.cinp, self.B, self.num_cus)
+                if (self.fp8_wgrad and self.B % 4 == 0
+                        and all(self.x8q[i] is not None and self.dz8q[i] is not None
+                                for i in g)):
+                    self.win8_groups.add(tuple(g))
+                    S = h.conv_wgrad_win8_splits(len(g), p.cout, p.cinp, self.B, self.num_cus)
+                else:
+                    S = h.conv_wgrad_win_splits(len(g), p.cout, p.cinp, self.B, self.num_cus)
                 plan_splits[tuple(g)] = S
                 gslab_elems = max(gslab_elems, len(g) * S * p.Mpad_w * p.KPw)
                 continue
@@ -807,12 +851,18 @@ class HipGoNet:
             spec0 = lay[g[0]]
             per = S * p0.Mpad_w * p0.KPw
             wrows, brows, rrows = [], [], []
+            w8 = tuple(g) in self.win8_groups
             for j, i in enumerate(g):
                 xin = self.x0 if i == 0 else self.act[i - 1]
                 slab = self.gslab.data_ptr() + 4 * j * per
                 bpart = self.gbpart.data_ptr() + 4 * j * bpart_per
                 spec = lay[i]
-                wrows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
+                if w8:   # fp8 copies + their scales: gradient s_g[i], input s_y[i - 1]
+                    wrows.append([self.dz8q[i].data_ptr(), self.x8q[i].data_ptr(), slab,
+                                  self.fp8_gscales.data_ptr() + 4 * i,
+                                  self.fp8_scales.data_ptr() + 4 * (2 * (i - 1) + 1)])
+                else:
+                    wrows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
                 brows.append([self.dz[i].data_ptr(), bpart])
                 rrows.append([slab, G_ + spec.w_off * f4, bpart, G_ + spec.pos_off * f4,
                               G_ + spec.b_off * f4, S, p0.cout, p0.Mpad_w, p0.KPw,
@@ -828,8 +878,8 @@ class HipGoNet:
             self._bwd[g[0]][0:3] = [
                 (h.bias_grad_partial_multi, (bt.ctypes.data, len(bt), self.B, p0.cout,
                                              self.dzp[g[0]])),
-                (h.conv_wgrad_win, (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp,
-                                    self.B, p0.KPw, S))
+                (h.conv_wgrad_win8 if w8 else h.conv_wgrad_win,
+                 (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp, self.B, p0.KPw, S))
                 if tuple(g) in self.win_groups else
                 (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,

@@ -660,3 +660,55 @@ def test_input_prefetch_matches_single_buffer(layers, ch, B, graphs):
         assert runs[0][2] == runs[1][2]
     else:   # the 64-channel per-layer kernels reduce some gradients with atomics
         assert (runs[0][1] - runs[1][1]).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("ch,layers", [(256, 5), (128, 6)])
+def test_fp8_weight_gradient_teacher_forced(ch, layers):
+    """MX-fp8 window weight gradients (conv_wgrad_win8.hip) on the fp8 stacks' e4m3 / e5m2
+    copies: (1) the fp8 copy-out frames dequantize EXACTLY to the bf16 frames the stacks
+    write (same bytes x power-of-two scale); (2) each hidden layer's weight gradient equals
+    a float64 CPU oracle — torch's conv2d weight gradient over those dequantized frames —
+    to fp32 summation order (the quantization itself is the oracle's input, so the test is
+    teacher-forced: it checks the kernel, not the fp8 rounding)."""
+    from deep_go_amd.models.hip_model import FP8_PITCH
+    _, net, _ = _setup(layers, ch, 8, seed=47, dtype="fp8")
+    assert net.win8_groups, "fp8 model must use the MX-fp8 window weight gradient"
+    net.forward_backward()
+    torch.cuda.synchronize()
+    B = net.B
+    hidden = [i for g in net.win8_groups for i in g]
+    assert sorted(hidden) == list(range(1, layers - 1))
+    for i in hidden:
+        s_x = net.fp8_scales[2 * (i - 1) + 1].item()
+        s_g = net.fp8_gscales[i].item()
+        # fp8 frames [B][448][C]: rows 0..440 are the 21x21 frame
+        x8 = net.x8q[i].view(B, FP8_PITCH, ch)[:, :441].view(torch.float8_e4m3fn).float() * s_x
+        g8 = net.dz8q[i].view(B, FP8_PITCH, ch)[:, :441].view(torch.float8_e5m2).float() * s_g
+        xb = net.act[i - 1].view(B, 441, ch).float()
+        gb = net.dz[i].view(B, 441, ch).float()
+        # a stack's own input (act[0] from conv_l1, dz[top] from the head) stays unquantized
+        # bf16: its fp8 copy is its rounding (e4m3: 2^-4, e5m2: 2^-3 relative); every other
+        # bf16 frame IS the dequantized fp8 image, bit for bit
+        # (bounds: half an ulp relative, plus the subnormal step: e4m3 2^-9, e5m2 2^-16)
+        if i == 1:
+            bad = int(((x8 - xb).abs() > xb.abs() * 2 ** -4 + 2 ** -9 * s_x).sum())
+            assert bad == 0, f"layer 1: {bad} fp8 activations off their rounding"
+        else:
+            assert torch.equal(x8, xb), f"layer {i}: fp8 activation copy != bf16 frame"
+        if i == layers - 2:
+            bad = int(((g8 - gb).abs() > gb.abs() * 2 ** -3 + 2 ** -16 * s_g).sum())
+            assert bad == 0, f"layer {i}: {bad} fp8 gradients off their rounding"
+        else:
+            assert torch.equal(g8, gb), f"layer {i}: fp8 gradient copy != bf16 frame"
+        x = x8.view(B, 21, 21, ch)[:, 1:20, 1:20].permute(0, 3, 1, 2).double().cpu()
+        dz = g8.view(B, 21, 21, ch)[:, 1:20, 1:20].permute(0, 3, 1, 2).double().cpu()
+        ref = torch.nn.grad.conv2d_weight(x, (ch, ch, 3, 3), dz, padding=1)   # [co][ci][kh][kw]
+        spec = net.layout.layers[i]
+        got = net.grads[spec.w_off:spec.w_off + spec.w_numel].view(ch, 3, 3, ch)
+        got = got.permute(0, 3, 1, 2).double().cpu()
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        print(f"fp8 wgrad layer {i}: max |err| / max |ref| = {err:.2e}")
+        # the fp8 MFMA sums each 128-product block before its fp32 accumulate (not exactly
+        # the fp64 order): ~1e-4 of the largest entry, against ~0.06-0.125 per-element
+        # quantization steps the oracle already contains
+        assert err < 5e-4, (i, err)
