@@ -117,11 +117,22 @@ struct F8Args {
   dghead::HeadMArgs head;
 };
 
-// swizzle signature of frame row f: (x + 3y) & mask — distinct for any 16 raster-consecutive
-// pixels (also across a board-row wrap), so 16 lanes reading one slot of 16 pixel rows hit
-// 16 different 16-B bank groups
+// swizzle signature of frame row f (16-B slot s of the row lives at s ^ sig): a table over
+// v = (x + 3y) & 7, which steps by 1 along raster order (also across a board-row wrap, and by
+// tsig = dx + 3 dy for a tap).  A B-fragment read (ds_read_b128) serves lanes in 4 groups of
+// 16 that mix two lane groups lq (slots 8c + 2lq + h): the sig must not disturb bit 1 of the
+// slot there.  C = 256: v's bits spread to slot bits {0, 2, 3}; C = 128 (8 slots, two rows
+// per 64 banks): a searched table.  Modelled bank conflicts of the 9-tap B reads (all
+// fragments): 1728 / 1728 group-reads (C = 128) and 2256 / 3456 (C = 256) extra cycles with
+// the round-2 sig (x + 3y) & mask, 72 and 144 with these.
 template <int C>
-DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & Geo<C>::SIGM; }
+DG_DEV int sig_of(int v) {
+  constexpr uint32_t TAB = C == 128 ? 0x60147107u : 0xDC985410u;
+  return (int)((TAB >> (4 * (v & 7))) & 15u);
+}
+DG_DEV int fv(int f) { return ((f % F) + 3 * (f / F)) & 7; }
+template <int C>
+DG_DEV int fsig(int f) { return sig_of<C>(fv(f)); }
 DG_DEV int fsig8(int f) { return ((f % F) + 3 * (f / F)) & 7; }
 
 DG_DEV void lds_barrier() {
@@ -178,7 +189,10 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // EPI_DGRAD: the backward-data chain dZ_{l-1} = mask_{l-1} * (W_l^T dZ_l) (e5m2 gradients,
 // e4m3 weights: MX MFMA with A e4m3 / B e5m2), dequantized bf16 dZ frames out.
 // MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out
+// 2 = no A loads in the K loop, 4 = no copy-out.  MODE bit 8 (production, fp8 weight
+// gradients): also store the raw fp8 copies (X8_0, every non-last layer's Y8) — a compile-time
+// switch: a runtime null test around the store splits the K loop's blocks and costs 24-45
+// spilled VGPRs
 template <int C, int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   using G = Geo<C>;
@@ -217,13 +231,15 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       o.x = pack8x4<EPI>(x[0], x[1], x[2], x[3]);
       o.y = pack8x4<EPI>(x[4], x[5], x[6], x[7]);
       *(uint2*)(sI + f * ROWB + (((q >> 1) ^ fsig<C>(f)) * 16) + (q & 1) * 8) = o;
+      // the fp8 copy of the quantized input (the fp8 weight gradient's operand)
+      if constexpr ((MODE & 8) != 0) *(uint2*)(a.X8_0 + ((size_t)(b * FP8P + f) * C + q * 8)) = o;
     }
     wg_amax(m, a.amax_x0, s_amax + 8);  // (contains the barrier: image complete)
   }
 
   const int lr = lane & 15;
   const int lq = lane >> 4;
-  // per fragment: row byte offset f*ROWB (20 bits) | sig << 20
+  // per fragment: row byte offset f*ROWB (20 bits) | v = (x + 3y) & 7 << 20
   uint32_t pk[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
@@ -231,7 +247,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     if (p >= NPTS) p = 0;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    pk[j] = (uint32_t)(f * ROWB) | ((uint32_t)fsig<C>(f) << 20);
+    pk[j] = (uint32_t)(f * ROWB) | ((uint32_t)fv(f) << 20);
   }
   const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
 
@@ -256,7 +272,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int off = (int)(pk[j] & 0xFFFFFu) + toff * ROWB +
-                      (((8 * c + 2 * lq) ^ (((int)(pk[j] >> 20) + tsig) & G::SIGM)) * 16);
+                      (((8 * c + 2 * lq) ^ sig_of<C>((int)(pk[j] >> 20) + tsig)) * 16);
       const i32x4 lo = *(const LDS_AS i32x4*)(base + off);
       const i32x4 hi = *(const LDS_AS i32x4*)(base + (off ^ 16));
       bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -282,9 +298,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const int f = (h + 1) * F + (w + 1);
     return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
   };
-  // (Y: the bf16 frame or null — layer 0's copy-out of the quantized input is fp8 only;
-  // y8: the fp8 copy or null)
-  auto co_store = [&](int s_, const uint4& v, char* Y, uint8_t* mask, uint8_t* y8,
+  // (y8: the fp8 copy of the previous layer's output, or null)
+  // (yb / y8b: the bf16 / fp8 output frames advanced to this board, per layer)
+  auto co_store = [&](int s_, const uint4& v, char* yb, uint8_t* y8b, uint8_t* mask,
                       float s_prev) {
     // (opaque piece index: visible, the compiler hoists the per-step 64-bit store offsets
     // out of the layer loop and spills them — reloaded with vmcnt(0) in every layer)
@@ -294,8 +310,8 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const int p = u / G::SLOTS, q = u % G::SLOTS;
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    if (y8) *(uint4*)(y8 + ((size_t)(b * FP8P + f) * C + q * 16)) = v;
-    if (!Y) return;
+    const int inner = f * C + q * 16;                  // element offset within the board
+    if constexpr ((MODE & 8) != 0) *(uint4*)(y8b + inner) = v;
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
     uint32_t bits = 0;
@@ -307,7 +323,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (EPI == EPI_FWD)
         bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
     }
-    char* yp = Y + ((size_t)(b * FF + f) * C + q * 16) * 2;
+    char* yp = yb + inner * 2;
     *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
     *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
     if constexpr (EPI == EPI_FWD)
@@ -322,12 +338,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const F8Layer L = a.L[l];
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
-    // the copy-out target of this layer's K loop: the previous layer's output (bf16 + mask
-    // + optional fp8), or at layer 0 the quantized input's fp8 copy only
-    char* coY = l > 0 ? Lprev.Y : nullptr;
-    uint8_t* coM = l > 0 ? Lprev.mask : nullptr;
-    uint8_t* coY8 = l > 0 ? Lprev.Y8 : a.X8_0;
-    const bool co_on = l > 0 || a.X8_0 != nullptr;
+    const bool co_on = l > 0;
+    char* co_yb = Lprev.Y + (size_t)b * FF * C * 2;
+    uint8_t* co_y8b = Lprev.Y8 ? Lprev.Y8 + (size_t)b * FP8P * C : nullptr;
     const bool last = l + 1 == a.nl;
     const float s_x = *L.s_in;
     const float deq = s_x * *L.s_w;
@@ -359,7 +372,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         mma(Ak, 2, bfr, acc);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(MODE & 2)) load_A(An, 2, Ak);
-        if (co) co_store(cs, co_v, coY, coM, coY8, s_x);
+        if (co) co_store(cs, co_v, co_yb, co_y8b, Lprev.mask, s_x);
         __builtin_amdgcn_sched_barrier(0);
       };
       // the copy-out steps (the first CO_STEPS of pass 0) and the rest as separate loops
@@ -421,7 +434,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         uint32_t pkj = pk[j];
         asm volatile("" : "+v"(pkj));
         const int f = (int)(pkj & 0xFFFFFu) / ROWB;
-        const int sig = (int)(pkj >> 20);
+        const int sig = sig_of<C>((int)(pkj >> 20));
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
           f32x4 v = acc[i][j];
@@ -539,7 +552,10 @@ hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
 
 template <int C>
 hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
-  if (epi == EPI_DGRAD) return launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
+  const bool y8 = a.X8_0 != nullptr;
+  if (epi == EPI_DGRAD)
+    return y8 ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream) : launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
+  if (y8) return launch_f8<C, EPI_FWD, 8>(a, B, stream);
   switch (g_f8_mode) {
     case 2: return launch_f8<C, EPI_FWD, 2>(a, B, stream);
     case 4: return launch_f8<C, EPI_FWD, 4>(a, B, stream);
@@ -549,8 +565,7 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
 }
 
 // table: nl rows of 8 int64 {A8, pbias, Y, mask, s_in, s_w, s_out, amax_out}
-// y8 (optional): nl + 1 int64 {X8_0, Y8 of layer 0 .. nl - 1} (0 = none; the last layer's
-// must be 0)
+
 hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void* X0,
                      const float* s_x0, unsigned* amax_x0, int B, const dghead::HeadMArgs* head,
                      const long long* y8, hipStream_t stream) {
@@ -562,6 +577,7 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
   a.s_x0 = s_x0;
   a.amax_x0 = amax_x0;
   a.X8_0 = y8 ? (uint8_t*)y8[0] : nullptr;
+  if (y8 && !a.X8_0) return hipErrorInvalidValue;
   a.nl = nl;
   a.fuse_head = head ? 1 : 0;
   a.head = head ? *head : dghead::HeadMArgs{};
@@ -577,7 +593,8 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
     L.s_out = (const float*)t[6];
     L.amax_out = (unsigned*)t[7];
     L.Y8 = y8 ? (uint8_t*)y8[1 + i] : nullptr;
-    if (L.Y8 && i + 1 == nl) return hipErrorInvalidValue;
+    // (a y8 table covers every layer: all non-last copies present, the last absent)
+    if (y8 && (i + 1 == nl) != (L.Y8 == nullptr)) return hipErrorInvalidValue;
     if (!L.A8 || !L.Y || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
       return hipErrorInvalidValue;
     if (epi == EPI_FWD && !L.pbias) return hipErrorInvalidValue;

@@ -23,8 +23,6 @@
 //
 // Reference semantics: SpatialConvolutionMM accGradParameters (experiments.lua:138, EXTERNAL
 // nn) — the gradient of the 3x3 hidden convolutions of getBasicModel (experiments.lua:135-149).
-#include <stdlib.h>
-
 #include "dg_common.h"
 
 using namespace dg;
@@ -79,10 +77,8 @@ DG_DEV int step_g0(int s) {
 // NW: waves per workgroup.  8: 128-co chunks, one workgroup per CU; 4: 64-co chunks, two
 // independent workgroups per CU (their K-step barriers are not in lockstep, so one's LDS
 // reads overlap the other's MFMAs).  Every wave owns 64 co x 9 taps x 16 ci either way.
-// WPS: waves per SIMD the launch bounds allow (workgroups per CU = WPS * 4 / NW); WPS = 1
-// with NW = 4: one wave per SIMD with the whole 512-register file (DG_WIN_1W=1)
-template <int ABL, int PD, int NW, bool SWP, int WPS = 8 / NW>
-__global__ void __launch_bounds__(64 * NW, WPS) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
+template <int ABL, int PD, int NW, bool SWP>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
   static_assert(PD >= 1 && PD <= 4, "prefetch distance");
   static_assert(NW == 4 || NW == 8, "waves");
   constexpr int COCH = 16 * NW;        // co per workgroup (64 or 128)
@@ -394,23 +390,11 @@ int g_win_ablate = 0;
 int g_win_pd = 4;
 int g_win_nw = 4;
 int g_win_swp = 0;
-int g_win_1w = -1;
-bool win_1w() {
-  if (g_win_1w < 0) {
-    const char* e = getenv("DG_WIN_1W");
-    g_win_1w = e && e[0] == '1' ? 1 : 0;
-  }
-  return g_win_1w == 1 && g_win_nw == 4;
-}
 
 template <int ABL, int PD, int NW, bool SWP = false>
 void launch_win(dim3 grid, const WinArgs& a, const WinLayers& Ls, hipStream_t stream) {
-  if (NW == 4 && ABL == 0 && !SWP && win_1w())
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW, SWP, 1>), grid, dim3(64 * NW), 0,
-                       stream, a, Ls);
-  else
-    hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW, SWP>), grid, dim3(64 * NW), 0,
-                       stream, a, Ls);
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW, SWP>), grid, dim3(64 * NW), 0, stream,
+                     a, Ls);
 }
 
 }  // namespace
@@ -426,8 +410,7 @@ void dg_conv_wgrad_win_set_swp(int on) { g_win_swp = on; }
 // CU).  At least 8 K-steps per split (the prologue loads a full window).
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
   const int pairs = nl * (M / (16 * g_win_nw)) * (Cx / 64);
-  const int wgs_per_cu = win_1w() ? 1 : 8 / g_win_nw;
-  int s = pairs > 0 ? num_cus * wgs_per_cu / pairs : 1;
+  int s = pairs > 0 ? num_cus * (8 / g_win_nw) / pairs : 1;
   const int smax = B * STEPS_PER_BOARD / 8;
   if (s > smax) s = smax;
   return s < 1 ? 1 : s;

@@ -276,26 +276,17 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   }
 }
 
-int g_win8_nw = -1;
-void win8_init() {
-  if (g_win8_nw < 0) {
-    const char* e = getenv("DG_WIN8_NW");
-    g_win8_nw = e && e[0] == '4' ? 4 : 8;
-  }
-}
-
 }  // namespace
 
 extern "C" {
 
-// Splits per (layer, chunk pair): one 4-wave workgroup per CU, so the launch runs in
+// Splits per (layer, chunk pair): one 8-wave workgroup per CU, so the launch runs in
 // rounds of num_cus workgroups.  Cost model in super-step times (~0.55 us): rounds x
 // super-steps per workgroup, plus each workgroup's 147 KB fp32 slab written and reduced
 // (~0.11 of a super-step of the whole machine).  d = 256 (160 pairs): 3 splits = 2 rounds
 // (256 + 224) of 278 super-steps; d = 128 (40 pairs): 6 splits = 1 round of 139 (1 split
 // would leave 96 CUs idle; a perfect fill at 8 / 32 splits writes 2.7x / 5x the slabs).
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
-  win8_init();
   const int pairs = nl * (M / 64) * (Cx / 64);
   const int TS = B * SPB / 4;
   if (pairs <= 0 || num_cus <= 0) return 1;
@@ -316,7 +307,6 @@ int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
 // e4m3), slab, s_dz, s_x} (int64)
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, hipStream_t stream) {
-  win8_init();
   if (nl <= 0 || nl > MAXL || M % 64 != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || B % 4 != 0 || splits <= 0 || splits > B * SPB / 4)
     return hipErrorInvalidValue;
@@ -333,10 +323,9 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   }
   Win8Args a{M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / 64) * (Cx / 64) * splits);
-  if (g_win8_nw == 8)
-    hipLaunchKernelGGL(conv_wgrad_win8_kernel<8>, grid, dim3(512), 0, stream, a, Ls);
-  else
-    hipLaunchKernelGGL(conv_wgrad_win8_kernel<4>, grid, dim3(256), 0, stream, a, Ls);
+  // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
+  // the same — profiles/r3_fp8_wgrad_ab.txt)
+  hipLaunchKernelGGL(conv_wgrad_win8_kernel<8>, grid, dim3(512), 0, stream, a, Ls);
   return hipGetLastError();
 }
 
