@@ -83,7 +83,7 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
                              int y_pad, const float* bias, const float* posb, const float* s_x,
                              const float* s_w, const float* s_y, unsigned* amax_y, void* mask,
                              hipStream_t stream);
-hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y, float w_margin,
+hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w, unsigned* amax_y, float w_margin,
                                int* sat, float* gscales, unsigned* gamax, hipStream_t s);
 hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
                          const float* s_w, hipStream_t s);
@@ -279,10 +279,11 @@ PYBIND11_MODULE(_dghip, m) {
                             P<void>(mask), S(stream)),
           "conv_board_fp8");
   });
-  m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, uintptr_t amax_y,
-                                float w_margin, uintptr_t sat, uintptr_t gscales,
-                                uintptr_t gamax, uintptr_t stream) {
-    check(dg_fp8_update_scales(n, P<float>(scales), P<unsigned>(amax_w), P<unsigned>(amax_y),
+  m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, int nparts_w,
+                                uintptr_t amax_y, float w_margin, uintptr_t sat,
+                                uintptr_t gscales, uintptr_t gamax, uintptr_t stream) {
+    check(dg_fp8_update_scales(n, P<float>(scales), P<unsigned>(amax_w), nparts_w,
+                               P<unsigned>(amax_y),
                                w_margin, P<int>(sat), P<float>(gscales), P<unsigned>(gamax),
                                S(stream)),
           "fp8_update_scales");

@@ -234,11 +234,27 @@ conv_board_fp8_kernel(Fp8Args a) {
 // was in use (448 s; e5m2 57344 s): values of that tensor were clamped in the last refresh /
 // forward / backward.  gscales / gamax (optional): the e5m2 gradient scales of dz[l] (fp8
 // backward-data stack), powers of two with 1.25x headroom like the activation scales.
-__global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
-                                         float w_margin, int* sat, float* gscales,
-                                         unsigned* gamax) {
-  const int l = threadIdx.x;
-  if (l >= n) return;
+// One wave per layer l.  amax_w: nparts_w per-workgroup |w| maxima per layer (float bits,
+// written by weight_refresh with plain stores — one same-address atomic per workgroup
+// serialised at the memory side and cost the fp8 refresh ~20 us), max-reduced here.
+__global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* scales,
+                                                               unsigned* amax_w, int nparts_w,
+                                                               unsigned* amax_y, float w_margin,
+                                                               int* sat, float* gscales,
+                                                               unsigned* gamax) {
+  const int l = blockIdx.x, lane = threadIdx.x;
+  unsigned mwb = 0u;   // unsigned max of non-negative float bits: inf / NaN bits win
+  for (int j = lane; j < nparts_w; j += 64) {
+    const unsigned v = amax_w[(size_t)l * nparts_w + j];
+    mwb = v > mwb ? v : mwb;
+    amax_w[(size_t)l * nparts_w + j] = 0u;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned v = (unsigned)__shfl_xor((int)mwb, o, 64);
+    mwb = v > mwb ? v : mwb;
+  }
+  if (l >= n || lane != 0) return;
   // a non-finite amax (an inf / NaN reached a quantized tensor: amax is an atomicMax over
   // float bits, so NaN bits win too) never becomes a scale — exp2f(inf) = inf would zero
   // every later quantized input and freeze the delayed scaling of the layers below — it
@@ -250,7 +266,7 @@ __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w,
     if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(1.25f * mg / 57344.f)));
     gamax[l] = 0u;
   }
-  const float mw = __uint_as_float(amax_w[l]);
+  const float mw = __uint_as_float(mwb);
   const float my = __uint_as_float(amax_y[l]);
   const bool okw = __builtin_isfinite(mw), oky = __builtin_isfinite(my);
   if (sat) {
@@ -263,7 +279,6 @@ __global__ void fp8_update_scales_kernel(int n, float* scales, unsigned* amax_w,
   // stress test); e4m3 <-> bf16 conversions then scale exactly (conv_stack_f8's
   // v_cvt_scalef32_pk_bf16_fp8 copy-out)
   if (oky && my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(1.25f * my / FP8_MAX)));
-  amax_w[l] = 0u;
   amax_y[l] = 0u;
 }
 
@@ -363,12 +378,12 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
   }
 }
 
-hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, unsigned* amax_y,
-                               float w_margin, int* sat, float* gscales, unsigned* gamax,
-                               hipStream_t s) {
-  if (n <= 0 || n > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(1), dim3(n < 64 ? 64 : (n + 63) / 64 * 64), 0,
-                     s, n, scales, amax_w, amax_y, w_margin, sat, gscales, gamax);
+hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w,
+                               unsigned* amax_y, float w_margin, int* sat, float* gscales,
+                               unsigned* gamax, hipStream_t s) {
+  if (n <= 0 || n > 1024 || nparts_w <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(n), dim3(64), 0, s, n, scales, amax_w,
+                     nparts_w, amax_y, w_margin, sat, gscales, gamax);
   return hipGetLastError();
 }
 

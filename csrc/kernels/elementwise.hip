@@ -242,7 +242,8 @@ struct WRefreshLayer {
   bf16_t* wd;          // may be null (first layer / head)
   uint8_t* wf8;        // e4m3 forward operand (fp8 layers) or null; same [co][t*cinp+ci], kpf
   const float* s_w;    // its quantization scale (device)
-  unsigned* amax_w;    // |w| max observed here (float bits) -> next step's s_w
+  unsigned* amax_w;    // |w| max observed here (float bits) -> next step's s_w: one slot per
+                       // workgroup (blockIdx.x < REFRESH_PARTS), reduced by fp8_update_scales
   const float* bias;   // [cout]            } pbias[p][co] = bf16(bias[co] + posb[p][co]):
   const float* posb;   // [361][cout]       } the forward epilogue's single bias table
   bf16_t* pbias;       // [361][cout] or null
@@ -254,9 +255,12 @@ struct WRefreshLayer {
   uint4* wf8_frag;     // conv_stack_f8 A operands (e4m3, quantized with s_w like wf8):
                        //   [h][tap 9][c][wm 2][i 4][half 2][lane 64] x 16 B (requires wf8)
   uint4* wd8_frag;     // the same for the backward-data operand (flipped taps, transposed)
+  // (wf / wd / wf8 may be null: the per-step refresh skips the plain copies no launch of the
+  // step reads — the stacks read the fragment-ordered ones; s_w != null marks an fp8 layer)
   int cout, cin, taps, cinp, kpf, kpd;
 };
 constexpr int MAX_REFRESH = 48;
+constexpr int REFRESH_PARTS = 512;   // max workgroups per layer (= amax_w slots per layer)
 struct WRefreshArgs {
   int n;
   WRefreshLayer L[MAX_REFRESH];
@@ -284,24 +288,26 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
     const int t = tix / (nct * nit);
     const int r = tix - t * nct * nit;
     const int cot = r / nit, cit = r - cot * nit;
-    const float inv8 = L.wf8 ? 1.f / *L.s_w : 0.f;
+    const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
     for (int e = threadIdx.x; e < 64 * 64; e += 256) {
       const int rr = e >> 6, cc = e & 63;
       const int co = cot * 64 + rr, ci = cit * 64 + cc;
       float v = 0.f;
       if (co < L.cout && ci < L.cin) {
         v = L.w[((size_t)co * L.taps + t) * L.cin + ci];
-        L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = f2bf(v);
-        if (L.wf8) {
-          const float q = fmaxf(fminf(v * inv8, 448.f), -448.f);
-          L.wf8[(size_t)co * L.kpf + t * L.cinp + ci] =
-              (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xFF);
+        if (L.wf) L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = f2bf(v);
+        if (L.s_w) {   // fp8 layer: |w| max for the next scale; the plain e4m3 copy if kept
+          if (L.wf8) {
+            const float q = fmaxf(fminf(v * inv8, 448.f), -448.f);
+            L.wf8[(size_t)co * L.kpf + t * L.cinp + ci] =
+                (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xFF);
+          }
           wmax = fmaxf(wmax, fabsf(v));
         }
       }
       tileS[rr][cc] = v;
     }
-    if (L.wd || L.wf_frag || L.wf8_frag || L.wd8_frag) __syncthreads();
+    if (L.wd || L.wf_frag || L.wd_frag || L.wf8_frag || L.wd8_frag) __syncthreads();
     if (L.wd) {
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
@@ -328,7 +334,7 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
         L.wf_frag[((((size_t)(kc >> 3) * 2 + cot) * 2 + ((kc >> 2) & 1)) * 4 + (rr >> 4)) * 64 +
                   lane] = uint4{f[0], f[1], f[2], f[3]};
       }
-    } else if (L.wf_frag) {
+    } else if (L.wf_frag || L.wd_frag) {
       // this tile is exactly one 8 KB (step, co-half) chunk of each fragment layout:
       //   forward: rows co (wm = cot), k = ci of chunk cit at tap t -> step cit * 9 + t
       //   dgrad  : rows ci (wm = cit), k = co of chunk cot at flipped tap 8 - t
@@ -345,10 +351,12 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
         }
         // (C = 256: [h = co half][36 steps] — h = cot / 2 (forward) / cit / 2 (dgrad rows))
         const int nst = (L.cin / 64) * 9;
-        L.wf_frag[(((size_t)(cot >> 1) * nst + cit * 9 + t) * 2 + (cot & 1)) * 512 + u] =
-            uint4{f[0], f[1], f[2], f[3]};
-        L.wd_frag[(((size_t)(cit >> 1) * nst + cot * 9 + (8 - t)) * 2 + (cit & 1)) * 512 + u] =
-            uint4{d[0], d[1], d[2], d[3]};
+        if (L.wf_frag)
+          L.wf_frag[(((size_t)(cot >> 1) * nst + cit * 9 + t) * 2 + (cot & 1)) * 512 + u] =
+              uint4{f[0], f[1], f[2], f[3]};
+        if (L.wd_frag)
+          L.wd_frag[(((size_t)(cit >> 1) * nst + cot * 9 + (8 - t)) * 2 + (cit & 1)) * 512 + u] =
+              uint4{d[0], d[1], d[2], d[3]};
       }
     }
     if (L.wf8_frag) {
@@ -399,7 +407,14 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
     }
     __syncthreads();
   }
-  if (L.wf8 && L.amax_w) block_amax(wmax, L.amax_w, s_amax);  // uniform per block
+  if (L.s_w && L.amax_w) {   // uniform per block: this workgroup's slot (a plain store)
+    wmax = wave_max(wmax);
+    if ((threadIdx.x & 63) == 0) s_amax[threadIdx.x >> 6] = wmax;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      L.amax_w[blockIdx.x] =
+          __float_as_uint(fmaxf(fmaxf(s_amax[0], s_amax[1]), fmaxf(s_amax[2], s_amax[3])));
+  }
   if (L.pbias) {
     const int n = NPTS * L.cout;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256)
@@ -579,25 +594,25 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     if (a.L[i].pbias_frag && a.L[i].cout != 128 && a.L[i].cout != 256) return hipErrorInvalidValue;
     a.L[i].wf_frag = (uint4*)t[16];
     a.L[i].wd_frag = (uint4*)t[17];
-    if (a.L[i].wd_frag && !a.L[i].wf_frag) return hipErrorInvalidValue;
-    if (a.L[i].wf_frag && !a.L[i].wd_frag &&   // the fused-first-layer layout (l1 mode)
-        (a.L[i].taps == 9 || a.L[i].cout != 128 || a.L[i].cin > 64 || a.L[i].cinp % 8 != 0 ||
+    if (a.L[i].wf8 && !a.L[i].s_w) return hipErrorInvalidValue;
+    if (a.L[i].wf_frag && a.L[i].taps != 9 &&   // the fused-first-layer layout (l1 mode)
+        (a.L[i].wd_frag || a.L[i].cout != 128 || a.L[i].cin > 64 || a.L[i].cinp % 8 != 0 ||
          a.L[i].taps * a.L[i].cinp > 1024))
       return hipErrorInvalidValue;
     a.L[i].wf8_frag = (uint4*)t[18];
     a.L[i].wd8_frag = (uint4*)t[19];
-    if (a.L[i].wd8_frag && !a.L[i].wf8_frag) return hipErrorInvalidValue;
-    if (a.L[i].wf8_frag && (!a.L[i].wf8 || a.L[i].taps != 9 || a.L[i].cout != a.L[i].cin ||
+    if ((a.L[i].wf8_frag || a.L[i].wd8_frag) &&
+        (!a.L[i].s_w || a.L[i].taps != 9 || a.L[i].cout != a.L[i].cin ||
                             (a.L[i].cout != 128 && a.L[i].cout != 256)))
       return hipErrorInvalidValue;
-    if (a.L[i].wf_frag && a.L[i].wd_frag &&
-        (a.L[i].cout != a.L[i].cin || (a.L[i].cout != 128 && a.L[i].cout != 256) ||
-         a.L[i].taps != 9))
+    if (a.L[i].wd_frag && a.L[i].taps != 9) return hipErrorInvalidValue;
+    if ((a.L[i].wf_frag || a.L[i].wd_frag) && a.L[i].taps == 9 &&
+        (a.L[i].cout != a.L[i].cin || (a.L[i].cout != 128 && a.L[i].cout != 256)))
       return hipErrorInvalidValue;
     const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
     if (tiles > maxtotal) maxtotal = tiles;
   }
-  const int blocks = maxtotal < 512 ? maxtotal : 512;
+  const int blocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
   hipLaunchKernelGGL(weight_refresh_kernel, dim3(blocks, n), dim3(256), 0, s, a, lr, decay, step);
   return hipGetLastError();
 }

@@ -40,6 +40,7 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
 
 
 FP8_PITCH = 448   # rows per board of the fp8 copy-out frames (441 + 7 zero rows)
+REFRESH_PARTS = 512   # weight_refresh workgroups per layer (elementwise.hip)
 
 
 @dataclass
@@ -225,7 +226,10 @@ class HipGoNet:
         self.dz8q: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
         self.fp8_amax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
-        self.fp8_amax_w = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
+        # |w| max per layer: one slot per weight_refresh workgroup (REFRESH_PARTS), reduced by
+        # fp8_update_scales
+        self.fp8_amax_w = torch.zeros((len(self.plans), REFRESH_PARTS), dtype=torch.int32,
+                                      device=dev)
         # saturation events per layer ([2l] weights, [2l + 1] activations): a step whose
         # observed amax exceeded 448 x the scale in use (values were clamped)
         # ([2L + l] gradients: the e5m2 dz[l] of the fp8 backward-data stack)
@@ -285,6 +289,7 @@ class HipGoNet:
         self._head_red_defer = False
         self._head_red_pending = False
         self._refresh_table = self._build_refresh_table()
+        self._step_refresh = None   # the per-step table (plain copies no launch reads dropped)
         self.launches = 0     # native launches issued through _run (SegmentedStep counts them)
         self._build_plans()
         self._head_red_defer = self.side_mode == "bias" and bool(self.wgroups)
@@ -304,7 +309,7 @@ class HipGoNet:
                          if self.pbias_frag[p.index] is not None else 0,
                          w8.data_ptr() if w8 is not None else 0,
                          self.fp8_scales.data_ptr() + 8 * p.index if w8 is not None else 0,
-                         self.fp8_amax_w.data_ptr() + 4 * p.index if w8 is not None else 0,
+                         self.fp8_amax_w[p.index].data_ptr() if w8 is not None else 0,
                          self.params.data_ptr() + 4 * spec.b_off,
                          self.params.data_ptr() + 4 * spec.pos_off,
                          self.pbias[p.index].data_ptr() if self.pbias[p.index] is not None else 0,
@@ -1101,9 +1106,49 @@ class HipGoNet:
                        grad_scale, gate, s)
         self._fp8_update(s)
         # bf16 (+ e4m3) operand copies of the updated weights + lr *= (1 - rateDecay)
-        self.h.weight_refresh_decay(self._refresh_table.ctypes.data, len(self._refresh_table),
-                                    self.lr.data_ptr(), float(self.cfg.rateDecay),
-                                    self.step_count.data_ptr(), s)
+        t = self._step_refresh_table()
+        self.h.weight_refresh_decay(t.ctypes.data, len(t), self.lr.data_ptr(),
+                                    float(self.cfg.rateDecay), self.step_count.data_ptr(), s)
+
+    def _op_pointers(self) -> set:
+        """Every integer argument (and int64 table entry) of the launches the model issues:
+        the input / forward / head / backward op lists that forward(), forward_backward(),
+        evaluate() and backward_layer() run."""
+        vals = set()
+
+        def add(op):
+            f, a = op
+            for v in a:
+                if isinstance(v, int):
+                    vals.add(v)
+        for lst in (self._pre, self._fwd, self._fwd_train, self._bwd_pre,
+                    getattr(self, "_l0_dgrad", []), *self._bwd):
+            for op in lst:
+                add(op)
+        for op in (self._head_train, self._head_red, self._head_eval):
+            add(op)
+        for t in [getattr(self, "_stack_table", None), getattr(self, "_dstack_table", None),
+                  *getattr(self, "_l2_tables", [])]:
+            if isinstance(t, np.ndarray) and t.dtype == np.int64:
+                vals.update(int(v) for v in t.ravel())
+        return vals
+
+    def _step_refresh_table(self) -> np.ndarray:
+        """The optimizer's refresh table: the full one minus the operand copies no launch of
+        the model reads — the plain bf16 / e4m3 layouts where the board-resident stacks read
+        fragment-ordered ones, and fragment orders of paths not taken (an fp8 model's bf16
+        fragments, ...) — so the per-step refresh does not rewrite them.  Built on the first
+        optimizer step, when every launch table exists."""
+        if self._step_refresh is None:
+            used = self._op_pointers()
+            t = self._refresh_table.copy()
+            # wf, wd, wf8 (plain) and wf_frag, wd_frag, wf8_frag, wd8_frag (stack orders)
+            for col in (1, 2, 10, 16, 17, 18, 19):
+                for r in range(len(t)):
+                    if t[r, col] and int(t[r, col]) not in used:
+                        t[r, col] = 0
+            self._step_refresh = np.ascontiguousarray(t)
+        return self._step_refresh
 
     def refresh_weights(self):
         """bf16 (and fp8) operand copies of the fp32 master weights (init / load)."""
@@ -1119,7 +1164,8 @@ class HipGoNet:
         forward's activation amax; runs BEFORE the refresh that quantizes with s_w."""
         if self.fp8:
             self.h.fp8_update_scales(len(self.plans), self.fp8_scales.data_ptr(),
-                                     self.fp8_amax_w.data_ptr(), self.fp8_amax.data_ptr(), 1.05,
+                                     self.fp8_amax_w.data_ptr(), REFRESH_PARTS,
+                                     self.fp8_amax.data_ptr(), 1.05,
                                      self.fp8_sat.data_ptr(), self.fp8_gscales.data_ptr(),
                                      self.fp8_gamax.data_ptr(), s)
 

@@ -394,7 +394,7 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     gamax = bits([float("inf"), 1000.0, float("nan")])
     sat = torch.zeros(3 * n, dtype=torch.int32, device=DEV)
     s0, g0 = scales.clone(), gscales.clone()
-    h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), amax_y.data_ptr(), 1.05,
+    h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), 1, amax_y.data_ptr(), 1.05,
                         sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(), stream_handle())
     torch.cuda.synchronize()
     assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
