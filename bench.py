@@ -348,8 +348,10 @@ class _Case:
         wg = None
         if use_dp:
             wg = args.wgrad_group or (max(1, (n_hidden + 1) // 2) if channels >= 256 else 16)
+        # (--grad-dtype bf16: the gradient reduces write the bf16 wire twin themselves)
         self.net = net = HipGoNet(self.cfg, B, device=dev, global_batch=B * world,
-                                  wgrad_group=wg)
+                                  wgrad_group=wg,
+                                  grad_wire=args.grad_dtype if use_dp else "fp32")
         # input prefetch (the next batch's copy on a load stream beside the previous step):
         # on for the pinned host pool (SDMA copies, +1.1%), off for the device pool (its
         # blit-kernel copy beside the step measured -1%; profiles/r2_input_prefetch_ab.txt)
@@ -371,7 +373,7 @@ class _Case:
             ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
             buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20), groups=net.wgroups)
             self.bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=args.grad_dtype,
-                                            comm=comm)
+                                            comm=comm, shadow=net.grads16)
         self.load(0)
         self.step = SegmentedStep(net, self.bucketer, use_graphs=not args.no_graph)
 

@@ -92,14 +92,16 @@ hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* sc
 hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, const void* X,
                          int x_pad, int x_C, int B, int KP, int splits, float* slab,
                          hipStream_t stream);
-hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, hipStream_t stream);
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int cols, hipStream_t stream);
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
                                       hipStream_t s);
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
-                           float* gposb, float* gbias, hipStream_t stream);
+                           float* gposb, float* gbias, void* out16, void* gposb16,
+                           void* gbias16, hipStream_t stream);
 hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n, float* gw,
-                          float* gbias, float* gposb, hipStream_t stream);
+                          float* gbias, float* gposb, void* gw16, void* gbias16, void* gposb16,
+                          hipStream_t stream);
 void dg_head_set_mfma(int on);
 hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                    const float* bias, const float* posb, const int* labels, float* loss,
@@ -114,11 +116,12 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
 int dg_bias_chunks(int B);
 int dg_bias_chunks_multi(int B);
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
-                  const float* gate, hipStream_t s);
+                  const float* gate, const void* g16, hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
-                      float decay, float gscale, const float* gate, hipStream_t s);
+                      float decay, float gscale, const float* gate, const void* g16,
+                      hipStream_t s);
 hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t ng, float* gate,
-                          int* bad_count, hipStream_t s);
+                          int* bad_count, const void* grads16, hipStream_t s);
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s);
@@ -301,9 +304,12 @@ PYBIND11_MODULE(_dghip, m) {
           "frame_to_fp8");
   });
   m.def("wgrad_reduce_multi", [](uintptr_t table, int nl, uintptr_t stream) {
-    check(dg_wgrad_reduce_multi(P<long long>(table), nl, S(stream)), "wgrad_reduce_multi");
+    check(dg_wgrad_reduce_multi(P<long long>(table), nl, 13, S(stream)), "wgrad_reduce_multi");
   }, "slab reduce + bias pass 2 of nl layers: table rows {slab, out, bpart, gposb, gbias, "
      "splits, M, Mpad, KP, taps, cin, cinp, bchunks}");
+  m.def("wgrad_reduce_multi_w", [](uintptr_t table, int nl, uintptr_t stream) {
+    check(dg_wgrad_reduce_multi(P<long long>(table), nl, 16, S(stream)), "wgrad_reduce_multi_w");
+  }, "wgrad_reduce_multi writing bf16 twins too: rows + {out16, gposb16, gbias16}");
   m.def("bias_grad_partial_multi", [](uintptr_t table, int nl, int B, int C, int pad,
                                       uintptr_t stream) {
     check(dg_bias_grad_partial_multi(P<long long>(table), nl, B, C, pad, S(stream)),
@@ -313,15 +319,33 @@ PYBIND11_MODULE(_dghip, m) {
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
                            uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {
     check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
-                          P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias), S(stream)),
+                          P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias), nullptr,
+                          nullptr, nullptr, S(stream)),
           "wgrad_reduce");
   });
+  m.def("wgrad_reduce_w", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
+                             int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
+                             uintptr_t gposb, uintptr_t gbias, uintptr_t out16,
+                             uintptr_t gposb16, uintptr_t gbias16, uintptr_t stream) {
+    check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
+                          P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias),
+                          P<void>(out16), P<void>(gposb16), P<void>(gbias16), S(stream)),
+          "wgrad_reduce_w");
+  }, "wgrad_reduce writing bf16 twins of the weight / position-bias / bias gradients too");
   m.def("head_reduce", [](uintptr_t dzb, uintptr_t gw_part, int B, int n, uintptr_t gw,
                           uintptr_t gbias, uintptr_t gposb, uintptr_t stream) {
     check(dg_head_reduce(P<float>(dzb), P<float>(gw_part), B, n, P<float>(gw), P<float>(gbias),
-                         P<float>(gposb), S(stream)),
+                         P<float>(gposb), nullptr, nullptr, nullptr, S(stream)),
           "head_reduce");
   });
+  m.def("head_reduce_w", [](uintptr_t dzb, uintptr_t gw_part, int B, int n, uintptr_t gw,
+                            uintptr_t gbias, uintptr_t gposb, uintptr_t gw16, uintptr_t gbias16,
+                            uintptr_t gposb16, uintptr_t stream) {
+    check(dg_head_reduce(P<float>(dzb), P<float>(gw_part), B, n, P<float>(gw), P<float>(gbias),
+                         P<float>(gposb), P<void>(gw16), P<void>(gbias16), P<void>(gposb16),
+                         S(stream)),
+          "head_reduce_w");
+  }, "head_reduce writing bf16 twins too");
   m.def("head", [](int kw, uintptr_t X, int x_pad, int C, int B, uintptr_t w, uintptr_t bias,
                    uintptr_t posb, uintptr_t labels, uintptr_t loss, uintptr_t pred,
                    uintptr_t logp, uintptr_t dZ, int dz_pad, uintptr_t gw, uintptr_t gbias,
@@ -351,22 +375,41 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("bias_chunks_multi", [](int B) { return dg_bias_chunks_multi(B); });
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
                   uintptr_t gate, uintptr_t stream) {
-    check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, P<float>(gate), S(stream)),
+    check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, P<float>(gate), nullptr,
+                 S(stream)),
           "sgd");
   });
+  m.def("sgd_bf16", [](uintptr_t p, uintptr_t g16, size_t n, uintptr_t lr, float gscale,
+                       uintptr_t gate, uintptr_t stream) {
+    check(dg_sgd(P<float>(p), nullptr, n, P<double>(lr), gscale, P<float>(gate), P<void>(g16),
+                 S(stream)),
+          "sgd_bf16");
+  }, "SGD reading the bf16 (wire-format) gradient");
   m.def("rmsprop", [](uintptr_t p, uintptr_t g, uintptr_t ms, size_t n, uintptr_t lr,
                       float decay, float gscale, uintptr_t gate, uintptr_t stream) {
     check(dg_rmsprop(P<float>(p), P<float>(g), P<float>(ms), n, P<double>(lr), decay, gscale,
-                     P<float>(gate), S(stream)),
+                     P<float>(gate), nullptr, S(stream)),
           "rmsprop");
   });
+  m.def("rmsprop_bf16", [](uintptr_t p, uintptr_t g16, uintptr_t ms, size_t n, uintptr_t lr,
+                           float decay, float gscale, uintptr_t gate, uintptr_t stream) {
+    check(dg_rmsprop(P<float>(p), nullptr, P<float>(ms), n, P<double>(lr), decay, gscale,
+                     P<float>(gate), P<void>(g16), S(stream)),
+          "rmsprop_bf16");
+  }, "RMSProp reading the bf16 (wire-format) gradient");
   // loss (or 0) rank-local; grads (or 0) the flat (all-reduced) gradient: gate = all finite
   m.def("finite_gate", [](uintptr_t loss, int n, uintptr_t grads, size_t ng, uintptr_t gate,
                           uintptr_t bad, uintptr_t stream) {
     check(dg_finite_gate(P<float>(loss), n, P<float>(grads), ng, P<float>(gate), P<int>(bad),
-                         S(stream)),
+                         nullptr, S(stream)),
           "finite_gate");
   });
+  m.def("finite_gate_bf16", [](uintptr_t loss, int n, uintptr_t grads16, size_t ng,
+                               uintptr_t gate, uintptr_t bad, uintptr_t stream) {
+    check(dg_finite_gate(P<float>(loss), n, nullptr, ng, P<float>(gate), P<int>(bad),
+                         P<void>(grads16), S(stream)),
+          "finite_gate_bf16");
+  }, "finite_gate over the bf16 (wire-format) gradient");
   m.def("lr_decay", [](uintptr_t lr, double decay, uintptr_t step, uintptr_t stream) {
     check(dg_lr_decay(P<double>(lr), decay, P<long long>(step), S(stream)), "lr_decay");
   });

@@ -649,6 +649,11 @@ struct ReduceLayers {  // blockIdx.y = layer (several layers, each with its own 
   const float* bpart[RD_MAXL];
   float* gposb[RD_MAXL];
   float* gbias[RD_MAXL];
+  // optional bf16 twins of out / gposb / gbias (the data-parallel bf16 wire format: the
+  // bucket all-reduce runs on them directly, no conversion kernels; null = fp32 only)
+  bf16_t* out16[RD_MAXL];
+  bf16_t* gposb16[RD_MAXL];
+  bf16_t* gbias16[RD_MAXL];
   int splits[RD_MAXL], M[RD_MAXL], Mpad[RD_MAXL], KP[RD_MAXL], taps[RD_MAXL], cin[RD_MAXL],
       cinp[RD_MAXL], bchunks[RD_MAXL], main_blocks[RD_MAXL];
 };
@@ -674,7 +679,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
     s0 = wave_sum(s0);
     if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = s0;
     __syncthreads();
-    if (threadIdx.x == 0) gbias[c] = (s_r[0] + s_r[1]) + (s_r[2] + s_r[3]);
+    if (threadIdx.x == 0) {
+      const float v = (s_r[0] + s_r[1]) + (s_r[2] + s_r[3]);
+      gbias[c] = v;
+      if (Ls.gbias16[ly]) Ls.gbias16[ly][c] = f2bf(v);
+    }
     return;
   }
   if ((int)blockIdx.x >= main_blocks) {
@@ -691,6 +700,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
       }
       for (; z < bchunks; ++z) s0 += bpart[(size_t)z * np + j];
       gposb[j] = s0 + s1;
+      if (Ls.gposb16[ly]) Ls.gposb16[ly][j] = f2bf(s0 + s1);
     }
     return;
   }
@@ -717,7 +727,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
       const int kk = k + e;
       const int t = kk / cinp;
       const int ci = kk - t * cinp;
-      if (t < taps && ci < cin) out[((size_t)co * taps + t) * cin + ci] = s[e];
+      if (t < taps && ci < cin) {
+        const size_t o = ((size_t)co * taps + t) * cin + ci;
+        out[o] = s[e];
+        if (Ls.out16[ly]) Ls.out16[ly][o] = f2bf(s[e]);
+      }
     }
   }
 }
@@ -965,24 +979,33 @@ static int reduce_grid_x(const ReduceLayers& Ls, int i) {
 
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
-                           float* gposb, float* gbias, hipStream_t stream) {
+                           float* gposb, float* gbias, void* out16, void* gposb16, void* gbias16,
+                           hipStream_t stream) {
   ReduceLayers Ls{};
   reduce_layer(Ls, 0, slab, out, bpart, gposb, gbias, splits, M, Mpad, KP, taps, cin, cinp,
                bchunks);
+  Ls.out16[0] = (bf16_t*)out16;
+  Ls.gposb16[0] = (bf16_t*)gposb16;
+  Ls.gbias16[0] = (bf16_t*)gbias16;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(reduce_grid_x(Ls, 0), 1), dim3(256), 0, stream,
                      Ls);
   return hipGetLastError();
 }
 
 // Slab reduce + bias-gradient pass 2 of nl layers (any shapes) in one launch: table = nl
-// rows of 13 int64 {slab, out (weight grad), bpart, gposb, gbias, splits, M, Mpad, KP, taps,
-// cin, cinp, bchunks}.
-hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, hipStream_t stream) {
-  if (nl <= 0 || nl > RD_MAXL) return hipErrorInvalidValue;
+// rows of `cols` int64 {slab, out (weight grad), bpart, gposb, gbias, splits, M, Mpad, KP,
+// taps, cin, cinp, bchunks[, out16, gposb16, gbias16]} (cols 13, or 16 with bf16 twins).
+hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int cols, hipStream_t stream) {
+  if (nl <= 0 || nl > RD_MAXL || (cols != 13 && cols != 16)) return hipErrorInvalidValue;
   ReduceLayers Ls{};
   int gx = 1;
   for (int i = 0; i < nl; ++i) {
-    const long long* t = table + 13 * i;
+    const long long* t = table + cols * i;
+    if (cols == 16) {
+      Ls.out16[i] = (bf16_t*)t[13];
+      Ls.gposb16[i] = (bf16_t*)t[14];
+      Ls.gbias16[i] = (bf16_t*)t[15];
+    }
     if (!t[0] || !t[1] || !t[2] || t[5] <= 0 || t[6] <= 0 || t[8] % 4 != 0)
       return hipErrorInvalidValue;
     reduce_layer(Ls, i, (const float*)t[0], (float*)t[1], (const float*)t[2], (float*)t[3],

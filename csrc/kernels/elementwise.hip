@@ -145,9 +145,21 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
 }
 
 // ------------------------------------------------------------------------------------
+// gradient element i as fp32: the flat fp32 gradient, or its bf16 twin (the data-parallel
+// bf16 wire format: the all-reduced bucket is read as it came off the wire)
+DG_DEV float grad_at(const float* g, size_t i) { return g[i]; }
+DG_DEV float grad_at(const bf16_t* g, size_t i) { return bf2f(g[i]); }
+DG_DEV f32x4 grad4_at(const float* g, size_t i4) { return ((const f32x4*)g)[i4]; }
+DG_DEV f32x4 grad4_at(const bf16_t* g, size_t i4) {
+  const uint2 u = ((const uint2*)g)[i4];
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u),
+               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xFFFF0000u)};
+}
+
 // SGD (optimizer.lua:24-27): theta -= lr * g over the flat fp32 master buffer.  lr lives
 // on the device (double) so the step can be replayed inside a hipGraph.
-__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n,
+template <typename G>
+__global__ void sgd_kernel(float* __restrict__ p, const G* __restrict__ g, size_t n,
                            const double* __restrict__ lr, float gscale,
                            const float* __restrict__ gate) {
   // gate (optional, device): 0 skips the update (non-finite loss/gradient policy, graph-
@@ -158,25 +170,26 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, s
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
     f32x4 pv = ((f32x4*)p)[i];
-    const f32x4 gv = ((const f32x4*)g)[i];
+    const f32x4 gv = grad4_at(g, i);
     pv -= l * gv;
     ((f32x4*)p)[i] = pv;
   }
   for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x)
-    p[i] -= l * g[i];
+    p[i] -= l * grad_at(g, i);
 }
 
 // RMSProp-style update (the reference's misnamed AdagradOptimizer, optimizer.lua:1-14):
 // ms = decay*ms + (1-decay)*g^2 ; theta -= lr * g / sqrt(ms); ms initialised to 1.
-__global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
+template <typename G>
+__global__ void rmsprop_kernel(float* __restrict__ p, const G* __restrict__ g,
                                float* __restrict__ ms, size_t n, const double* __restrict__ lr,
                                float decay, float gscale, const float* __restrict__ gate) {
   if (gate && *gate == 0.f) return;
   const float l = (float)(*lr);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
-    const float gi = g[i] * gscale;
+    const float gi = grad_at(g, i) * gscale;
     const float m = decay * ms[i] + (1.f - decay) * gi * gi;
     ms[i] = m;
     p[i] -= l * gi * rsqrtf(m);
@@ -207,18 +220,19 @@ __global__ void finite_gate_kernel(const float* __restrict__ loss, int n, float*
 // Under data parallelism every rank sees the same reduced gradient, so every rank takes the
 // same decision (a rank-local loss check would let one rank's NaN reach ranks that still
 // step).  The first lane that finds a bad value flips the gate and counts the step once.
-__global__ void grad_gate_kernel(const float* __restrict__ g, size_t n, float* __restrict__ gate,
+template <typename G>
+__global__ void grad_gate_kernel(const G* __restrict__ g, size_t n, float* __restrict__ gate,
                                  int* __restrict__ bad_count) {
   const size_t n4 = n / 4;
   bool bad = false;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
-    const f32x4 v = ((const f32x4*)g)[i];
+    const f32x4 v = grad4_at(g, i);
     bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
   }
   for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x)
-    bad |= !isfinite(g[i]);
+    bad |= !isfinite(grad_at(g, i));
   if (bad) {
     const int old = atomicExch((int*)gate, 0);
     if (old != 0 && bad_count) atomicAdd(bad_count, 1);
@@ -521,38 +535,54 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
 int dg_bias_chunks_multi(int B) { return (B + BG_BT_MULTI - 1) / BG_BT_MULTI; }
 
+// g16 (optional): read the bf16 twin gradient instead of g (data-parallel bf16 wire)
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
-                  const float* gate, hipStream_t s) {
+                  const float* gate, const void* g16, hipStream_t s) {
   int blocks = (int)((n / 4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sgd_kernel, dim3(blocks), dim3(256), 0, s, p, g, n, lr, gscale, gate);
+  if (g16)
+    hipLaunchKernelGGL(sgd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, p,
+                       (const bf16_t*)g16, n, lr, gscale, gate);
+  else
+    hipLaunchKernelGGL(sgd_kernel<float>, dim3(blocks), dim3(256), 0, s, p, g, n, lr, gscale,
+                       gate);
   return hipGetLastError();
 }
 
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
-                      float decay, float gscale, const float* gate, hipStream_t s) {
+                      float decay, float gscale, const float* gate, const void* g16,
+                      hipStream_t s) {
   int blocks = (int)((n + 255) / 256);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, s, p, g, ms, n, lr, decay,
-                     gscale, gate);
+  if (g16)
+    hipLaunchKernelGGL(rmsprop_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, p,
+                       (const bf16_t*)g16, ms, n, lr, decay, gscale, gate);
+  else
+    hipLaunchKernelGGL(rmsprop_kernel<float>, dim3(blocks), dim3(256), 0, s, p, g, ms, n, lr,
+                       decay, gscale, gate);
   return hipGetLastError();
 }
 
-// loss (optional, rank-local) and grads (optional, flat, all-reduced) -> gate in {0, 1}
+// loss (optional, rank-local) and grads (optional, flat, all-reduced; or its bf16 twin
+// grads16) -> gate in {0, 1}
 hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t ng, float* gate,
-                          int* bad_count, hipStream_t s) {
+                          int* bad_count, const void* grads16, hipStream_t s) {
   if (loss) {
     hipLaunchKernelGGL(finite_gate_kernel, dim3(1), dim3(256), 0, s, loss, n, gate, bad_count);
   } else {
     hipLaunchKernelGGL(set_gate_kernel, dim3(1), dim3(64), 0, s, gate);
   }
-  if (grads && ng) {
+  if ((grads || grads16) && ng) {
     int blocks = (int)((ng / 4 + 255) / 256);
     if (blocks > 1024) blocks = 1024;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(grad_gate_kernel, dim3(blocks), dim3(256), 0, s, grads, ng, gate,
-                       bad_count);
+    if (grads16)
+      hipLaunchKernelGGL(grad_gate_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s,
+                         (const bf16_t*)grads16, ng, gate, bad_count);
+    else
+      hipLaunchKernelGGL(grad_gate_kernel<float>, dim3(blocks), dim3(256), 0, s, grads, ng,
+                         gate, bad_count);
   }
   return hipGetLastError();
 }

@@ -316,7 +316,9 @@ __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
 constexpr int HR_G = 16;
 __global__ void __launch_bounds__(1024)
 head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_part, int B, int n,
-                   float* __restrict__ gw, float* __restrict__ gbias, float* __restrict__ gposb) {
+                   float* __restrict__ gw, float* __restrict__ gbias, float* __restrict__ gposb,
+                   bf16_t* gw16, bf16_t* gbias16, bf16_t* gposb16) {
+  // (gw16 / gbias16 / gposb16: optional bf16 twins for the data-parallel bf16 wire format)
   __shared__ float s_red[HR_G][64];
   const int nout = n + NPTS;
   const int tid = threadIdx.x;
@@ -338,6 +340,7 @@ head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_p
       float t = 0.f;
       for (int w = 0; w < 16; ++w) t += s_red[0][w];
       *gbias = t;
+      if (gbias16) *gbias16 = f2bf(t);
     }
     return;
   }
@@ -366,18 +369,24 @@ head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_p
     float v = 0.f;
 #pragma unroll
     for (int g = 0; g < HR_G; ++g) v += s_red[g][tid];
-    if (is_w) gw[o] = v;
-    else gposb[o - n] = v;
+    if (is_w) {
+      gw[o] = v;
+      if (gw16) gw16[o] = f2bf(v);
+    } else {
+      gposb[o - n] = v;
+      if (gposb16) gposb16[o - n] = f2bf(v);
+    }
   }
 }
 
 }  // namespace
 
 extern "C" hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n,
-                                     float* gw, float* gbias, float* gposb, hipStream_t stream) {
+                                     float* gw, float* gbias, float* gposb, void* gw16,
+                                     void* gbias16, void* gposb16, hipStream_t stream) {
   const int blocks = (n + NPTS + 63) / 64 + 1;  // + the gbias workgroup
   hipLaunchKernelGGL(head_reduce_kernel, dim3(blocks), dim3(1024), 0, stream, dzb, gw_part, B, n,
-                     gw, gbias, gposb);
+                     gw, gbias, gposb, (bf16_t*)gw16, (bf16_t*)gbias16, (bf16_t*)gposb16);
   return hipGetLastError();
 }
 

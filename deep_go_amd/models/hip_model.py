@@ -72,7 +72,8 @@ class HipGoNet:
 
     def __init__(self, cfg: ExperimentConfig, batch: int, device="cuda",
                  flat_params: Optional[torch.Tensor] = None, num_cus: Optional[int] = None,
-                 global_batch: Optional[int] = None, wgrad_group: Optional[int] = None):
+                 global_batch: Optional[int] = None, wgrad_group: Optional[int] = None,
+                 grad_wire: str = "fp32"):
         if cfg.numLayers < 2:
             raise ValueError("HIP executor needs >= 2 layers (conv stack + head)")
         self.cfg = cfg
@@ -99,6 +100,14 @@ class HipGoNet:
             flat_params = init_params(self.layout, cfg.seed)
         self.params = flat_params.to(dev, torch.float32).contiguous()
         self.grads = torch.zeros_like(self.params)
+        # data-parallel bf16 wire format: every gradient reduce also writes a bf16 twin
+        # (grads16, same flat layout), the bucket all-reduces run on it and the optimizer
+        # reads it — no conversion kernels around the collectives
+        if grad_wire not in ("fp32", "bf16"):
+            raise ValueError(f"grad_wire {grad_wire!r}")
+        self.grad_wire = grad_wire
+        self.grads16 = (torch.zeros(self.params.numel(), dtype=torch.bfloat16, device=dev)
+                        if grad_wire == "bf16" else None)
         self.lr = torch.tensor([cfg.rate], dtype=torch.float64, device=dev)
         self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ms = None
@@ -296,6 +305,10 @@ class HipGoNet:
         self.refresh_weights()
         self.grad_hooks: List[Tuple[int, Callable[[], None]]] = []  # (after bwd layer i, fn)
 
+    def _g16(self, off: int) -> int:
+        """Address of flat gradient element off in the bf16 twin (grad_wire='bf16')."""
+        return self.grads16.data_ptr() + 2 * off
+
     # ------------------------------------------------------------------ planning
     def _build_refresh_table(self) -> np.ndarray:
         rows = []
@@ -404,6 +417,9 @@ class HipGoNet:
         self._head_red = (h.head_reduce, (self.head_dzb.data_ptr(), self.head_gw_part.data_ptr(),
                                           self.B, hd.k * hd.k * hd.cin, G + hd.w_off * f4,
                                           G + hd.b_off * f4, G + hd.pos_off * f4))
+        if self.grads16 is not None:
+            self._head_red = (h.head_reduce_w, self._head_red[1] + (
+                self._g16(hd.w_off), self._g16(hd.b_off), self._g16(hd.pos_off)))
         self._head_eval = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
                                     P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
                                     self.labels.data_ptr(), self.eval_loss.data_ptr(),
@@ -453,10 +469,15 @@ class HipGoNet:
             ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
                                        xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
                                        p.splits, slab)))
-            ops.append((h.wgrad_reduce, (slab, G + spec.w_off * f4, p.splits,
-                                         p.cout, p.Mpad_w, p.KPw, p.k * p.k, p.cin, p.cinp,
-                                         bpart, self.bchunks,
-                                         G + spec.pos_off * f4, G + spec.b_off * f4)))
+            red = (slab, G + spec.w_off * f4, p.splits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
+                   p.cin, p.cinp, bpart, self.bchunks, G + spec.pos_off * f4,
+                   G + spec.b_off * f4)
+            if self.grads16 is not None:
+                ops.append((h.wgrad_reduce_w, red + (self._g16(spec.w_off),
+                                                     self._g16(spec.pos_off),
+                                                     self._g16(spec.b_off))))
+            else:
+                ops.append((h.wgrad_reduce, red))
             if i > 0:
                 prev = lay.layers[i - 1]
                 if (p.board_d and self.wdfrag[i] is not None and p.cout == 256
@@ -871,7 +892,9 @@ class HipGoNet:
                 brows.append([self.dz[i].data_ptr(), bpart])
                 rrows.append([slab, G_ + spec.w_off * f4, bpart, G_ + spec.pos_off * f4,
                               G_ + spec.b_off * f4, S, p0.cout, p0.Mpad_w, p0.KPw,
-                              p0.k * p0.k, p0.cin, p0.cinp, self.bchunks_g])
+                              p0.k * p0.k, p0.cin, p0.cinp, self.bchunks_g]
+                             + ([self._g16(spec.w_off), self._g16(spec.pos_off),
+                                 self._g16(spec.b_off)] if self.grads16 is not None else []))
                 self.plans[i].splits = S
                 # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
                 # launches all three passes for the whole group
@@ -889,7 +912,8 @@ class HipGoNet:
                 (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
                                       S)),
-                (h.wgrad_reduce_multi, (rt.ctypes.data, len(rt))),
+                (h.wgrad_reduce_multi_w if self.grads16 is not None else h.wgrad_reduce_multi,
+                 (rt.ctypes.data, len(rt))),
             ]
 
     # ------------------------------------------------------------------ execution
@@ -1089,21 +1113,24 @@ class HipGoNet:
         s = stream_handle()
         n = self.layout.numel
         gate = 0
+        # (bf16 wire: the optimizer reads the all-reduced bf16 twin)
+        w16 = self.grads16 is not None
+        g = self.grads16.data_ptr() if w16 else self.grads.data_ptr()
         if self.cfg.nan_policy == "skip":
             # gate = finite(gradients) [and finite(local loss) on one rank]: under DP every
             # rank sees the same all-reduced gradient, so all ranks skip together
             dp = self.global_batch != self.B
-            self.h.finite_gate(0 if dp else self.loss.data_ptr(), self.B,
-                               self.grads.data_ptr(), n, self.gate.data_ptr(),
-                               self.bad_steps.data_ptr(), s)
+            (self.h.finite_gate_bf16 if w16 else self.h.finite_gate)(
+                0 if dp else self.loss.data_ptr(), self.B, g, n, self.gate.data_ptr(),
+                self.bad_steps.data_ptr(), s)
             gate = self.gate.data_ptr()
         if self.ms is not None:
-            self.h.rmsprop(self.params.data_ptr(), self.grads.data_ptr(), self.ms.data_ptr(), n,
-                           self.lr.data_ptr(), float(self.cfg.rmsprop_decay), grad_scale, gate,
-                           s)
+            (self.h.rmsprop_bf16 if w16 else self.h.rmsprop)(
+                self.params.data_ptr(), g, self.ms.data_ptr(), n, self.lr.data_ptr(),
+                float(self.cfg.rmsprop_decay), grad_scale, gate, s)
         else:
-            self.h.sgd(self.params.data_ptr(), self.grads.data_ptr(), n, self.lr.data_ptr(),
-                       grad_scale, gate, s)
+            (self.h.sgd_bf16 if w16 else self.h.sgd)(self.params.data_ptr(), g, n,
+                                                     self.lr.data_ptr(), grad_scale, gate, s)
         self._fp8_update(s)
         # bf16 (+ e4m3) operand copies of the updated weights + lr *= (1 - rateDecay)
         t = self._step_refresh_table()

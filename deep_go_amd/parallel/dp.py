@@ -359,11 +359,15 @@ class GradBucketer:
     stream and queues the bucket's all-reduce there — graph-capturable; ``join()`` makes the
     current stream wait for every queued bucket.
 
-    ``grad_dtype="bf16"``: the wire format is bf16 (half the bytes); the bucket is rounded
-    into a bf16 shadow on the comm stream and the sum written back to the fp32 gradients."""
+    ``grad_dtype="bf16"``: the wire format is bf16 (half the bytes).  With ``shadow`` (the
+    model's bf16 gradient twin, HipGoNet(grad_wire="bf16").grads16, written by the gradient
+    reduce kernels themselves) the buckets are all-reduced in place on it and the optimizer
+    reads it: no conversion kernels.  Without, the bucket is rounded into a private bf16
+    shadow on the comm stream and the sum written back to the fp32 gradients."""
 
     def __init__(self, grads: torch.Tensor, buckets: List[Tuple[int, int, int]],
-                 group=None, grad_dtype: str = "fp32", comm=None):
+                 group=None, grad_dtype: str = "fp32", comm=None,
+                 shadow: Optional[torch.Tensor] = None):
         self.grads = grads
         self.buckets = buckets
         self.comm = comm if comm is not None else TorchComm(group)
@@ -371,8 +375,16 @@ class GradBucketer:
         self.grad_dtype = grad_dtype
         self.works = []
         self._shadow = None
+        self.direct = False          # all-reduce the model's own bf16 twin (no copies)
         if grad_dtype == "bf16":
-            self._shadow = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device)
+            if shadow is not None:
+                if shadow.dtype != torch.bfloat16 or shadow.numel() != grads.numel():
+                    raise ValueError("shadow must be a bf16 twin of the flat gradient")
+                self._shadow = shadow
+                self.direct = True
+            else:
+                self._shadow = torch.empty(grads.numel(), dtype=torch.bfloat16,
+                                           device=grads.device)
 
     @property
     def in_graph(self) -> bool:
@@ -385,7 +397,8 @@ class GradBucketer:
         s, e, _ = self.buckets[b]
         if self._shadow is not None:
             sh = self._shadow[s:e]
-            sh.copy_(self.grads[s:e])
+            if not self.direct:
+                sh.copy_(self.grads[s:e])
             self.works.append((self.comm.all_reduce_async(sh), b))
         else:
             self.works.append((self.comm.all_reduce_async(self.grads[s:e]), b))
@@ -395,7 +408,7 @@ class GradBucketer:
             return self.join()
         for w, b in self.works:
             w.wait()
-            if self._shadow is not None:
+            if self._shadow is not None and not self.direct:
                 s, e, _ = self.buckets[b]
                 self.grads[s:e].copy_(self._shadow[s:e])
         self.works = []
@@ -408,9 +421,12 @@ class GradBucketer:
         with torch.cuda.stream(cs):
             if self._shadow is not None:
                 sh = self._shadow[s:e]
-                sh.copy_(self.grads[s:e])
-                self.comm.all_reduce_(sh)
-                self.grads[s:e].copy_(sh)
+                if self.direct:
+                    self.comm.all_reduce_(sh)
+                else:
+                    sh.copy_(self.grads[s:e])
+                    self.comm.all_reduce_(sh)
+                    self.grads[s:e].copy_(sh)
             else:
                 self.comm.all_reduce_(self.grads[s:e])
 

@@ -155,7 +155,8 @@ class HIPBackend:
         self.world = world
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.net = HipGoNet(cfg, batch, device=self.device, flat_params=flat,
-                            global_batch=batch * world)
+                            global_batch=batch * world,
+                            grad_wire=grad_dtype if world > 1 else "fp32")
         self.layout = self.net.layout
         if world > 1 and flat is None:
             dp.broadcast_(self.net.params, 0)
@@ -171,7 +172,8 @@ class HIPBackend:
             self.bucketer = dp.GradBucketer(self.net.grads,
                                             dp.make_buckets(ranges, int(bucket_mb * 2 ** 20),
                                                             groups=self.net.wgroups),
-                                            grad_dtype=grad_dtype, comm=self.comm)
+                                            grad_dtype=grad_dtype, comm=self.comm,
+                                            shadow=self.net.grads16)
         # the loader's pinned slots are copied on a load stream beside the previous step
         # (HipGoNet.enable_prefetch; +1.1% with host batches, DG_PREFETCH=0: off)
         if os.environ.get("DG_PREFETCH", "auto") != "0":

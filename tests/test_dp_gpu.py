@@ -29,8 +29,11 @@ def rccl_world1(monkeypatch):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16", "bf16-direct"])
 def test_segmented_step_with_rccl_buckets(rccl_world1, grad_dtype):
+    """Graph segments between bucket all-reduces (world 1); bf16 wire through a private
+    shadow (copies around the collective) or directly on the model's bf16 twin, which the
+    gradient reduce kernels write and the optimizer reads (no conversion kernels)."""
     from deep_go_amd.config import ExperimentConfig
     from deep_go_amd.data.synthetic import random_planes
     from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep
@@ -40,7 +43,8 @@ def test_segmented_step_with_rccl_buckets(rccl_world1, grad_dtype):
     ref = HipGoNet(cfg, 8, device="cuda")
     ref.set_batch(*data)
     ref.forward_backward()
-    net = HipGoNet(cfg, 8, device="cuda")
+    direct = grad_dtype == "bf16-direct"
+    net = HipGoNet(cfg, 8, device="cuda", grad_wire="bf16" if direct else "fp32")
     dp.broadcast_(net.params, 0)
     net.refresh_weights()
     net.set_batch(*data)
@@ -48,18 +52,26 @@ def test_segmented_step_with_rccl_buckets(rccl_world1, grad_dtype):
     ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
     buckets = dp.make_buckets(ranges, 256 * 1024)  # small buckets: several segments
     assert len(buckets) >= 3
-    bk = dp.GradBucketer(net.grads, buckets, grad_dtype=grad_dtype)
+    bk = dp.GradBucketer(net.grads, buckets, grad_dtype="bf16" if direct else grad_dtype,
+                         shadow=net.grads16)
+    assert bk.direct == direct
     step = SegmentedStep(net, bk, use_graphs=True)
     assert len(step.graphs) >= 3
     step.forward_backward()
     torch.cuda.synchronize()
     tol = dict(rtol=1e-5, atol=1e-8) if grad_dtype == "fp32" else dict(rtol=1e-2, atol=1e-5)
     assert torch.allclose(net.grads, ref.grads, **tol)
+    if direct:   # the twin is the fp32 gradient rounded once (world 1: the sum of one)
+        assert torch.equal(net.grads16, ref.grads.to(torch.bfloat16))
     # the optimizer graph runs after the all-reduced gradients
     p0 = net.params.clone()
+    lr = net.lr.item()
     step.optimizer()
     torch.cuda.synchronize()
     assert not torch.equal(p0, net.params)
+    if direct:   # SGD read the bf16 twin
+        want = p0 - torch.tensor(lr, dtype=torch.float32) * net.grads16.float()
+        assert torch.allclose(net.params, want, rtol=1e-6, atol=1e-9)
     vals = dp.all_reduce_scalars([1.5, 2.0], device="cuda")
     assert vals == [1.5, 2.0]
 
