@@ -206,6 +206,150 @@ hipError_t launch_l1(const L1Args& a, int Mpad, hipStream_t stream) {
 
 int g_l1_nw = 4;
 
+// ---- the 5x5 / 40-channel first layer on the forward stack's K loop (conv_l1_frag) ----
+// The generic kernel above stages the weights through an LDS ring (one barrier per K-step)
+// and reads the input frame in its linear 80-B-per-pixel layout (4.6M LDS bank-conflict
+// cycles per launch at d = 256, 26% MFMA busy; profiles/r2_s4_pmc_12x256.txt).  This one
+// is conv_stack2.hip's fused-first-layer scheme as a kernel of its own, for the shapes the
+// stack cannot take (d = 256, fp8 models):
+//   * one workgroup (8 waves) per board; the 23x23x40 frame is gathered ONCE into the
+//     conflict-free plane layout cell(c8, y, x) = c8 * 816 + 35 y + x (16-B cells) and serves
+//     every 128-channel output pass (h loop), so a board's frame is staged once instead of
+//     once per (half board, 128 channels) workgroup;
+//   * the weights stream from L2 into VGPRs in fragment order ([h][16 steps][2][2][4][64] x
+//     8 bf16, written by weight_refresh), half a K-step ahead, with no barrier in the K loop;
+//   * the epilogue adds the stack-order bias table (bf16 bias + position bias), applies
+//     ReLU and stores straight from the accumulators (four 32-B pieces of a pixel's 64
+//     channels back to back), plus the ReLU bitmask the backward-data chain reads.
+constexpr int PF_RP = 35, PF_PS = 816, PF_CELLS = 5 * PF_PS;  // conv_stack2.hip L1RP / L1PS
+constexpr int PF_F = 23, PF_XB = 80, PF_BYTES = PF_F * PF_F * PF_XB;
+constexpr int PF_STEPS = 16, PF_CHUNKS = 125;
+constexpr int PF_STEP_BYTES = 2 * 2 * MF * 64 * 16;   // 16 KB per K-step and 128-co pass
+constexpr int PF_LDS = (PF_CELLS + 63) / 64 * 1024;   // whole 1-KB DMA blocks (65,536 B)
+
+struct L1FragArgs {
+  const char* A;          // fragment-ordered weights, nh passes of 16 x 16 KB
+  const uint2* pbias;     // stack-order bf16 (bias + pos-bias): [h][24][2][4][64] x 4 bf16
+  const char* X;          // input frame [B][23][23][40] bf16
+  char* Y;                // output frame [B][21][21][M] bf16 (interior written)
+  uint8_t* mask;          // optional ReLU bits [B][361][M/8]
+  int M, nh;
+};
+
+__global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int b = blockIdx.x;
+
+  // gather: cell -> (chunk, frame row, column); padding cells re-read pixel 0 (never used)
+  {
+    const char* Xb = a.X + (size_t)b * PF_BYTES;
+    for (int blk = wave; blk < PF_LDS / 1024; blk += 8) {
+      const int cell = blk * 64 + lane;
+      const int c8 = cell / PF_PS, rem = cell - c8 * PF_PS;
+      const int y = rem / PF_RP, x = rem - y * PF_RP;
+      const int off = (c8 < 5 && y < PF_F && x < PF_F) ? (y * PF_F + x) * PF_XB + c8 * 16 : 0;
+      glds16(Xb + off, (LDS_AS void*)(smem + blk * 1024));
+    }
+  }
+  const int lr = lane & 15, lq = lane >> 4;
+  int pbase[NF];   // this lane's pixel centre in the plane layout (bytes)
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    int p = wn * NF * 16 + j * 16 + lr;
+    if (p >= NPTS) p = 0;
+    const int hh = p / BOARD, w = p - (p / BOARD) * BOARD;
+    pbase[j] = ((hh + 2) * PF_RP + (w + 2)) * 16;
+  }
+  const uint32_t a_lane = (uint32_t)(wm * (PF_STEP_BYTES / 2) + lane * 16);
+  auto load_A = [&](const char* A, int kk, bf16x8 (&r)[MF]) {
+    const char* p = A + a_lane + kk * MF * 1024;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) r[i] = *(const bf16x8*)(p + i * 1024);
+  };
+  auto read_B = [&](int s, int kk, bf16x8 (&bfr)[NF]) {
+    int kc = s * 8 + kk * 4 + lq;          // this lane group's (tap, c8) chunk
+    if (kc >= PF_CHUNKS) kc = 0;           // padding chunks: zero weights
+    const int t = kc / 5, c8 = kc - (kc / 5) * 5;
+    const int koff = (c8 * PF_PS + (t / 5 - 2) * PF_RP + (t % 5 - 2)) * 16;
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+      bfr[j] = lds_read_b128((const LDS_AS char*)(smem + pbase[j] + koff));
+  };
+  __syncthreads();   // frame landed
+
+  bf16x8 Ak[2][MF];
+  load_A(a.A, 0, Ak[0]);
+  load_A(a.A, 1, Ak[1]);
+  for (int h = 0; h < a.nh; ++h) {
+    const char* Ah = a.A + (size_t)h * PF_STEPS * PF_STEP_BYTES;
+    const char* A_next = h + 1 < a.nh ? Ah + PF_STEPS * PF_STEP_BYTES : Ah;
+    f32x4 acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int s = 0; s < PF_STEPS; ++s) {
+      // (past the last step of the last pass: a harmless re-load of its step 0)
+      const char* An = s + 1 < PF_STEPS ? Ah + (s + 1) * PF_STEP_BYTES : A_next;
+      bf16x8 bfr[NF];
+      read_B(s, 0, bfr);
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(Ak[0][i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      load_A(An, 0, Ak[0]);
+      read_B(s, 1, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(Ak[1][i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      load_A(An, 1, Ak[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue: + bias table, ReLU, bf16 -> output frame (interior), ReLU bits
+    int z0 = 0;
+    asm volatile("" : "+v"(z0));
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int p = wn * NF * 16 + j * 16 + lr;
+      const int pc = p < NPTS ? p : NPTS - 1;
+      const int hh = pc / BOARD, w = pc - (pc / BOARD) * BOARD;
+      const uint2* pf = a.pbias + (((size_t)(h * 24 + wn * NF + j) * 2 + wm) * 4) * 64 + lane + z0;
+      char* yrow = a.Y + (((size_t)b * 21 + hh + 1) * 21 + (w + 1)) * a.M * 2;
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const uint2 eb = pf[i * 64];
+        const f32x4 v = acc[i][j];
+        const float y0 = fmaxf(v[0] + __uint_as_float(eb.x << 16), 0.f);
+        const float y1 = fmaxf(v[1] + __uint_as_float(eb.x & 0xFFFF0000u), 0.f);
+        const float y2 = fmaxf(v[2] + __uint_as_float(eb.y << 16), 0.f);
+        const float y3 = fmaxf(v[3] + __uint_as_float(eb.y & 0xFFFF0000u), 0.f);
+        uint2 o;
+        o.x = pack_bf16x2(y0, y1);
+        o.y = pack_bf16x2(y2, y3);
+        const int co = h * 128 + wm * 64 + i * 16 + lq * 4;
+        if (a.mask) {
+          // lanes l and l ^ 16 hold channels co..co+3 / co+4..co+7 of one pixel: one byte
+          const uint32_t nib = ((o.x & 0xFFFFu) ? 1u : 0u) | ((o.x >> 16) ? 2u : 0u) |
+                               ((o.y & 0xFFFFu) ? 4u : 0u) | ((o.y >> 16) ? 8u : 0u);
+          const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 16, 64);
+          if (p < NPTS && !(lq & 1))
+            a.mask[((size_t)b * NPTS + p) * (a.M >> 3) + (co >> 3)] = (uint8_t)(nib | (hi << 4));
+        }
+        if (p < NPTS) *(uint2*)(yrow + co * 2) = o;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -239,6 +383,29 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
 }
 
 void dg_conv_l1_set_nw(int nw) { g_l1_nw = nw == 8 ? 8 : 4;
+}
+
+// conv_l1_frag: 5x5 over the [B][23][23][40] input frame -> [B][21][21][M] (pad 1), M a
+// multiple of 128; A = weight_refresh's fragment-ordered first-layer operand, pbias = its
+// stack-order bias table; mask optional.
+int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad) {
+  return kw == 5 && x_pad == 2 && x_C == 40 && M % 128 == 0 && M <= 512 && y_pad == 1;
+}
+
+hipError_t dg_conv_l1_frag(const void* A, const void* pbias, const void* X, int B, int M,
+                           void* Y, void* mask, hipStream_t stream) {
+  if (!A || !pbias || !X || !Y || B <= 0 || M % 128 != 0 || M > 512)
+    return hipErrorInvalidValue;
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
+    done = true;
+  }
+  L1FragArgs a{(const char*)A, (const uint2*)pbias, (const char*)X, (char*)Y,
+               (uint8_t*)mask, M, M / 128};
+  hipLaunchKernelGGL(conv_l1_frag_kernel, dim3(B), dim3(512), PF_LDS, stream, a);
+  return hipGetLastError();
 }
 
 }  // extern "C"

@@ -331,11 +331,12 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       }
     }
     if (L.wf_frag && L.taps != 9) {
-      // the first layer fused in front of the forward stack (conv_stack2.hip l1 mode):
-      // [128 co][K = taps*cinp (linear, padded to 1024)] in the stack's fragment order
-      // [s][wm][kk][i][lane] x 8 bf16; the 16-B unit of row co and 8-channel chunk
-      // kc = t*gpt + c8 sits at s = kc/8, kk = (kc/4)&1, lane group kc&3 (chunks past the
-      // last tap stay zero: the buffer is zero-initialised and never written there)
+      // the first layer fused in front of the forward stack (conv_stack2.hip l1 mode) or
+      // on conv_l1_frag (conv_l1.hip): [co][K = taps*cinp (linear, padded to 1024)] in the
+      // stack's fragment order [h][s][wm][kk][i][lane] x 8 bf16 (h = 128-channel output
+      // pass); the 16-B unit of row co and 8-channel chunk kc = t*gpt + c8 sits at s = kc/8,
+      // kk = (kc/4)&1, lane group kc&3 (chunks past the last tap stay zero: the buffer is
+      // zero-initialised and never written there)
       const int gpt = L.cinp / 8;
       for (int u = threadIdx.x; u < 64 * gpt; u += 256) {
         const int rr = u / gpt, c8 = u - (u / gpt) * gpt;
@@ -345,8 +346,8 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           f[e] = pack_bf16x2(tileS[rr][c8 * 8 + 2 * e], tileS[rr][c8 * 8 + 2 * e + 1]);
-        L.wf_frag[((((size_t)(kc >> 3) * 2 + cot) * 2 + ((kc >> 2) & 1)) * 4 + (rr >> 4)) * 64 +
-                  lane] = uint4{f[0], f[1], f[2], f[3]};
+        L.wf_frag[(((((size_t)(cot >> 1) * 16 + (kc >> 3)) * 2 + (cot & 1)) * 2 +
+                    ((kc >> 2) & 1)) * 4 + (rr >> 4)) * 64 + lane] = uint4{f[0], f[1], f[2], f[3]};
       }
     } else if (L.wf_frag || L.wd_frag) {
       // this tile is exactly one 8 KB (step, co-half) chunk of each fragment layout:
@@ -626,7 +627,8 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
     a.L[i].wd_frag = (uint4*)t[17];
     if (a.L[i].wf8 && !a.L[i].s_w) return hipErrorInvalidValue;
     if (a.L[i].wf_frag && a.L[i].taps != 9 &&   // the fused-first-layer layout (l1 mode)
-        (a.L[i].wd_frag || a.L[i].cout != 128 || a.L[i].cin > 64 || a.L[i].cinp % 8 != 0 ||
+        (a.L[i].wd_frag || (a.L[i].cout != 128 && a.L[i].cout != 256) || a.L[i].cin > 64 ||
+         a.L[i].cinp % 8 != 0 ||
          a.L[i].taps * a.L[i].cinp > 1024))
       return hipErrorInvalidValue;
     a.L[i].wf8_frag = (uint4*)t[18];

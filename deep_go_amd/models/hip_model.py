@@ -162,10 +162,11 @@ class HipGoNet:
         self.wf8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.wd8frag: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         for p in self.plans:
-            if p.index == 0 and self._stack_l1_ok(p):
+            if p.index == 0 and (self._stack_l1_ok(p) or self._l1_frag_ok(p)):
                 # the first layer fused in front of the forward stack (conv_stack2.hip l1
-                # mode): [128][1024] weights in fragment order (k linear), no dgrad operand
-                self.wfrag[0] = torch.zeros(128 * 1024, dtype=torch.bfloat16, device=dev)
+                # mode) or on conv_l1_frag (conv_l1.hip): [cout][1024] weights in fragment
+                # order (k linear), no dgrad operand
+                self.wfrag[0] = torch.zeros(p.cout * 1024, dtype=torch.bfloat16, device=dev)
             if (p.index > 0 and p.k == 3 and p.cin == p.cout == p.cinp
                     and (p.cout == 128 or (p.cout == 256 and self._layer2_ok(p)))):
                 # 128: the layer stacks; 256: the per-layer conv_layer2 kernel
@@ -374,6 +375,15 @@ class HipGoNet:
                     xin.data_ptr(), x_pad, p.cinp, self.B,
                     self.act[p.index].data_ptr(), y_pad,
                     0, 0, self.pbias[p.index].data_ptr(), 0, 0,
+                    msk.data_ptr() if msk is not None else 0)))
+            elif self._l1_res_ok(p) and self.wfrag[0] is not None:
+                # first layer on conv_l1_frag (conv_l1.hip): one board per workgroup, the
+                # input frame gathered once into a conflict-free plane layout, fragment-ordered
+                # weights streamed into VGPRs (when the forward stack does not absorb it)
+                msk = self.relu_mask[0]
+                self._fwd.append((h.conv_l1_frag, (
+                    self.wfrag[0].data_ptr(), self.pbias_frag[0].data_ptr(), xin.data_ptr(),
+                    self.B, p.cout, self.act[0].data_ptr(),
                     msk.data_ptr() if msk is not None else 0)))
             elif self._l1_res_ok(p):
                 # first layer board-resident (conv_l1.hip): the 23x23x40 input frame staged
@@ -593,7 +603,7 @@ class HipGoNet:
         # the first layer in front of the stack (conv_stack2.hip l1 mode): its input frame is
         # the expanded network input, its output act[0] leaves by the stack's copy-out
         self.stack_l1 = (not fp8 and first == 1 and self.wfrag[0] is not None
-                         and self.relu_mask[0] is not None)
+                         and self.relu_mask[0] is not None and self._stack_l1_ok(self.plans[0]))
         if self.stack_l1:
             rows.insert(0, [self.wfrag[0].data_ptr(), self.pbias_frag[0].data_ptr(),
                             self.act[0].data_ptr(), self.relu_mask[0].data_ptr()])
@@ -765,6 +775,15 @@ class HipGoNet:
                 and p.KP == 1024 and lay[0].pad == 2 and len(lay) > 2 and lay[1].pad == 1
                 and os.environ.get("DG_STACK_L1", "1") != "0"
                 and os.environ.get("DG_STACK", "1") != "0" and self._l1_res_ok(p))
+
+    def _l1_frag_ok(self, p: ConvPlan) -> bool:
+        """The 5x5 / 40-channel first layer on conv_l1_frag (conv_l1.hip: board per
+        workgroup, fragment-ordered weights, conflict-free input planes) when the forward
+        stack does not absorb it (d = 256, fp8 models).  DG_L1_FRAG=0: conv_l1."""
+        lay = self.layout.layers
+        return (p.index == 0 and p.KP == 1024 and len(lay) > 2 and self._l1_res_ok(p)
+                and os.environ.get("DG_L1_FRAG", "1") != "0"
+                and bool(self.h.conv_l1_frag_ok(p.k, lay[0].pad, p.cinp, p.cout, lay[1].pad)))
 
     def _l1_res_ok(self, p: ConvPlan) -> bool:
         """First layer on the board-resident kernel (conv_l1.hip) where its shape checks

@@ -70,6 +70,26 @@ def conv_l1(x: torch.Tensor, w: torch.Tensor, bias, posb, with_mask: bool = Fals
     return LY.from_frame(yf, 1, cout)
 
 
+def conv_l1_frag(x: torch.Tensor, w: torch.Tensor, bias, posb):
+    """First-layer forward on conv_l1_frag (conv_l1.hip: one board per workgroup, plane-staged
+    input, fragment-ordered weights, stack-order bf16 bias table) for the 5x5 / 37-40 channel
+    layer: relu(conv + bf16(bias + posb)) as fp32 NCHW, and the ReLU bitmask [B][361][Cout/8]."""
+    h = hip()
+    dev = w.device
+    B, cin = x.shape[:2]
+    cout, k, _, _ = w.shape
+    assert k == 5 and cin <= 40 and h.conv_l1_frag_ok(k, 2, 40, cout, 1)
+    KP, _, Mpad = LY.conv_dims(k, 40, cout, 128)
+    xf = LY.to_frame(x.to(dev), 2, 40)
+    yf = LY.alloc_frame(B, cout, 1, dev)
+    A = LY.stack_frag_linear(LY.fwd_weight(w.float(), 40, KP, Mpad), cout)
+    pbf = LY.stack_pbias_frag(bias.to(dev), posb.to(dev))
+    mask = torch.zeros(B, NPTS, cout // 8, dtype=torch.uint8, device=dev)
+    h.conv_l1_frag(A.data_ptr(), pbf.data_ptr(), xf.data_ptr(), B, cout, yf.data_ptr(),
+                   mask.data_ptr(), stream_handle())
+    return LY.from_frame(yf, 1, cout), mask
+
+
 def conv_nt_mask(x: torch.Tensor, w: torch.Tensor, bias, posb):
     """Pixel-tiled forward that also writes the ReLU bitmask [B][361][Cout/8] (bit k of
     byte q = channel 8q + k > 0).  Returns (NCHW output, mask)."""

@@ -76,14 +76,26 @@ def stack_frag(A: torch.Tensor) -> torch.Tensor:
     return a.permute(4, 3, 0, 5, 1, 6, 2, 7).reshape(-1).contiguous()
 
 
-def stack_frag_linear(A: torch.Tensor) -> torch.Tensor:
-    """conv_stack2's fused-first-layer A order (l1 mode) of a [128][1024] operand matrix with
-    LINEAR k (fwd_weight of the 5x5 40-channel first layer, k = tap*40 + c, zero-padded from
-    1000): flat [s 16][wm 2][kk 2][i 4][lane 64][e 8] with row wm*64 + i*16 + (lane & 15),
-    column s*64 + kk*32 + (lane >> 4)*8 + e."""
-    assert A.shape[0] >= 128 and A.shape[1] >= 1024
-    a = A[:128, :1024].reshape(2, 4, 16, 16, 2, 4, 8)     # wm i lr | s kk lq e
-    return a.permute(3, 0, 4, 1, 5, 2, 6).reshape(-1).contiguous()
+def stack_frag_linear(A: torch.Tensor, cout: int = 128) -> torch.Tensor:
+    """conv_stack2's fused-first-layer A order (l1 mode; also conv_l1_frag) of a
+    [cout][1024] operand matrix with LINEAR k (fwd_weight of the 5x5 40-channel first layer,
+    k = tap*40 + c, zero-padded from 1000): flat [h cout/128][s 16][wm 2][kk 2][i 4][lane 64]
+    [e 8] with row 128h + wm*64 + i*16 + (lane & 15), column s*64 + kk*32 + (lane >> 4)*8 + e."""
+    assert cout % 128 == 0 and A.shape[0] >= cout and A.shape[1] >= 1024
+    a = A[:cout, :1024].reshape(cout // 128, 2, 4, 16, 16, 2, 4, 8)   # h wm i lr | s kk lq e
+    return a.permute(0, 4, 1, 5, 2, 6, 3, 7).reshape(-1).contiguous()
+
+
+def stack_pbias_frag(bias: torch.Tensor, posb: torch.Tensor) -> torch.Tensor:
+    """The forward stacks' epilogue table (weight_refresh pbias_frag): bf16(bias + posb) of
+    [361][cout] (cout = 128h) as flat [h][24 px frags][wm 2][i 4][lane 64][4] with pixel
+    jg*16 + (lane & 15) (clamped to 360) and channels 128h + wm*64 + i*16 + (lane >> 4)*4 + e."""
+    cout = bias.numel()
+    t = (posb.float() + bias.float()[None, :]).to(torch.bfloat16)            # [361][cout]
+    p = torch.arange(24 * 16, device=t.device).clamp(max=360)
+    t = t[p]                                                                 # [384][cout]
+    a = t.reshape(24, 16, cout // 128, 2, 4, 4, 4)       # jg lr | h wm i lq e
+    return a.permute(2, 0, 3, 4, 5, 1, 6).reshape(-1).contiguous()
 
 
 def stack_frag_f8(w8: torch.Tensor) -> torch.Tensor:

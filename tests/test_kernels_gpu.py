@@ -249,6 +249,26 @@ def test_conv_l1(B, cin, cout, k, nw):
     assert torch.equal(bits.reshape(B, 361, cout).bool(), nz)
 
 
+@pytest.mark.parametrize("B,cin,cout", [(3, 37, 128), (2, 40, 256), (5, 37, 384), (1, 16, 128)])
+def test_conv_l1_frag(B, cin, cout):
+    """First layer on conv_l1_frag (conv_l1.hip: one board per workgroup, the input frame in
+    conflict-free planes, fragment-ordered weights, 1-3 128-channel passes) vs the fp32
+    reference with the same bf16-rounded bias table, and its ReLU bitmask."""
+    torch.manual_seed(9)
+    from deep_go_amd.ops import functional as Fn
+    x = bf(torch.randn(B, cin, 19, 19, device=DEV))
+    w = bf(torch.randn(cout, 5, 5, cin, device=DEV) * 0.1)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pb = torch.randn(361, cout, device=DEV) * 0.1
+    y, mask = Fn.conv_l1_frag(x, w, b, pb)
+    tab = (pb + b[None, :]).to(torch.bfloat16).float()
+    ref = torch.relu(conv_ref(x, w, 5) + tab.t().reshape(1, cout, 19, 19))
+    assert rel_err(y, ref) < 1e-2
+    bits = (mask.unsqueeze(-1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1
+    nz = (y.to(torch.bfloat16) != 0).permute(0, 2, 3, 1).reshape(B, 361, cout)
+    assert torch.equal(bits.reshape(B, 361, cout).bool(), nz)
+
+
 @pytest.mark.parametrize("B,cin,cout,splits", [
     (3, 128, 128, None), (1, 128, 128, 1), (2, 128, 128, 26), (5, 256, 256, None),
     (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5), (3, 128, 64, None)])

@@ -357,24 +357,52 @@ def test_first_layer_fused_into_forward_stack(monkeypatch):
     """conv_stack2 l1 mode: the 5x5 first layer runs inside the forward stack's launch
     (default) — its fragment-ordered weights are fwd_weight permuted by stack_frag_linear,
     and activations, ReLU masks, loss and gradients are bit-identical to the standalone
-    conv_l1 launch (DG_STACK_L1=0; both add the same bf16 bias table)."""
+    first-layer launches: conv_l1_frag (DG_STACK_L1=0) and conv_l1 (DG_L1_FRAG=0 too); all
+    add the same bf16 bias table."""
     from deep_go_amd.ops import layouts as LY
     monkeypatch.setenv("DG_STACK_L1", "0")
+    monkeypatch.setenv("DG_L1_FRAG", "0")
+    _, n2, _ = _setup(5, 128, 5, seed=21)
+    monkeypatch.setenv("DG_L1_FRAG", "1")
     _, n0, _ = _setup(5, 128, 5, seed=21)
     monkeypatch.setenv("DG_STACK_L1", "1")
     _, n1, _ = _setup(5, 128, 5, seed=21)
-    assert n1.stack_l1 and not n0.stack_l1
-    assert not any(f is n1.h.conv_l1 for f, _ in n1._fwd_train)
-    assert any(f is n0.h.conv_l1 for f, _ in n0._fwd_train)
+    assert n1.stack_l1 and not n0.stack_l1 and not n2.stack_l1
+    assert not any(f in (n1.h.conv_l1, n1.h.conv_l1_frag) for f, _ in n1._fwd_train)
+    assert any(f is n0.h.conv_l1_frag for f, _ in n0._fwd_train)
+    assert any(f is n2.h.conv_l1 for f, _ in n2._fwd_train)
     assert torch.equal(n1.wfrag[0], LY.stack_frag_linear(n1.wf[0]))
+    for n in (n0, n1, n2):
+        n.forward_backward()
+    torch.cuda.synchronize()
+    for other in (n0, n2):
+        for a0, a1 in zip(other.act, n1.act):
+            assert torch.equal(a0, a1)
+        for m0, m1 in zip(other.relu_mask, n1.relu_mask):
+            if m0 is not None:
+                assert torch.equal(m0, m1)
+        assert torch.equal(other.loss, n1.loss)
+        assert torch.allclose(other.grads, n1.grads, rtol=1e-5, atol=1e-8)
+
+
+def test_first_layer_frag_kernel_d256(monkeypatch):
+    """At d = 256 the first layer runs on conv_l1_frag (two 128-channel passes over one staged
+    input frame); its activations and ReLU bits equal the generic conv_l1 kernel's bit for
+    bit (same K order, same bf16 bias table), and the model's weight refresh writes the
+    two-pass fragment order stack_frag_linear(wf[0], 256)."""
+    from deep_go_amd.ops import layouts as LY
+    monkeypatch.setenv("DG_L1_FRAG", "0")
+    _, n0, _ = _setup(4, 256, 4, seed=5)
+    monkeypatch.setenv("DG_L1_FRAG", "1")
+    _, n1, _ = _setup(4, 256, 4, seed=5)
+    assert any(f is n1.h.conv_l1_frag for f, _ in n1._fwd_train)
+    assert any(f is n0.h.conv_l1 for f, _ in n0._fwd_train)
+    assert torch.equal(n1.wfrag[0], LY.stack_frag_linear(n1.wf[0], 256))
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
-    for a0, a1 in zip(n0.act, n1.act):
-        assert torch.equal(a0, a1)
-    for m0, m1 in zip(n0.relu_mask, n1.relu_mask):
-        if m0 is not None:
-            assert torch.equal(m0, m1)
+    assert torch.equal(n0.act[0], n1.act[0])
+    assert torch.equal(n0.relu_mask[0], n1.relu_mask[0])
     assert torch.equal(n0.loss, n1.loss)
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-5, atol=1e-8)
 
