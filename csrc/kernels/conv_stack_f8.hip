@@ -192,7 +192,9 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // 2 = no A loads in the K loop, 4 = no copy-out.  MODE bit 8 (production, fp8 weight
 // gradients): also store the raw fp8 copies (X8_0, every non-last layer's Y8) — a compile-time
 // switch: a runtime null test around the store splits the K loop's blocks and costs 24-45
-// spilled VGPRs
+// spilled VGPRs.  MODE bit 16 (with 8, forward): no dequantized bf16 copy-out of the non-last
+// layers — every consumer of those activations reads the fp8 copies (the MX-fp8 weight
+// gradient) or the ReLU bits (the backward-data chain); the table's Y is null there
 template <int C, int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   using G = Geo<C>;
@@ -323,9 +325,11 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (EPI == EPI_FWD)
         bits |= nzbits4(wd[k]) << (4 * k);   // ReLU bit = byte nonzero (values are >= 0)
     }
-    char* yp = yb + inner * 2;
-    *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
-    *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
+    if constexpr ((MODE & 16) == 0) {
+      char* yp = yb + inner * 2;
+      *(uint4*)yp = uint4{o[0], o[1], o[2], o[3]};
+      *(uint4*)(yp + 16) = uint4{o[4], o[5], o[6], o[7]};
+    }
     if constexpr (EPI == EPI_FWD)
       *(uint16_t*)(mask + ((size_t)b * NPTS + p) * (C / 8) + q * 2) = (uint16_t)bits;
   };
@@ -339,7 +343,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
     const bool co_on = l > 0;
-    char* co_yb = Lprev.Y + (size_t)b * FF * C * 2;
+    char* co_yb = (MODE & 16) ? nullptr : Lprev.Y + (size_t)b * FF * C * 2;
     uint8_t* co_y8b = Lprev.Y8 ? Lprev.Y8 + (size_t)b * FP8P * C : nullptr;
     const bool last = l + 1 == a.nl;
     const float s_x = *L.s_in;
@@ -555,7 +559,12 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
   const bool y8 = a.X8_0 != nullptr;
   if (epi == EPI_DGRAD)
     return y8 ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream) : launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
-  if (y8) return launch_f8<C, EPI_FWD, 8>(a, B, stream);
+  if (y8) {
+    // no bf16 activation frame wanted for any non-last layer: skip their bf16 copy-out
+    bool any_y = false;
+    for (int i = 0; i + 1 < a.nl; ++i) any_y |= a.L[i].Y != nullptr;
+    return any_y ? launch_f8<C, EPI_FWD, 8>(a, B, stream) : launch_f8<C, EPI_FWD, 24>(a, B, stream);
+  }
   switch (g_f8_mode) {
     case 2: return launch_f8<C, EPI_FWD, 2>(a, B, stream);
     case 4: return launch_f8<C, EPI_FWD, 4>(a, B, stream);
@@ -595,8 +604,12 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
     L.Y8 = y8 ? (uint8_t*)y8[1 + i] : nullptr;
     // (a y8 table covers every layer: all non-last copies present, the last absent)
     if (y8 && (i + 1 == nl) != (L.Y8 == nullptr)) return hipErrorInvalidValue;
-    if (!L.A8 || !L.Y || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
+    // (Y of a non-last forward layer may be null when the fp8 copies are written: then every
+    // non-last Y must be null and the bf16 copy-out is skipped)
+    const bool y_opt = y8 && epi == EPI_FWD && i + 1 < nl;
+    if (!L.A8 || (!L.Y && !y_opt) || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
       return hipErrorInvalidValue;
+    if (y_opt && i > 0 && (L.Y == nullptr) != (a.L[0].Y == nullptr)) return hipErrorInvalidValue;
     if (epi == EPI_FWD && !L.pbias) return hipErrorInvalidValue;
   }
   return C == 128 ? launch_mode<128>(epi, a, B, stream) : launch_mode<256>(epi, a, B, stream);

@@ -73,7 +73,7 @@ class HipGoNet:
     def __init__(self, cfg: ExperimentConfig, batch: int, device="cuda",
                  flat_params: Optional[torch.Tensor] = None, num_cus: Optional[int] = None,
                  global_batch: Optional[int] = None, wgrad_group: Optional[int] = None,
-                 grad_wire: str = "fp32"):
+                 grad_wire: str = "fp32", keep_act_frames: bool = False):
         if cfg.numLayers < 2:
             raise ValueError("HIP executor needs >= 2 layers (conv stack + head)")
         self.cfg = cfg
@@ -83,6 +83,9 @@ class HipGoNet:
         # data parallelism splits the hidden layers into groups so the top group's
         # all-reduce runs beside the next group's launch (bench.py --wgrad-group)
         self._wgrad_group = wgrad_group
+        # keep_act_frames: always write every layer's bf16 activation frame (tests / tools
+        # that inspect them); by default an fp8 stack skips frames no launch reads
+        self.keep_act_frames = keep_act_frames
         self.device = torch.device(device)
         self.h = hip()
         self.layout = ParamLayout(cfg)
@@ -441,8 +444,7 @@ class HipGoNet:
         self._fwd_train = self._fwd
         if (self.stack and self.stack[-1] == len(self.plans) - 1 and hd.k == 3
                 and hd.cin == 128 and hd.pad == 1 and self.dzp[-1] == 1
-                and os.environ.get("DG_FUSE_HEAD", "1") != "0"
-                and os.environ.get("DG_HEAD_MFMA", "1") != "0"):
+                and os.environ.get("DG_FUSE_HEAD", "1") != "0"):
             first = self.stack[0]
             fused = (h.conv_stack2_fwd_head, (
                 self._stack_table.ctypes.data, len(self._stack_table),
@@ -514,6 +516,23 @@ class HipGoNet:
             self._bwd.append(ops)
         self._fuse_dgrad_stack()
         self._bwd_pre, _ = self._merge_layer2_runs(self._bwd_pre)
+        self._drop_unread_act_frames()
+
+    def _drop_unread_act_frames(self):
+        """fp8 forward stack with the MX-fp8 weight gradients: when no launch of the model
+        reads the bf16 activation frame of any non-last stack layer (the weight gradients read
+        the e4m3 copies, the backward-data chain the ReLU bits), null those rows' Y so the
+        stack skips their dequantized bf16 copy-out (conv_stack_f8.hip MODE 16).
+        ``self.act_frames_dropped`` lists the layers whose act frame is then not written."""
+        self.act_frames_dropped = []
+        t = getattr(self, "_stack_table", None)
+        if (not self.keep_act_frames and self.stack_fp8 and getattr(self, "_fwd_y8", None)
+                is not None and isinstance(t, np.ndarray) and len(t) > 1):
+            used = self._op_pointers(exclude=(t,))   # pointers read by every OTHER launch
+            ys = [int(v) for v in t[:-1, 2]]
+            if not any(y in used for y in ys):
+                t[:-1, 2] = 0
+                self.act_frames_dropped = list(self.stack[:-1])
 
     def _merge_layer2_runs(self, ops, owners=None):
         """Consecutive conv_layer2 launches of one kind whose layers chain (X of the next =
@@ -1156,7 +1175,7 @@ class HipGoNet:
         self.h.weight_refresh_decay(t.ctypes.data, len(t), self.lr.data_ptr(),
                                     float(self.cfg.rateDecay), self.step_count.data_ptr(), s)
 
-    def _op_pointers(self) -> set:
+    def _op_pointers(self, exclude=()) -> set:
         """Every integer argument (and int64 table entry) of the launches the model issues:
         the input / forward / head / backward op lists that forward(), forward_backward(),
         evaluate() and backward_layer() run."""
@@ -1173,10 +1192,15 @@ class HipGoNet:
                 add(op)
         for op in (self._head_train, self._head_red, self._head_eval):
             add(op)
-        for t in [getattr(self, "_stack_table", None), getattr(self, "_dstack_table", None),
-                  *getattr(self, "_l2_tables", [])]:
-            if isinstance(t, np.ndarray) and t.dtype == np.int64:
-                vals.update(int(v) for v in t.ravel())
+        # every int64 launch table the model holds (stack / dgrad-stack / layer-run / grouped
+        # weight-gradient / fp8 copy-out tables), except the refresh tables (operand copies
+        # are what _step_refresh_table decides about) and any passed in `exclude`
+        skip = {id(getattr(self, "_refresh_table", None)), id(getattr(self, "_step_refresh", None))}
+        skip.update(id(t) for t in exclude)
+        for name, v in vars(self).items():
+            for t in (v if isinstance(v, (list, tuple)) else [v]):
+                if (isinstance(t, np.ndarray) and t.dtype == np.int64 and id(t) not in skip):
+                    vals.update(int(x) for x in t.ravel())
         return vals
 
     def _step_refresh_table(self) -> np.ndarray:

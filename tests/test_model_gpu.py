@@ -698,8 +698,16 @@ def test_fp8_weight_gradient_teacher_forced(ch, layers):
     a float64 CPU oracle — torch's conv2d weight gradient over those dequantized frames —
     to fp32 summation order (the quantization itself is the oracle's input, so the test is
     teacher-forced: it checks the kernel, not the fp8 rounding)."""
-    from deep_go_amd.models.hip_model import FP8_PITCH
-    _, net, _ = _setup(layers, ch, 8, seed=47, dtype="fp8")
+    from deep_go_amd.models.hip_model import FP8_PITCH, HipGoNet
+    _, net0, data = _setup(layers, ch, 8, seed=47, dtype="fp8")
+    # production skips the bf16 frames of the non-last stack layers (nothing reads them);
+    # keep_act_frames writes them for the comparison below
+    assert net0.act_frames_dropped == list(range(1, layers - 2))
+    net = HipGoNet(net0.cfg, 8, device="cuda", keep_act_frames=True)
+    assert net.act_frames_dropped == []
+    planes, player, rank, labels = data
+    net.set_batch(torch.from_numpy(planes).cuda(), torch.from_numpy(player).cuda(),
+                  torch.from_numpy(rank).cuda(), torch.from_numpy(labels).cuda())
     assert net.win8_groups, "fp8 model must use the MX-fp8 window weight gradient"
     net.forward_backward()
     torch.cuda.synchronize()

@@ -19,7 +19,7 @@
 #   list             rocprofv3 -L -> gpurun_out/counters.txt
 #   py:SCRIPT ARGS   python SCRIPT ARGS (a tools/ script), stdout -> gpurun_out/py_<n>.log
 #   ab:R:A|B|...     R interleaved rounds of bench.py under env settings A, B, ... ("-" = none;
-#                    extra bench.py arguments from $AB_ARGS)
+#                    extra bench.py arguments from $AB_ARGS; "ENV@ARGS" adds ARGS to one arm)
 set -o pipefail
 mkdir -p gpurun_out
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -90,8 +90,9 @@ for step in "$@"; do
       rc=0
       for r in $(seq 1 $rounds); do
         for cfg in "${cfgs[@]}"; do
-          e="$cfg"; [ "$e" = "-" ] && e=""
-          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 ${AB_ARGS:-} 2>/dev/null \
+          e="${cfg%%@*}"; [ "$e" = "-" ] && e=""
+          xa=""; [ "$e" != "$cfg" ] || true; case "$cfg" in *@*) xa="${cfg#*@}" ;; esac
+          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 ${AB_ARGS:-} $xa 2>/dev/null \
                 | grep metric) || { rc=1; break 2; }
           echo "$cfg $(echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")" \
             | tee -a gpurun_out/ab.txt
