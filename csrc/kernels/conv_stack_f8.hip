@@ -192,9 +192,10 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // 2 = no A loads in the K loop, 4 = no copy-out.  MODE bit 8 (production, fp8 weight
 // gradients): also store the raw fp8 copies (X8_0, every non-last layer's Y8) — a compile-time
 // switch: a runtime null test around the store splits the K loop's blocks and costs 24-45
-// spilled VGPRs.  MODE bit 16 (with 8, forward): no dequantized bf16 copy-out of the non-last
-// layers — every consumer of those activations reads the fp8 copies (the MX-fp8 weight
-// gradient) or the ReLU bits (the backward-data chain); the table's Y is null there
+// spilled VGPRs.  MODE bit 16 (with 8): no dequantized bf16 copy-out of the non-last layers —
+// every consumer reads the fp8 copies instead (forward: the MX-fp8 weight gradient, the
+// backward-data chain reads ReLU bits; backward-data: the weight gradient and the bias-gradient
+// partials read the e5m2 copies); the table's Y is null there
 template <int C, int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   using G = Geo<C>;
@@ -557,14 +558,16 @@ hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
 template <int C>
 hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
   const bool y8 = a.X8_0 != nullptr;
-  if (epi == EPI_DGRAD)
-    return y8 ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream) : launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
-  if (y8) {
-    // no bf16 activation frame wanted for any non-last layer: skip their bf16 copy-out
-    bool any_y = false;
-    for (int i = 0; i + 1 < a.nl; ++i) any_y |= a.L[i].Y != nullptr;
-    return any_y ? launch_f8<C, EPI_FWD, 8>(a, B, stream) : launch_f8<C, EPI_FWD, 24>(a, B, stream);
+  // no bf16 frame wanted for any non-last layer (with the fp8 copies): skip their bf16 copy-out
+  bool any_y = false;
+  for (int i = 0; i + 1 < a.nl; ++i) any_y |= a.L[i].Y != nullptr;
+  if (epi == EPI_DGRAD) {
+    if (!y8) return launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
+    return any_y ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream)
+                 : launch_f8<C, EPI_DGRAD, 24>(a, B, stream);
   }
+  if (y8)
+    return any_y ? launch_f8<C, EPI_FWD, 8>(a, B, stream) : launch_f8<C, EPI_FWD, 24>(a, B, stream);
   switch (g_f8_mode) {
     case 2: return launch_f8<C, EPI_FWD, 2>(a, B, stream);
     case 4: return launch_f8<C, EPI_FWD, 4>(a, B, stream);
@@ -606,7 +609,7 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
     if (y8 && (i + 1 == nl) != (L.Y8 == nullptr)) return hipErrorInvalidValue;
     // (Y of a non-last forward layer may be null when the fp8 copies are written: then every
     // non-last Y must be null and the bf16 copy-out is skipped)
-    const bool y_opt = y8 && epi == EPI_FWD && i + 1 < nl;
+    const bool y_opt = y8 && i + 1 < nl;
     if (!L.A8 || (!L.Y && !y_opt) || !L.mask || !L.s_in || !L.s_w || !L.s_out || !L.amax_out)
       return hipErrorInvalidValue;
     if (y_opt && i > 0 && (L.Y == nullptr) != (a.L[0].Y == nullptr)) return hipErrorInvalidValue;

@@ -89,7 +89,12 @@ constexpr int BG_MAXL = 16;
 struct BiasLayers {  // blockIdx.z = layer (several same-shape layers in one launch)
   const char* dZ[BG_MAXL];
   float* part[BG_MAXL];
+  // optional: dZ is the fp8 backward-data stack's e5m2 copy ([B][FP8_ROWS][C] bytes, the
+  // 21x21 frame in rows 0..440) and *s8 its power-of-two scale — the bf16 frame it replaces
+  // is exactly e5m2 x s8, so the partials are bit-identical (null: a bf16 frame)
+  const float* s8[BG_MAXL];
 };
+constexpr int BG_FP8_ROWS = 448;
 __global__ void __launch_bounds__(1024)
 bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int bt) {
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
@@ -97,34 +102,62 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
   const int chunk = blockIdx.y;
   const char* __restrict__ dZ = Ls.dZ[blockIdx.z];
   float* __restrict__ part = Ls.part[blockIdx.z];
+  const float* s8p = Ls.s8[blockIdx.z];
+  const bool f8 = s8p != nullptr;            // uniform per workgroup
+  const float s8 = f8 ? *s8p : 1.f;
   const int b0 = chunk * bt;
   const int G = C / 8;
   const int F = BOARD + 2 * pad;
   const int items = BOARD * G;  // (w, g) pairs of the row
   const int tid = threadIdx.x;
-  const size_t board_stride = (size_t)F * F * C * 2;
-  const char* row0 = dZ + ((size_t)((h + pad) * F + pad) * C) * 2;
+  const int esz = f8 ? 1 : 2;
+  const size_t board_stride = (size_t)(f8 ? BG_FP8_ROWS : F * F) * C * esz;
+  const char* row0 = dZ + ((size_t)((h + pad) * F + pad) * C) * esz;
   float* prow = part + ((size_t)chunk * NPTS + h * BOARD) * C;
   // blockDim covers all 19*C/8 items of the row in ONE pass (the 256-thread version ran a
   // second pass on 48 threads whose load latency the whole workgroup waited for)
   for (int it = tid; it < items; it += blockDim.x) {
     const int w = it / G, g = it - (it / G) * G;
-    const char* src = row0 + ((size_t)w * C + g * 8) * 2;
+    const char* src = row0 + ((size_t)w * C + g * 8) * esz;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
-      uint4 v[BG_LD];
+    if (f8) {
+      for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
+        uint2 v[BG_LD];
 #pragma unroll
-      for (int j = 0; j < BG_LD; ++j) {
-        const int b = b0 + jb + j;
-        v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
+        for (int j = 0; j < BG_LD; ++j) {
+          const int b = b0 + jb + j;
+          v[j] = b < B ? *(const uint2*)(src + (size_t)b * board_stride) : uint2{0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < BG_LD; ++j) {
+          const int u[2] = {(int)v[j].x, (int)v[j].y};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto lo = __builtin_amdgcn_cvt_pk_f32_bf8(u[e], false);
+            const auto hi = __builtin_amdgcn_cvt_pk_f32_bf8(u[e], true);
+            acc[4 * e] += lo[0] * s8;
+            acc[4 * e + 1] += lo[1] * s8;
+            acc[4 * e + 2] += hi[0] * s8;
+            acc[4 * e + 3] += hi[1] * s8;
+          }
+        }
       }
+    } else {
+      for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
+        uint4 v[BG_LD];
 #pragma unroll
-      for (int j = 0; j < BG_LD; ++j) {
-        const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        for (int j = 0; j < BG_LD; ++j) {
+          const int b = b0 + jb + j;
+          v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += __uint_as_float(u[e] << 16);
-          acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+        for (int j = 0; j < BG_LD; ++j) {
+          const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[2 * e] += __uint_as_float(u[e] << 16);
+            acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+          }
         }
       }
     }
@@ -515,7 +548,8 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
   return hipGetLastError();
 }
 
-// Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part};
+// Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part, s8}
+// (s8: 0 = bf16 frame, else the e5m2 copy's scale pointer; pad must be 1 then);
 // chunks of BG_BT_MULTI boards (dg_bias_chunks_multi).
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
                                       hipStream_t s) {
@@ -526,8 +560,10 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
   if (threads < 64) threads = 64;
   BiasLayers Ls{};
   for (int i = 0; i < nl; ++i) {
-    Ls.dZ[i] = (const char*)table[2 * i];
-    Ls.part[i] = (float*)table[2 * i + 1];
+    Ls.dZ[i] = (const char*)table[3 * i];
+    Ls.part[i] = (float*)table[3 * i + 1];
+    Ls.s8[i] = (const float*)table[3 * i + 2];
+    if (Ls.s8[i] && pad != 1) return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, nl), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);

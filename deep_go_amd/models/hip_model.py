@@ -525,6 +525,7 @@ class HipGoNet:
         stack skips their dequantized bf16 copy-out (conv_stack_f8.hip MODE 16).
         ``self.act_frames_dropped`` lists the layers whose act frame is then not written."""
         self.act_frames_dropped = []
+        self.dz_frames_dropped = []
         t = getattr(self, "_stack_table", None)
         if (not self.keep_act_frames and self.stack_fp8 and getattr(self, "_fwd_y8", None)
                 is not None and isinstance(t, np.ndarray) and len(t) > 1):
@@ -533,6 +534,16 @@ class HipGoNet:
             if not any(y in used for y in ys):
                 t[:-1, 2] = 0
                 self.act_frames_dropped = list(self.stack[:-1])
+        # the same for the fp8 backward-data stack's bf16 dZ frames (rows i -> dz[i - 1]):
+        # the MX-fp8 weight gradients and the bias partials read the e5m2 copies instead
+        t = getattr(self, "_dstack_table", None)
+        if (not self.keep_act_frames and self.dstack_fp8 and getattr(self, "_dstack_y8", None)
+                is not None and isinstance(t, np.ndarray) and len(t) > 1):
+            used = self._op_pointers(exclude=(t,))
+            ys = [int(v) for v in t[:-1, 2]]
+            if not any(y in used for y in ys):
+                t[:-1, 2] = 0
+                self.dz_frames_dropped = [i - 1 for i in self.dstack[:-1]]
 
     def _merge_layer2_runs(self, ops, owners=None):
         """Consecutive conv_layer2 launches of one kind whose layers chain (X of the next =
@@ -678,6 +689,7 @@ class HipGoNet:
         self.wgroups: List[List[int]] = []
         self._bwd_pre: List[Tuple[Callable, tuple]] = []
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
+        self._dz8_exact = set()    # layers whose e5m2 gradient copy equals their bf16 dZ
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
@@ -727,6 +739,8 @@ class HipGoNet:
                                                dtype=torch.uint8, device=self.device)
                 y8 = [self.dz8q[run[0]].data_ptr()] + [
                     self.dz8q[i - 1].data_ptr() if i != run[-1] else 0 for i in run]
+                # dz8q[j] that are exactly the bf16 frame dz[j] (the copy-out bytes)
+                self._dz8_exact = {i - 1 for i in run if i != run[-1]}
                 self._dstack_y8 = np.ascontiguousarray(np.array(y8, dtype=np.int64))
                 self._bwd_pre.append((self.h.conv_stack_f8_y8,
                                       args + (self._dstack_y8.ctypes.data,)))
@@ -927,7 +941,13 @@ class HipGoNet:
                                   self.fp8_scales.data_ptr() + 4 * (2 * (i - 1) + 1)])
                 else:
                     wrows.append([self.dz[i].data_ptr(), xin.data_ptr(), slab])
-                brows.append([self.dz[i].data_ptr(), bpart])
+                # bias partials: from the e5m2 copy where it is exactly the bf16 frame (the
+                # fp8 backward-data stack's copy-out; not its top input, which it rounds)
+                if w8 and i in self._dz8_exact:
+                    brows.append([self.dz8q[i].data_ptr(), bpart,
+                                  self.fp8_gscales.data_ptr() + 4 * i])
+                else:
+                    brows.append([self.dz[i].data_ptr(), bpart, 0])
                 rrows.append([slab, G_ + spec.w_off * f4, bpart, G_ + spec.pos_off * f4,
                               G_ + spec.b_off * f4, S, p0.cout, p0.Mpad_w, p0.KPw,
                               p0.k * p0.k, p0.cin, p0.cinp, self.bchunks_g]

@@ -702,15 +702,23 @@ def test_fp8_weight_gradient_teacher_forced(ch, layers):
     _, net0, data = _setup(layers, ch, 8, seed=47, dtype="fp8")
     # production skips the bf16 frames of the non-last stack layers (nothing reads them);
     # keep_act_frames writes them for the comparison below
+    # (and the backward-data stack's bf16 dZ frames below its top: the weight gradients and
+    # the bias partials read the e5m2 copies)
     assert net0.act_frames_dropped == list(range(1, layers - 2))
+    assert sorted(net0.dz_frames_dropped) == list(range(1, layers - 2))
     net = HipGoNet(net0.cfg, 8, device="cuda", keep_act_frames=True)
-    assert net.act_frames_dropped == []
+    assert net.act_frames_dropped == [] and net.dz_frames_dropped == []
     planes, player, rank, labels = data
     net.set_batch(torch.from_numpy(planes).cuda(), torch.from_numpy(player).cuda(),
                   torch.from_numpy(rank).cuda(), torch.from_numpy(labels).cuda())
     assert net.win8_groups, "fp8 model must use the MX-fp8 window weight gradient"
     net.forward_backward()
+    net0.forward_backward()
     torch.cuda.synchronize()
+    # dropping the frames changes no result: loss and every gradient (the bias partials
+    # from e5m2 x scale == from the bf16 frame) bit for bit
+    assert torch.equal(net0.loss, net.loss)
+    assert torch.equal(net0.grads, net.grads)
     B = net.B
     hidden = [i for g in net.win8_groups for i in g]
     assert sorted(hidden) == list(range(1, layers - 1))
