@@ -95,7 +95,13 @@ struct BiasLayers {  // blockIdx.z = layer (several same-shape layers in one lau
   const float* s8[BG_MAXL];
 };
 constexpr int BG_FP8_ROWS = 448;
-__global__ void __launch_bounds__(1024)
+// LD: 16-B loads in flight per thread.  The multi-layer launch runs beside the window weight
+// gradient, whose two workgroups per CU leave 64 VGPRs per SIMD: its variant (LD 2, 256
+// threads, 48 VGPRs) fits next to them on every CU instead of only on the 32 CUs that hold
+// one window workgroup (the 1024-thread, 110-VGPR version was confined there and outlasted
+// the window kernel at d = 256: 12x256 bf16 +1.5%, profiles/r3_bias_partial_small_wg.txt).
+template <int LD>
+__global__ void __launch_bounds__(LD == BG_LD ? 1024 : 256, LD == BG_LD ? 1 : 8)
 bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int bt) {
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
   const int h = blockIdx.x;
@@ -121,15 +127,15 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
     const char* src = row0 + ((size_t)w * C + g * 8) * esz;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (f8) {
-      for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
-        uint2 v[BG_LD];
+      for (int jb = 0; jb < bt && b0 + jb < B; jb += LD) {
+        uint2 v[LD];
 #pragma unroll
-        for (int j = 0; j < BG_LD; ++j) {
+        for (int j = 0; j < LD; ++j) {
           const int b = b0 + jb + j;
           v[j] = b < B ? *(const uint2*)(src + (size_t)b * board_stride) : uint2{0u, 0u};
         }
 #pragma unroll
-        for (int j = 0; j < BG_LD; ++j) {
+        for (int j = 0; j < LD; ++j) {
           const int u[2] = {(int)v[j].x, (int)v[j].y};
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -143,15 +149,15 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
         }
       }
     } else {
-      for (int jb = 0; jb < bt && b0 + jb < B; jb += BG_LD) {
-        uint4 v[BG_LD];
+      for (int jb = 0; jb < bt && b0 + jb < B; jb += LD) {
+        uint4 v[LD];
 #pragma unroll
-        for (int j = 0; j < BG_LD; ++j) {
+        for (int j = 0; j < LD; ++j) {
           const int b = b0 + jb + j;
           v[j] = b < B ? *(const uint4*)(src + (size_t)b * board_stride) : uint4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
-        for (int j = 0; j < BG_LD; ++j) {
+        for (int j = 0; j < LD; ++j) {
           const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -543,7 +549,7 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
   BiasLayers Ls{};
   Ls.dZ[0] = (const char*)dZ;
   Ls.part[0] = part;
-  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, 1), dim3(threads),
+  hipLaunchKernelGGL(bias_grad_partial_kernel<BG_LD>, dim3(BOARD, nchunks, 1), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT);
   return hipGetLastError();
 }
@@ -556,7 +562,7 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
   if (C % 8 != 0 || C > 2048 || nl <= 0 || nl > BG_MAXL) return hipErrorInvalidValue;
   const int nchunks = (B + BG_BT_MULTI - 1) / BG_BT_MULTI;
   int threads = (BOARD * (C / 8) + 63) / 64 * 64;
-  if (threads > 1024) threads = 1024;
+  if (threads > 256) threads = 256;
   if (threads < 64) threads = 64;
   BiasLayers Ls{};
   for (int i = 0; i < nl; ++i) {
@@ -565,7 +571,7 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
     Ls.s8[i] = (const float*)table[3 * i + 2];
     if (Ls.s8[i] && pad != 1) return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(BOARD, nchunks, nl), dim3(threads),
+  hipLaunchKernelGGL(bias_grad_partial_kernel<2>, dim3(BOARD, nchunks, nl), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);
   return hipGetLastError();
 }
