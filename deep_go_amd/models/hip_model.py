@@ -885,11 +885,11 @@ class HipGoNet:
         # partials (on the main stream before that group's launch measured -2.1% at 12x128,
         # -0.4% at 12x256: profiles/r2_l0_first_ab.txt; removed in round 3)
         self._l0_side_at = groups[-1][0] if l0_ok else None
-        if self._l0_side_at is not None and 1 in self._pre_dgrads:
-            # nothing in the groups needs dZ_0: layer 1's dgrad joins the side chain too
-            drop = set(id(op) for op in self._pre_dgrads[1])
-            self._bwd_pre = [op for op in self._bwd_pre if id(op) not in drop]
-            self._l0_dgrad = list(self._pre_dgrads[1])
+        # layer 1's dgrad (-> dZ_0; d = 256 bf16, where the backward-data run stops at layer
+        # 2) stays on the main stream before the grouped launch: on the side stream after the
+        # bias partials it could not co-reside with the window workgroups (112 KB of LDS) and
+        # stretched past the window kernel's end (12x256: +0.5% on the main stream once the
+        # bias partials fit beside the window kernel; profiles/r3_bias_partial_small_wg.txt)
         wgs = h.conv_wgrad_wgs_per_cu_for(self.plans[groups[0][0]].KPw)
         gslab_elems = 0
         plan_splits = {}
