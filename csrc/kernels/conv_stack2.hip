@@ -449,8 +449,10 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     lds_barrier();  // the next layer's input is complete
   }
   lds_barrier();  // C: image 1 of the last layer's output (wm 1) is complete
-  // last layer's output: exposed copy-out
-  {
+  // last layer's output: exposed copy-out — not with the fused head (training): its only
+  // readers are the head (here, on the resident image) and the evaluation forward, which runs
+  // the head-less launch; the head's backward gates with the image itself, not the bitmask
+  if (EPI != EPI_FWD || !a.fuse_head) {
     const StackLayer Ll = a.L[a.nl - 1];
     for (int s_ = 0; s_ < CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
     for (int s_ = T; s_ < T + CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);

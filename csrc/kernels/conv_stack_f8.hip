@@ -517,10 +517,11 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     lds_barrier();  // the next layer's input is complete
   }
   if constexpr (BF16_LAST_IMAGE) {
-    // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2
+    // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2 (skipped with
+    // the fused head: training reads neither; evaluation runs the head-less launch)
     const F8Layer Ll = a.L[a.nl - 1];
     const int co_q = tid & 15;
-    for (int s_ = 0; s_ < (NPTS * 16 + NT - 1) / NT; ++s_) {
+    for (int s_ = 0; s_ < (a.fuse_head ? 0 : (NPTS * 16 + NT - 1) / NT); ++s_) {
       const int p = min((tid >> 4) + 32 * s_, NPTS - 1);
       const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
       const int f = (h + 1) * F + (w + 1);
