@@ -183,6 +183,35 @@ def test_stack_frag_linear_indexing():
         assert f[s_, wm, kk, i, lane, e].item() == A[row, col].item()
 
 
+def test_stack_frag_linear_multi_pass_and_pbias_indexing():
+    """conv_l1_frag's operands (conv_l1.hip): the first layer's [256][1024] weights as two
+    128-channel passes [h][s][wm][kk][i][lane][e] (pass 0 = the 128-channel layout), and the
+    stack-order bias table [h][24][wm][i][lane][4] = bf16(bias + posb) of pixel
+    jg*16 + (lane & 15) (clamped to 360), channels 128h + wm*64 + i*16 + (lane >> 4)*4 + e —
+    the order weight_refresh writes (CPU check of the index algebra)."""
+    import torch
+    from deep_go_amd.ops import layouts as LY
+    A = torch.arange(256 * 1024, dtype=torch.int64).reshape(256, 1024)
+    f = LY.stack_frag_linear(A, 256).reshape(2, 16, 2, 2, 4, 64, 8)
+    assert torch.equal(f[0].reshape(-1), LY.stack_frag_linear(A[:128]))
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        h, s_, wm, kk, i, lane, e = (int(rng.integers(n)) for n in (2, 16, 2, 2, 4, 64, 8))
+        row = 128 * h + wm * 64 + i * 16 + (lane & 15)
+        col = s_ * 64 + kk * 32 + (lane >> 4) * 8 + e
+        assert f[h, s_, wm, kk, i, lane, e].item() == A[row, col].item()
+    C = 256
+    bias = torch.randn(C)
+    posb = torch.randn(361, C)
+    tab = (posb + bias[None, :]).to(torch.bfloat16)
+    pf = LY.stack_pbias_frag(bias, posb).reshape(2, 24, 2, 4, 64, 4)
+    for _ in range(200):
+        h, jg, wm, i, lane, e = (int(rng.integers(n)) for n in (2, 24, 2, 4, 64, 4))
+        p = min(jg * 16 + (lane & 15), 360)
+        c = 128 * h + wm * 64 + i * 16 + (lane >> 4) * 4 + e
+        assert pf[h, jg, wm, i, lane, e].item() == tab[p, c].item()
+
+
 def test_stack_frag_layout_indexing():
     """layouts.stack_frag puts A[row][col] at the conv_stack2 fragment index (CPU check of the
     permutation the kernel and weight_refresh assume)."""
