@@ -50,6 +50,12 @@ hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X
                                    const int* labels, float* loss, int* pred, void* dZ,
                                    float* gw_part, float* dzb, int head_relu, float grad_scale,
                                    hipStream_t stream);
+hipError_t dg_conv_stack2_fwd_head_x(const long long* table, int nl, void* X0, int B,
+                                     const void* planes, const void* player, const void* rank,
+                                     const float* w, const float* bias, const float* posb,
+                                     const int* labels, float* loss, int* pred, void* dZ,
+                                     float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream);
 hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int M, int Mpad,
                             const void* X, int x_pad, int x_C, int B, void* Y, int y_pad,
                             const float* bias, const float* posb, const void* pbias,
@@ -208,6 +214,19 @@ PYBIND11_MODULE(_dghip, m) {
                                   head_relu, grad_scale, S(stream)),
           "conv_stack2_fwd_head");
   }, "conv_stack2 forward + the fused 3x3/128 policy head");
+  m.def("conv_stack2_fwd_head_x", [](uintptr_t table, int nl, uintptr_t X0, int B,
+                                     uintptr_t planes, uintptr_t player, uintptr_t rank,
+                                     uintptr_t w, uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                     uintptr_t loss, uintptr_t pred, uintptr_t dZ,
+                                     uintptr_t gw_part, uintptr_t dzb, int head_relu,
+                                     float grad_scale, uintptr_t stream) {
+    check(dg_conv_stack2_fwd_head_x(P<long long>(table), nl, P<void>(X0), B, P<void>(planes),
+                                    P<void>(player), P<void>(rank), P<float>(w), P<float>(bias),
+                                    P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
+                                    P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
+                                    grad_scale, S(stream)),
+          "conv_stack2_fwd_head_x");
+  }, "conv_stack2 forward (l1) with the feature expansion fused into its prologue + the head");
   // conv_stack_f8.hip: the fp8 (e4m3, MX MFMA) forward stack of the hidden 128 -> 128 layers
   m.def("conv_stack_f8", [](int C, int epi, uintptr_t table, int nl, uintptr_t X0,
                             uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t stream) {

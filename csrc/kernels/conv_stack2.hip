@@ -40,6 +40,7 @@
 #include <stdlib.h>
 
 #include "dg_common.h"
+#include "dg_features.h"
 #include "head_body.h"
 
 using namespace dg;
@@ -79,6 +80,12 @@ struct StackArgs {
   int nl;
   int fuse_head;        // EPI_FWD: run the policy head on the final image
   int l1;               // EPI_FWD: row 0 is the network's first layer (5x5, 40 -> 128 channels)
+  // l1 with the feature expansion fused (in_planes non-null): the prologue builds the staged
+  // input planes from the packed uint8 batch itself and writes the expanded frame to X0 (the
+  // first layer's weight gradient reads it) instead of gathering X0 written by a launch before
+  const uint8_t* in_planes;   // [B][9][361]
+  const uint8_t* in_player;   // [B]
+  const uint8_t* in_rank;     // [B]
   StackLayer L[MAXL];
   dghead::HeadMArgs head;  // (head_body.h; X unused: the image is resident)
 };
@@ -154,8 +161,34 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   char* sH = smem + SCRATCH;  // image c at sH + c * H_BYTES
 
   // ---- prologue: the first layer's input frame (both 64-channel images) by LDS-DMA ----
-  if (EPI == EPI_FWD && a.l1) {   // (l1: a linear copy of the 23x23x40 frame, whole 1-KB
-                                  // blocks; the last block's tail re-reads the last 16 B)
+  if (EPI == EPI_FWD && a.l1 && a.in_planes) {
+    // fused expansion: every frame pixel's 5 cells (8 channels each) computed here; border
+    // pixels are zero; interior pixels also go to the expanded frame X0 (its border is zero
+    // from allocation and never written).  The same planes as expand_features (dg_features.h).
+    const uint8_t* plb = a.in_planes + (size_t)b * 9 * NPTS;
+    const int pi = a.in_player[b], rk = a.in_rank[b];
+    char* Xw = (char*)a.X0 + (size_t)b * L1_BYTES;
+    for (int f = tid; f < L1F * L1F; f += NT) {
+      const int y = f / L1F, x = f - (f / L1F) * L1F;
+      uint4 cell[5];
+#pragma unroll
+      for (int c8 = 0; c8 < 5; ++c8) cell[c8] = uint4{0u, 0u, 0u, 0u};
+      if (y >= 2 && y < 21 && x >= 2 && x < 21) {
+        float v[40];
+        expand_point(plb + (y - 2) * BOARD + (x - 2), pi, rk, v);
+#pragma unroll
+        for (int c8 = 0; c8 < 5; ++c8) {
+          cell[c8] = uint4{pack_bf16x2(v[8 * c8], v[8 * c8 + 1]), pack_bf16x2(v[8 * c8 + 2], v[8 * c8 + 3]),
+                           pack_bf16x2(v[8 * c8 + 4], v[8 * c8 + 5]), pack_bf16x2(v[8 * c8 + 6], v[8 * c8 + 7])};
+          *(uint4*)(Xw + f * L1XB + c8 * 16) = cell[c8];
+        }
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < 5; ++c8)
+        *(uint4*)(sH + (c8 * L1PS + y * L1RP + x) * 16) = cell[c8];
+    }
+  } else if (EPI == EPI_FWD && a.l1) {   // (l1: a linear copy of the 23x23x40 frame, whole 1-KB
+                                         // blocks; the last block's tail re-reads the last 16 B)
     const char* Xb = a.X0 + (size_t)b * L1_BYTES;
     for (int blk = wave; blk < (L1_CELLS + 63) / 64; blk += NW) {
       // cell -> (chunk, frame row, column); padding cells re-read pixel 0 (never used)
@@ -480,13 +513,19 @@ hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
 int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
 
 hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int l1, int B,
-                         const dghead::HeadMArgs* head, hipStream_t stream) {
+                         const dghead::HeadMArgs* head, hipStream_t stream,
+                         const uint8_t* in_planes = nullptr, const uint8_t* in_player = nullptr,
+                         const uint8_t* in_rank = nullptr) {
   if (nl <= 0 || nl > MAXL || B <= 0) return hipErrorInvalidValue;
   if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
   if (l1 && (epi != EPI_FWD || nl < 2)) return hipErrorInvalidValue;
   static_assert(L1_CELLS * 16 <= 2 * H_BYTES, "l1 frame in the image area");
   StackArgs a;
   a.l1 = l1 ? 1 : 0;
+  if (in_planes && (!l1 || !in_player || !in_rank)) return hipErrorInvalidValue;
+  a.in_planes = in_planes;
+  a.in_player = in_player;
+  a.in_rank = in_rank;
   a.fuse_head = 0;
   a.head = dghead::HeadMArgs{};
   a.X0 = (const char*)X0;
@@ -543,6 +582,20 @@ hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
   return stack2_launch(EPI_FWD, table, nl, X0, l1, B, &h, stream);
+}
+
+// The same with the feature expansion fused into the first layer's prologue (l1 only): the
+// packed batch's planes / player / rank in, the expanded frame X0 written out.
+hipError_t dg_conv_stack2_fwd_head_x(const long long* table, int nl, void* X0, int B,
+                                     const void* planes, const void* player, const void* rank,
+                                     const float* w, const float* bias, const float* posb,
+                                     const int* labels, float* loss, int* pred, void* dZ,
+                                     float* gw_part, float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream) {
+  const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
+                            gw_part, dzb, head_relu, grad_scale};
+  return stack2_launch(EPI_FWD, table, nl, X0, 1, B, &h, stream, (const uint8_t*)planes,
+                       (const uint8_t*)player, (const uint8_t*)rank);
 }
 
 }  // extern "C"

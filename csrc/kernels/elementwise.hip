@@ -2,6 +2,7 @@
 // gradients, fused SGD / RMSProp updates, device-side LR decay and the bf16 weight
 // refresh that re-lays the fp32 OHWI master weights into the two MFMA operand layouts.
 #include "dg_common.h"
+#include "dg_features.h"
 
 using namespace dg;
 
@@ -23,37 +24,8 @@ __global__ void expand_features_kernel(const uint8_t* __restrict__ planes,
   const int b = idx / NPTS;
   const int p = idx - b * NPTS;
   const uint8_t* pl = planes + (size_t)b * 9 * NPTS + p;
-  const int pi = player[b];
-  const int op = 3 - pi;
-  const int stone = pl[0 * NPTS];
-  const int lib = pl[1 * NPTS];
-  const int la = pl[(pi == 1 ? 2 : 3) * NPTS];
-  const int kill = pl[(pi == 1 ? 4 : 5) * NPTS];
-  const int age = pl[6 * NPTS];
-  const int lad = pl[(pi == 1 ? 7 : 8) * NPTS];
-  const int rk = rank[b];
   float v[48];
-#pragma unroll
-  for (int c = 0; c < 48; ++c) v[c] = 0.f;
-  v[0] = stone == 0;
-  v[1] = stone == pi;
-  v[2] = stone == op;
-#pragma unroll
-  for (int i = 1; i <= 3; ++i) v[2 + i] = lib == i;
-  v[6] = lib >= 4;
-  v[7] = (stone == 0) && (la == 0);
-#pragma unroll
-  for (int i = 1; i <= 5; ++i) v[7 + i] = la == i;
-  v[13] = la >= 6;
-#pragma unroll
-  for (int i = 1; i <= 6; ++i) v[13 + i] = kill == i;
-  v[20] = kill >= 7;
-#pragma unroll
-  for (int i = 1; i <= 5; ++i) v[20 + i] = age == i;
-  v[26] = lad >= 1;
-  // v[27] stays 0: the reference's dead plane 28 (RANK + rank, rank in 1..9)
-#pragma unroll
-  for (int r = 1; r <= 9; ++r) v[27 + r] = (rk == r);
+  expand_point(pl, player[b], rank[b], v);
   const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
   char* dst = out + frame_off(b, h, w, pad, CP);
   // optional second frame with CP2 (64) channels for the board-tiled first layer; its

@@ -346,6 +346,9 @@ class HipGoNet:
         self._pre.append((h.expand_features, (
             self.planes.data_ptr(), self.player.data_ptr(), self.rank.data_ptr(),
             self.x0.data_ptr(), self.B, self.plans[0].pad, INPUT_CP)))
+        # the training step's input ops (the expansion moves into the forward stack's launch
+        # when that runs the first layer, below)
+        self._pre_train = self._pre
         for p in self.plans:
             spec = lay.layers[p.index]
             xin = self.x0 if p.index == 0 else self.act[p.index - 1]
@@ -461,11 +464,22 @@ class HipGoNet:
                     AM + 4 * (first - 1), self.B) + fused[1][5:])
                 if self.fp8_wgrad:
                     fused = (h.conv_stack_f8_fwd_head_y8, fused[1] + (self._fwd_y8.ctypes.data,))
+            elif self.stack_l1 and self._stack_x0 is self.x0:
+                # the feature expansion fused into the stack's first-layer prologue: the
+                # launch builds its staged input planes from the packed batch and writes the
+                # expanded frame x0 for the first layer's weight gradient (no expansion launch
+                # and no x0 gather before the stack; evaluation keeps both)
+                fused = (h.conv_stack2_fwd_head_x, (
+                    self._stack_table.ctypes.data, len(self._stack_table), self.x0.data_ptr(),
+                    self.B, self.planes.data_ptr(), self.player.data_ptr(),
+                    self.rank.data_ptr()) + fused[1][5:])
+                self._pre_train = [op for op in self._pre if op[0] is not h.expand_features]
             self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8,
                                               h.conv_stack_f8_y8) else (f, a)
                                for f, a in self._fwd]
-            if any(f in (h.conv_stack2_fwd_head, h.conv_stack_f8_fwd_head,
-                         h.conv_stack_f8_fwd_head_y8) for f, _ in self._fwd_train):
+            if any(f in (h.conv_stack2_fwd_head, h.conv_stack2_fwd_head_x,
+                         h.conv_stack_f8_fwd_head, h.conv_stack_f8_fwd_head_y8)
+                   for f, _ in self._fwd_train):
                 self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
@@ -1003,7 +1017,7 @@ class HipGoNet:
         def sub(op):
             f, a = op
             return (f, tuple(m.get(x, x) if type(x) is int else x for x in a))
-        names = ("_pre", "_fwd", "_fwd_train")
+        names = ("_pre", "_pre_train", "_fwd", "_fwd_train")
         ops0 = {n: list(getattr(self, n)) for n in names}
         ops0["_head_train"] = self._head_train
         ops0["_head_eval"] = self._head_eval
@@ -1088,7 +1102,7 @@ class HipGoNet:
         s = stream_handle()
         # (no gradient zeroing: every gradient entry is written — not accumulated — by the
         # slab reduces and the deterministic head reduce)
-        self._run(self._pre, s)
+        self._run(self._pre_train, s)
         self._run(self._fwd_train, s)
         self._run([self._head_train], s)
         self.head_reduce()
@@ -1332,7 +1346,7 @@ class SegmentedStep:
         def emit(fn):
             cur.append(fn)
 
-        emit(lambda: net._run(net._pre, stream_handle()))
+        emit(lambda: net._run(net._pre_train, stream_handle()))
         emit(lambda: net._run(net._fwd_train, stream_handle()))
         emit(lambda: net._run([net._head_train], stream_handle()))
         emit(net.head_reduce)

@@ -420,16 +420,22 @@ def test_first_layer_frag_kernel_d256(monkeypatch):
 @pytest.mark.parametrize("layers", [4, 7])
 def test_head_fused_into_forward_stack(layers, monkeypatch):
     """The policy head run inside the forward stack's launch (on the resident board image)
-    gives the standalone MFMA head's loss, predictions, dZ and gradients bit for bit."""
+    gives the standalone MFMA head's loss, predictions, dZ and gradients bit for bit.  With
+    the first layer in the stack, the feature expansion runs in the same launch's prologue
+    (conv_stack2_fwd_head_x): no expansion launch in the training step, the same expanded
+    frame x0 (which the first layer's weight gradient reads)."""
     monkeypatch.setenv("DG_FUSE_HEAD", "0")
     _, n0, _ = _setup(layers, 128, 5, seed=12)
     monkeypatch.setenv("DG_FUSE_HEAD", "1")
     _, n1, _ = _setup(layers, 128, 5, seed=12)
     assert n0._fwd_train is n0._fwd
-    assert any(f is n1.h.conv_stack2_fwd_head for f, _ in n1._fwd_train)
+    assert any(f is n1.h.conv_stack2_fwd_head_x for f, _ in n1._fwd_train)
+    assert not any(f is n1.h.expand_features for f, _ in n1._pre_train)
+    assert any(f is n1.h.expand_features for f, _ in n1._pre)   # (evaluation keeps it)
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
+    assert torch.equal(n0.x0, n1.x0)
     assert torch.equal(n0.loss, n1.loss) and torch.equal(n0.pred, n1.pred)
     assert torch.equal(n0.dz[-1], n1.dz[-1])
     assert torch.equal(n0.grads, n1.grads)
