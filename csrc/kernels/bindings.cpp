@@ -71,8 +71,9 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
 int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
 void dg_conv_l1_set_nw(int nw);
 int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad);
-hipError_t dg_conv_l1_frag(const void* A, const void* pbias, const void* X, int B, int M,
-                           void* Y, void* mask, hipStream_t stream);
+hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
+                           void* Y, void* mask, const void* planes, const void* player,
+                           const void* rank, hipStream_t stream);
 hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void* X, int x_pad,
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
                       void* mask, const void* pbias, hipStream_t stream);
@@ -473,12 +474,14 @@ PYBIND11_MODULE(_dghip, m) {
     return dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP);
   });
   m.def("conv_l1_frag", [](uintptr_t A, uintptr_t pbias, uintptr_t X, int B, int M, uintptr_t Y,
-                           uintptr_t mask, uintptr_t stream) {
+                           uintptr_t mask, uintptr_t planes, uintptr_t player, uintptr_t rank,
+                           uintptr_t stream) {
     check(dg_conv_l1_frag(P<void>(A), P<void>(pbias), P<void>(X), B, M, P<void>(Y), P<void>(mask),
-                          S(stream)),
+                          P<void>(planes), P<void>(player), P<void>(rank), S(stream)),
           "conv_l1_frag");
   }, "5x5 / 40-channel first layer, one board per workgroup, fragment-ordered weights "
-     "(conv_l1.hip conv_l1_frag_kernel)");
+     "(conv_l1.hip conv_l1_frag_kernel); planes/player/rank non-zero: the feature expansion "
+     "fused in (X written)");
   m.def("conv_l1_frag_ok", [](int kw, int x_pad, int x_C, int M, int y_pad) {
     return dg_conv_l1_frag_ok(kw, x_pad, x_C, M, y_pad);
   });

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include "dg_common.h"
+#include "dg_features.h"
 
 using namespace dg;
 
@@ -230,10 +231,15 @@ constexpr int PF_LDS = (PF_CELLS + 63) / 64 * 1024;   // whole 1-KB DMA blocks (
 struct L1FragArgs {
   const char* A;          // fragment-ordered weights, nh passes of 16 x 16 KB
   const uint2* pbias;     // stack-order bf16 (bias + pos-bias): [h][24][2][4][64] x 4 bf16
-  const char* X;          // input frame [B][23][23][40] bf16
+  char* X;                // input frame [B][23][23][40] bf16 (written when in_planes is set)
   char* Y;                // output frame [B][21][21][M] bf16 (interior written)
   uint8_t* mask;          // optional ReLU bits [B][361][M/8]
   int M, nh;
+  // optional: the feature expansion fused into the prologue — the staged planes are built from
+  // the packed uint8 batch and the expanded frame X is written for the layer's weight gradient
+  const uint8_t* in_planes;   // [B][9][361]
+  const uint8_t* in_player;   // [B]
+  const uint8_t* in_rank;     // [B]
 };
 
 __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
@@ -244,8 +250,33 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
   const int wm = wave >> 2, wn = wave & 3;
   const int b = blockIdx.x;
 
-  // gather: cell -> (chunk, frame row, column); padding cells re-read pixel 0 (never used)
-  {
+  if (a.in_planes) {
+    // fused expansion (dg_features.h, as expand_features): border pixels zero, interior
+    // pixels also written to the expanded frame X (its border is zero from allocation)
+    const uint8_t* plb = a.in_planes + (size_t)b * 9 * NPTS;
+    const int pi = a.in_player[b], rk = a.in_rank[b];
+    char* Xw = a.X + (size_t)b * PF_BYTES;
+    for (int f = tid; f < PF_F * PF_F; f += 512) {
+      const int y = f / PF_F, x = f - (f / PF_F) * PF_F;
+      uint4 cell[5];
+#pragma unroll
+      for (int c8 = 0; c8 < 5; ++c8) cell[c8] = uint4{0u, 0u, 0u, 0u};
+      if (y >= 2 && y < 21 && x >= 2 && x < 21) {
+        float v[40];
+        expand_point(plb + (y - 2) * BOARD + (x - 2), pi, rk, v);
+#pragma unroll
+        for (int c8 = 0; c8 < 5; ++c8) {
+          cell[c8] = uint4{pack_bf16x2(v[8 * c8], v[8 * c8 + 1]), pack_bf16x2(v[8 * c8 + 2], v[8 * c8 + 3]),
+                           pack_bf16x2(v[8 * c8 + 4], v[8 * c8 + 5]), pack_bf16x2(v[8 * c8 + 6], v[8 * c8 + 7])};
+          *(uint4*)(Xw + f * PF_XB + c8 * 16) = cell[c8];
+        }
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < 5; ++c8)
+        *(uint4*)(smem + (c8 * PF_PS + y * PF_RP + x) * 16) = cell[c8];
+    }
+  } else {
+    // gather: cell -> (chunk, frame row, column); padding cells re-read pixel 0 (never used)
     const char* Xb = a.X + (size_t)b * PF_BYTES;
     for (int blk = wave; blk < PF_LDS / 1024; blk += 8) {
       const int cell = blk * 64 + lane;
@@ -392,8 +423,10 @@ int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad) {
   return kw == 5 && x_pad == 2 && x_C == 40 && M % 128 == 0 && M <= 512 && y_pad == 1;
 }
 
-hipError_t dg_conv_l1_frag(const void* A, const void* pbias, const void* X, int B, int M,
-                           void* Y, void* mask, hipStream_t stream) {
+hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
+                           void* Y, void* mask, const void* planes, const void* player,
+                           const void* rank, hipStream_t stream) {
+  if (planes && (!player || !rank)) return hipErrorInvalidValue;
   if (!A || !pbias || !X || !Y || B <= 0 || M % 128 != 0 || M > 512)
     return hipErrorInvalidValue;
   static bool done = false;
@@ -402,8 +435,8 @@ hipError_t dg_conv_l1_frag(const void* A, const void* pbias, const void* X, int 
                               hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
     done = true;
   }
-  L1FragArgs a{(const char*)A, (const uint2*)pbias, (const char*)X, (char*)Y,
-               (uint8_t*)mask, M, M / 128};
+  L1FragArgs a{(const char*)A, (const uint2*)pbias, (char*)X, (char*)Y, (uint8_t*)mask, M,
+               M / 128, (const uint8_t*)planes, (const uint8_t*)player, (const uint8_t*)rank};
   hipLaunchKernelGGL(conv_l1_frag_kernel, dim3(B), dim3(512), PF_LDS, stream, a);
   return hipGetLastError();
 }

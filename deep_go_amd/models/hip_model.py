@@ -386,11 +386,14 @@ class HipGoNet:
                 # first layer on conv_l1_frag (conv_l1.hip): one board per workgroup, the
                 # input frame gathered once into a conflict-free plane layout, fragment-ordered
                 # weights streamed into VGPRs (when the forward stack does not absorb it)
+                # (the feature expansion fused into its prologue: it writes x0 itself, so the
+                # separate expansion launch leaves _pre)
                 msk = self.relu_mask[0]
                 self._fwd.append((h.conv_l1_frag, (
                     self.wfrag[0].data_ptr(), self.pbias_frag[0].data_ptr(), xin.data_ptr(),
                     self.B, p.cout, self.act[0].data_ptr(),
-                    msk.data_ptr() if msk is not None else 0)))
+                    msk.data_ptr() if msk is not None else 0, self.planes.data_ptr(),
+                    self.player.data_ptr(), self.rank.data_ptr())))
             elif self._l1_res_ok(p):
                 # first layer board-resident (conv_l1.hip): the 23x23x40 input frame staged
                 # once per board instead of a 5x5x40 im2col patch per pixel and tile
@@ -421,6 +424,11 @@ class HipGoNet:
         self._fuse_forward_stack()
         self._l2_tables = []
         self._fwd, self._fwd_owner = self._merge_layer2_runs(self._fwd, self._fwd_owner)
+        if any(f is h.conv_l1_frag for f, _ in self._fwd):
+            # conv_l1_frag (still in the list: the forward stack did not absorb the first
+            # layer) expands the features itself and writes x0: no expansion launch
+            self._pre = [op for op in self._pre if op[0] is not h.expand_features]
+            self._pre_train = self._pre
         hd = self.head
         hx = self.act[-1]
         self._head_train = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,

@@ -86,7 +86,7 @@ def conv_l1_frag(x: torch.Tensor, w: torch.Tensor, bias, posb):
     pbf = LY.stack_pbias_frag(bias.to(dev), posb.to(dev))
     mask = torch.zeros(B, NPTS, cout // 8, dtype=torch.uint8, device=dev)
     h.conv_l1_frag(A.data_ptr(), pbf.data_ptr(), xf.data_ptr(), B, cout, yf.data_ptr(),
-                   mask.data_ptr(), stream_handle())
+                   mask.data_ptr(), 0, 0, 0, stream_handle())
     return LY.from_frame(yf, 1, cout), mask
 
 

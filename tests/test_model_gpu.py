@@ -408,9 +408,12 @@ def test_first_layer_frag_kernel_d256(monkeypatch):
     assert any(f is n1.h.conv_l1_frag for f, _ in n1._fwd_train)
     assert any(f is n0.h.conv_l1 for f, _ in n0._fwd_train)
     assert torch.equal(n1.wfrag[0], LY.stack_frag_linear(n1.wf[0], 256))
+    # (conv_l1_frag also runs the feature expansion in its prologue: no expansion launch)
+    assert not any(f is n1.h.expand_features for f, _ in n1._pre)
     n0.forward_backward()
     n1.forward_backward()
     torch.cuda.synchronize()
+    assert torch.equal(n0.x0, n1.x0)
     assert torch.equal(n0.act[0], n1.act[0])
     assert torch.equal(n0.relu_mask[0], n1.relu_mask[0])
     assert torch.equal(n0.loss, n1.loss)
