@@ -1,6 +1,6 @@
 """Timeline of ONE training step from a rocprofv3 --kernel-trace CSV of bench.py in hipGraph
-mode: every kernel of the second-to-last complete step (steps delimited by
-expand_features launches) with its start offset, duration and queue, plus the busy time
+mode: every kernel of the second-to-last complete step (steps delimited by the
+feature expansion launch, or by the first layer's kernel where the expansion is fused into it) with its start offset, duration and queue, plus the busy time
 of the union of all kernels (so side-stream overlap is visible).
 Usage: python tools/step_timeline.py TRACE.csv"""
 import csv
@@ -16,7 +16,11 @@ def short(s):
 
 def main(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "expand_features" in r["Kernel_Name"]]
+    # a step's first launch: the feature expansion, or (fused into it) the first layer's kernel
+    for mark in ("expand_features", "conv_l1_frag_kernel", "conv_stack2_kernel<1"):
+        starts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
+        if len(starts) >= 3:
+            break
     a, b = starts[-3], starts[-2]
     seg = rows[a:b]
     t0 = int(seg[0]["Start_Timestamp"])
