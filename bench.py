@@ -35,10 +35,16 @@ After the headline timing (never inside it) the same process measures:
     same network's step without collectives, and from those the exposed communication time
     and the fraction of it hidden behind compute.
 
-Multi-rank safety: every rank arms a phase guard (``utils/faults.PhaseGuard``: comm set-up,
-capture, warmup, timed, report; exit 42 and a status file on expiry) and the launcher bounds
-the whole child run.  If the native in-graph communicator (``--comm auto``) hangs, the
-launcher re-runs ONCE with ``--comm torch`` and says so in the JSON (``comm_fallback``).
+Multi-rank safety: every rank arms a phase guard (``utils/faults.PhaseGuard``) before the
+process-group rendezvous.  Each phase has its own deadline: ``init`` / ``comm`` / ``capture``
+(--comm-timeout, 90 s), ``warmup`` / ``timed`` / ``report`` and each secondary config's
+capture / warmup / timed (--phase-timeout, 60 s); on expiry the rank writes
+``hang:<phase>:<communicator kind>`` to its status file and exits 42.  Under the driver's
+own ``torch.distributed.run`` that bounds a hung rank to ~90 s.  Through this file's launcher
+(``--gpus N`` without WORLD_SIZE) the whole job is bounded by --launch-budget (540 s): when a
+guard fired on a rank that was on the native in-graph communicator in a phase that issues
+its collectives, the launcher re-runs ONCE with ``--comm torch`` inside the remaining budget
+and says so in the JSON (``comm_fallback``); any other failure is reported as it is.
 
 ``--cpu-dry-run``: the same launcher / rank / timing / JSON path on the CPU over gloo with
 the fp32 oracle at BASELINE config 1 size (tests/test_bench_launcher.py drives it at N=2, 4).
@@ -112,9 +118,19 @@ def parse(argv=None):
                          "the GPU leaves its idle clock state over the first ~25 ms of load, so "
                          "without it a 20-step (20 ms) timed window measures the DVFS ramp "
                          "(20/5 steps: 0.97 ms/step, 200/50: 0.90 on the same box)")
-    ap.add_argument("--phase-timeout", type=float, default=300.0,
-                    help="N > 1: per-rank limit of each phase (comm set-up, capture, warmup, "
-                         "timed, report) in seconds")
+    ap.add_argument("--comm-timeout", type=float, default=90.0,
+                    help="N > 1: per-rank limit (s) of the process-group init, the communicator "
+                         "set-up and the headline's capture phase (each)")
+    ap.add_argument("--phase-timeout", type=float, default=60.0,
+                    help="N > 1: per-rank limit (s) of every other phase: the headline's warmup, "
+                         "timed and report phases, and each secondary config's capture, warmup "
+                         "and timed phases (each has its own deadline)")
+    ap.add_argument("--launch-budget", type=float, default=540.0,
+                    help="N > 1 launcher (no WORLD_SIZE in the environment): wall-clock bound "
+                         "of the whole job including one --comm torch fallback run.  The first "
+                         "run may use the budget minus a 150-s reserve; if a rank's guard "
+                         "reports a hang while it was on the native communicator, the "
+                         "fallback run gets what is left.  Worst case: %(default)s s")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/timing/JSON path on CPU over gloo (BASELINE config 1 "
                          "model); no GPU")
@@ -166,6 +182,7 @@ def _run_ranks(args, argv, status_dir, limit_s):
 
 
 def _hangs(status_dir):
+    """{rank file: (phase, comm kind)} of every rank whose phase guard fired."""
     out = {}
     for f in sorted(os.listdir(status_dir)):
         try:
@@ -173,27 +190,46 @@ def _hangs(status_dir):
         except OSError:
             continue
         if txt.startswith("hang:"):
-            out[f] = txt[5:]
+            parts = txt.split(":")
+            out[f] = (parts[1], parts[2] if len(parts) > 2 else "")
     return out
+
+
+# phases in which a rank issues collectives through the chosen communicator (the process-group
+# init comes before any choice)
+_COMM_PHASES = ("comm", "capture", "warmup", "timed", "report")
+
+
+def _native_hang(hangs) -> bool:
+    """A guard fired while its rank was on (or setting up) the native communicator, in a phase
+    that issues its collectives: the case a --comm torch re-run can cure."""
+    return any(kind == "native" and (ph in _COMM_PHASES or ph.startswith("sec-"))
+               for ph, kind in hangs.values())
 
 
 def launch(args, argv) -> int:
     """Parent of an N-rank run: torch.distributed.run as a child process (never exec: the
     parent must not replace itself, and it touches no GPU), relay rank 0's JSON line.
-    If a rank's phase guard reports a hang while the native communicator was in use
-    (--comm auto), re-run once with torch.distributed collectives."""
-    limit = 6 * args.phase_timeout + 120
+    If a rank's phase guard reports a hang while that rank was on the native communicator
+    (--comm auto), re-run once with torch.distributed collectives.  The whole job is bounded
+    by --launch-budget: the first run by the budget minus a 150-s reserve, the fallback by
+    what is left."""
+    t_start = time.monotonic()
+    budget = max(60.0, args.launch_budget)
+    reserve = min(150.0, budget / 3)
     status_dir = tempfile.mkdtemp(prefix="dg_bench_")
     fallback = None
+    hangs = {}
     try:
-        rc, lines = _run_ranks(args, argv, status_dir, limit)
+        rc, lines = _run_ranks(args, argv, status_dir, budget - reserve)
         hangs = _hangs(status_dir)
-        if (rc != 0 and hangs and args.comm == "auto" and not args.cpu_dry_run):
+        left = budget - (time.monotonic() - t_start)
+        if (rc != 0 and args.comm == "auto" and _native_hang(hangs) and left > 30):
             fallback = f"native communicator run hung ({hangs}); re-run with --comm torch"
             sys.stderr.write(f"bench: {fallback}\n")
             for f in os.listdir(status_dir):
                 os.remove(os.path.join(status_dir, f))
-            rc, lines = _run_ranks(args, argv + ["--comm", "torch"], status_dir, limit)
+            rc, lines = _run_ranks(args, argv + ["--comm", "torch"], status_dir, left)
             hangs = _hangs(status_dir)
     finally:
         shutil.rmtree(status_dir, ignore_errors=True)
@@ -265,21 +301,31 @@ class _NoGuard:
     def phase(self, *_):
         pass
 
+    def set_comm(self, *_):
+        pass
+
     def stop(self):
         pass
 
 
-def _guard(rank, world, args):
+def _guard(args):
+    """The rank's phase guard, armed BEFORE torch.distributed's rendezvous (rank / world from
+    the environment torch.distributed.run sets)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return _NoGuard()
     from deep_go_amd.utils.faults import PhaseGuard
-    return PhaseGuard(rank, os.environ.get("DG_BENCH_STATUS_DIR"))
+    return PhaseGuard(int(os.environ.get("RANK", "0")), os.environ.get("DG_BENCH_STATUS_DIR"))
 
 
-def _test_hang(rank, phase):
-    """Test hook (tests/test_bench_launcher.py): DG_BENCH_HANG=RANK:PHASE sleeps there."""
+def _test_hang(rank, phase, comm=""):
+    """Test hook (tests/test_bench_launcher.py): DG_BENCH_HANG=RANK:PHASE[:COMM] sleeps there
+    (with COMM: only while this rank is on that communicator kind)."""
     spec = os.environ.get("DG_BENCH_HANG", "")
-    if spec and spec == f"{rank}:{phase}":
+    if not spec:
+        return
+    parts = spec.split(":")
+    if parts[:2] == [str(rank), phase] and (len(parts) < 3 or parts[2] == comm):
         time.sleep(3600)
 
 
@@ -292,13 +338,23 @@ def run_cpu_dry(args) -> int:
     from deep_go_amd.data.synthetic import random_planes
     from deep_go_amd.parallel import dp
     from deep_go_amd.train.backends import CPUBackend
+    guard = _guard(args)
+    guard.phase("init", args.comm_timeout)
     info = dp.init_distributed(backend="gloo")
     world = info.world
     if os.environ.get("DG_BENCH_FAIL_RANK") == str(info.rank):   # launcher test hook
         raise SystemExit(f"rank {info.rank}: injected failure")
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
-    guard = _guard(info.rank, world, args)
+    # communicator set-up.  There is no RCCL on the CPU: --comm auto / native rehearses the
+    # native communicator's set-up phase (the guard reports the rank as on "native" while a
+    # gloo barrier stands in for ncclCommInitRank), so the launcher's hang -> --comm torch
+    # fallback path runs here; the collectives themselves are gloo's either way
+    kind = "native" if args.comm in ("auto", "native") else "torch"
+    guard.phase("comm", args.comm_timeout)
+    guard.set_comm(kind)
+    _test_hang(info.rank, "comm", kind)
+    dp.barrier()
     torch.set_num_threads(1)
     cfg = get_preset("cpu-1layer-k16", batchSize=args.batch * world, seed=1234)
     be = CPUBackend(cfg, args.batch, world=world)
@@ -323,7 +379,8 @@ def run_cpu_dry(args) -> int:
     if info.rank == 0:
         args.layers, args.channels = cfg.numLayers, cfg.channelSize
         rec = _record(args, world, elapsed_all, cfg.train_flops_per_board(),
-                      {"dry_run": "cpu-gloo", "dtype": "fp32"})
+                      {"dry_run": "cpu-gloo", "dtype": "fp32",
+                       "comm": f"gloo ({kind} set-up rehearsed)"})
         rec["config"]["model"] = "cpu-1layer-k16 (BASELINE config 1; dry run, not a GPU number)"
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
@@ -433,12 +490,16 @@ def _dp_report(case, comm, world, dev, args, step_ms) -> dict:
         rep["proxy"] = {"world": comm.proxy_world, "gbps": comm.gbps, "blocks": comm.blocks}
     devs = {"rank": dp.env_info().rank, "device": dev.index,
             "pci_bus_id": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None)}
+    # what the communicator itself reports (RCCL's rank count / rank / device for native)
+    devs.update({f"comm_{k}": v for k, v in comm.seen().items()})
     if world > 1:
         allv = [None] * world
         torch.distributed.all_gather_object(allv, devs)
         rep["devices"] = allv
+        rep["ranks_seen"] = sorted({d.get("comm_ranks_seen") for d in allv}, key=str)
     else:
         rep["devices"] = [devs]
+        rep["ranks_seen"] = [devs.get("comm_ranks_seen")]
     # (a) the bucket collectives alone, back to back on the comm stream (same count on every
     # rank): us per step and the ring bus bandwidth 2(n-1)/n * bytes / time
     reps = 20
@@ -490,17 +551,20 @@ def run_gpu(args) -> int:
     ndev = torch.cuda.device_count()
     if world_env > ndev:
         raise SystemExit(f"WORLD_SIZE={world_env} > {ndev} visible GPUs")
+    guard = _guard(args)
+    guard.phase("init", args.comm_timeout)
     info = dp.init_distributed()
     world = info.world
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
-    guard = _guard(info.rank, world, args)
     dev = torch.device("cuda", info.local_rank if world > 1 else 0)
     torch.cuda.set_device(dev)
     use_dp = world > 1 or args.force_dp
     comm = None
-    guard.phase("comm", args.phase_timeout)
-    _test_hang(info.rank, "comm")
+    extra_comm = {}
+    guard.phase("comm", args.comm_timeout)
+    guard.set_comm("native" if args.comm in ("auto", "native") else args.comm)
+    _test_hang(info.rank, "comm", "native" if args.comm in ("auto", "native") else args.comm)
     if use_dp and world == 1 and args.comm == "torch" and not torch.distributed.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
@@ -508,16 +572,22 @@ def run_gpu(args) -> int:
     if use_dp:
         comm = dp.make_communicator(args.comm, dev, world=args.proxy_world,
                                     gbps=args.proxy_gbps, blocks=args.proxy_blocks)
+        guard.set_comm(comm.kind)
+        extra_comm = {"comm_seen": comm.seen()}
         if comm.world != world:
             raise SystemExit(f"communicator world {comm.world} != {world}")
+        seen = comm.seen()
+        if world > 1 and seen.get("ranks_seen", world) != world:
+            raise SystemExit(f"rank {info.rank}: the communicator reports "
+                             f"{seen.get('ranks_seen')} ranks, WORLD_SIZE is {world}")
 
-    guard.phase("capture", args.phase_timeout)
+    guard.phase("capture", args.comm_timeout)
     case = _Case(args, args.channels, args.dtype, world, info, dev, comm, use_dp)
     guard.phase("warmup", args.phase_timeout)
     case.run(args.spinup_steps)     # untimed: clock ramp (see --help)
     case.run(args.warmup)
     guard.phase("timed", args.phase_timeout)
-    _test_hang(info.rank, "timed")
+    _test_hang(info.rank, "timed", comm.kind if comm is not None else "")
     elapsed_all = case.timed(args.steps, dev)
     guard.phase("report", args.phase_timeout)
     phases = None
@@ -545,6 +615,7 @@ def run_gpu(args) -> int:
         extra["comm"] = comm.kind
         extra["ranks_params_identical"] = consistent
         extra["grad_dtype"] = args.grad_dtype
+        extra.update(extra_comm)
         if not args.no_report:
             extra["dp"] = _dp_report(case, comm, world, dev, args, step_ms)
     if phases:
@@ -560,9 +631,13 @@ def run_gpu(args) -> int:
         ch, dt = item.split(":")
         if int(ch) == args.channels and dt == args.dtype:
             continue
+        tag = item.replace(":", "-")     # (the status file is colon-separated)
+        guard.phase(f"sec-{tag}-capture", args.phase_timeout)
         c2 = _Case(args, int(ch), dt, world, info, dev, comm, use_dp)
+        guard.phase(f"sec-{tag}-warmup", args.phase_timeout)
         c2.run(100)
         c2.run(args.warmup)
+        guard.phase(f"sec-{tag}-timed", args.phase_timeout)
         t = c2.timed(args.steps, dev)
         ok = c2.params_identical(world)
         if not ok:

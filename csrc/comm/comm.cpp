@@ -125,6 +125,26 @@ class Comm {
   }
   int world() const { return world_; }
   int rank() const { return rank_; }
+  // what the communicator itself reports (ncclCommCount / UserRank / CuDevice): the
+  // bench's "ranks_seen", checked against WORLD_SIZE
+  int count() const {
+    live();
+    int n = 0;
+    check(ncclCommCount(comm_, &n), "ncclCommCount");
+    return n;
+  }
+  int user_rank() const {
+    live();
+    int r = -1;
+    check(ncclCommUserRank(comm_, &r), "ncclCommUserRank");
+    return r;
+  }
+  int device() const {
+    live();
+    int d = -1;
+    check(ncclCommCuDevice(comm_, &d), "ncclCommCuDevice");
+    return d;
+  }
 
  private:
   void live() const {
@@ -162,6 +182,9 @@ PYBIND11_MODULE(_dgcomm, m) {
       .def("async_error", &Comm::async_error)
       .def("abort", &Comm::abort)
       .def("destroy", &Comm::destroy)
+      .def("count", &Comm::count)
+      .def("user_rank", &Comm::user_rank)
+      .def("device", &Comm::device)
       .def_property_readonly("world", &Comm::world)
       .def_property_readonly("rank", &Comm::rank);
 }

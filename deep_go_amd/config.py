@@ -95,11 +95,16 @@ class ExperimentConfig:
         return n
 
     def train_flops_per_board(self) -> float:
-        """2*MACs over 361 output points per layer, train ~= 3x forward."""
+        """Useful training FLOPs per board: 2*MACs over 361 output points per layer for the
+        forward, the weight gradient and the input gradient — except the FIRST layer's input
+        gradient, which nothing needs and the step never computes (BASELINE.md's "train ~=
+        3x forward" counted it: +2.5% at 12x128, +1.3% at 12x256).  Real channel counts (37
+        input planes, not the 40 the kernels pad to)."""
         f = 0.0
-        for cin, cout, k in self.layer_specs():
-            f += 2.0 * cout * cin * k * k * NUM_POINTS
-        return 3.0 * f
+        for i, (cin, cout, k) in enumerate(self.layer_specs()):
+            fwd = 2.0 * cout * cin * k * k * NUM_POINTS
+            f += fwd * (2.0 if i == 0 else 3.0)
+        return f
 
     def replace(self, **kw) -> "ExperimentConfig":
         return override(self, kw)

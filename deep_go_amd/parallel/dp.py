@@ -127,6 +127,9 @@ class TorchComm:
             dist.broadcast(t, root, group=self.group)
         return t
 
+    def seen(self) -> dict:
+        return {"ranks_seen": self.world, "user_rank": self.rank}
+
     def async_error(self) -> str:
         return ""
 
@@ -197,6 +200,15 @@ class NativeComm:
             cur.wait_stream(self.stream)
         return t
 
+    def seen(self) -> dict:
+        """What the RCCL communicator itself reports (ncclCommCount / UserRank / CuDevice),
+        independent of the environment this rank was started with."""
+        try:
+            return {"ranks_seen": int(self.c.count()), "user_rank": int(self.c.user_rank()),
+                    "device": int(self.c.device())}
+        except (AttributeError, RuntimeError) as e:   # an older _dgcomm build / aborted comm
+            return {"error": str(e)}
+
     def async_error(self) -> str:
         return self.c.async_error()
 
@@ -236,6 +248,9 @@ class ProxyComm:
 
     def broadcast_(self, t: torch.Tensor, root: int = 0):
         return t
+
+    def seen(self) -> dict:
+        return {"ranks_seen": 1, "user_rank": 0, "proxy_world": self.proxy_world}
 
     def async_error(self) -> str:
         return ""

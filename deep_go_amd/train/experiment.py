@@ -178,75 +178,79 @@ class Experiment:
         n_log = 0
         last_val = None
         save_now = False
-        for _ in range(iters):
-            with trace.range("load_batch"):
-                batch = be.load_next(loader)
-            self.loader_seq = loader.consumed
-            step = self.iterations + 1
-            # nothing reads the pre-update state this iteration (no validation, no host NaN
-            # check before the update): forward/backward + update as one fused step
-            fused = (step % cfg.validation_interval != 0 and cfg.nan_policy != "raise"
-                     and not fault)
-            # the rate this iteration's update uses, read before the step so fused and unfused
-            # iterations log the same thing (only on logging iterations: it syncs the device)
-            lr_now = (be.rate if step % cfg.log_interval == 0
-                      or step % cfg.validation_interval == 0 else None)
-            with trace.range("fwd_bwd"):
-                if fused:
-                    be.train_step()
-                else:
-                    be.forward_backward()
-            inj = maybe_inject(info.rank, step, fault) if fault else None
-            need_cost = (step % cfg.log_interval == 0) or (step % cfg.validation_interval == 0) \
-                or ema is None or cfg.nan_policy == "raise"
-            if need_cost:
-                loss = be.loss_sum() / self.local_batch
-                if inj == "nan":
-                    loss = float("nan")
-                if batch is None and not np.isfinite(loss):
-                    batch = be.current_batch()  # only for the bad-batch dump
-                if not check_finite(loss, step, cfg.nan_policy, batch, cfg.checkpoint_dir):
-                    loss = ema if ema is not None else 0.0
-                ema = loss if ema is None else 0.95 * ema + 0.05 * loss
-            self.iterations = step
-            n_log += 1
-            if step % cfg.validation_interval == 0:
-                with trace.range("validation"):
-                    vc, va = self.eval_batch_set(val)
-                last_val = vc
-                self.validation_costs.append(vc)
-                self.validation_accuracies.append(va)
-                self.metrics.line(f"validation at iteration {step}: cost={vc}, accuracy={va}")
-                self.metrics.record(kind="validation", step=step, val_cost=vc, val_acc=va,
-                                    lr=lr_now)
-                # the reference saves here, BEFORE this iteration's update (train.lua:124):
-                # that checkpoint pairs iteration N with N-1 updates.  We save after the
-                # update below so a resumed run continues bit-exactly (auto-resume).
-                save_now = info.is_main
-            if step % cfg.log_interval == 0:
-                now = time.perf_counter()
-                bps = n_log * cfg.batchSize / max(now - t_log, 1e-9)
-                self.train_costs.append(ema)
-                if step % cfg.validation_interval != 0:
-                    self.metrics.line(f"training {ema} (samples per second {bps:.1f})")
-                self.metrics.record(kind="train", step=step, loss_ema=ema, boards_per_sec=bps,
-                                    lr=lr_now)
-                t_log, n_log = now, 0
-            if not fused:
-                with trace.range("optimizer"):
-                    be.optimizer_step()
-            if save_now:
-                with trace.range("checkpoint"):
-                    self.save()
-                save_now = False
+        try:
+            for _ in range(iters):
+                with trace.range("load_batch"):
+                    batch = be.load_next(loader)
+                self.loader_seq = loader.consumed
+                step = self.iterations + 1
+                # nothing reads the pre-update state this iteration (no validation, no host NaN
+                # check before the update): forward/backward + update as one fused step
+                fused = (step % cfg.validation_interval != 0 and cfg.nan_policy != "raise"
+                         and not fault)
+                # the rate this iteration's update uses, read before the step so fused and unfused
+                # iterations log the same thing (only on logging iterations: it syncs the device)
+                lr_now = (be.rate if step % cfg.log_interval == 0
+                          or step % cfg.validation_interval == 0 else None)
+                with trace.range("fwd_bwd"):
+                    if fused:
+                        be.train_step()
+                    else:
+                        be.forward_backward()
+                inj = maybe_inject(info.rank, step, fault) if fault else None
+                need_cost = (step % cfg.log_interval == 0) or (step % cfg.validation_interval == 0) \
+                    or ema is None or cfg.nan_policy == "raise"
+                if need_cost:
+                    loss = be.loss_sum() / self.local_batch
+                    if inj == "nan":
+                        loss = float("nan")
+                    if batch is None and not np.isfinite(loss):
+                        batch = be.current_batch()  # only for the bad-batch dump
+                    if not check_finite(loss, step, cfg.nan_policy, batch, cfg.checkpoint_dir):
+                        loss = ema if ema is not None else 0.0
+                    ema = loss if ema is None else 0.95 * ema + 0.05 * loss
+                self.iterations = step
+                n_log += 1
+                if step % cfg.validation_interval == 0:
+                    with trace.range("validation"):
+                        vc, va = self.eval_batch_set(val)
+                    last_val = vc
+                    self.validation_costs.append(vc)
+                    self.validation_accuracies.append(va)
+                    self.metrics.line(f"validation at iteration {step}: cost={vc}, accuracy={va}")
+                    self.metrics.record(kind="validation", step=step, val_cost=vc, val_acc=va,
+                                        lr=lr_now)
+                    # the reference saves here, BEFORE this iteration's update (train.lua:124):
+                    # that checkpoint pairs iteration N with N-1 updates.  We save after the
+                    # update below so a resumed run continues bit-exactly (auto-resume).
+                    save_now = info.is_main
+                if step % cfg.log_interval == 0:
+                    now = time.perf_counter()
+                    bps = n_log * cfg.batchSize / max(now - t_log, 1e-9)
+                    self.train_costs.append(ema)
+                    if step % cfg.validation_interval != 0:
+                        self.metrics.line(f"training {ema} (samples per second {bps:.1f})")
+                    self.metrics.record(kind="train", step=step, loss_ema=ema, boards_per_sec=bps,
+                                        lr=lr_now)
+                    t_log, n_log = now, 0
+                if not fused:
+                    with trace.range("optimizer"):
+                        be.optimizer_step()
+                if save_now:
+                    with trace.range("checkpoint"):
+                        self.save()
+                    save_now = False
+                if watchdog:
+                    watchdog.beat()
+            if torch.cuda.is_available() and self._device_kind() == "hip":
+                torch.cuda.synchronize()
+            total = time.perf_counter() - t_start
+        finally:
+            # also when the loop raises (NonFiniteLoss, a loader error): a live watchdog would
+            # later os._exit() a process that may still be saving or running other work
+            loader.close()
             if watchdog:
-                watchdog.beat()
-        if torch.cuda.is_available() and self._device_kind() == "hip":
-            torch.cuda.synchronize()
-        total = time.perf_counter() - t_start
-        loader.close()
-        if watchdog:
-            watchdog.stop()
+                watchdog.stop()
         tps = cfg.batchSize * iters / total
         self.metrics.line(f"total samples per second {tps:.1f}")
         row = {"name": f"{cfg.name}:{self.id}", "numLayers": cfg.numLayers,

@@ -76,7 +76,7 @@ class StepWatchdog:
         self.comm_error = ""
         self._beat = time.monotonic()
         self._stop = threading.Event()
-        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t = threading.Thread(target=self._run, daemon=True, name="dg-step-watchdog")
         self._t.start()
 
     def beat(self):
@@ -109,8 +109,8 @@ class StepWatchdog:
 class PhaseGuard:
     """Per-rank hang guard for a run made of named phases (bench.py: ``comm`` set-up,
     ``capture``, ``warmup``, ``timed``, ``report``).  ``phase(name, limit_s)`` arms a
-    deadline; a thread that outlives it writes ``hang:<name>`` to ``<status_dir>/rank<r>``
-    (read by the launcher), reports on stderr and ends the process with ``os._exit(42)``,
+    deadline; a thread that outlives it writes ``hang:<name>:<comm kind>`` to
+    ``<status_dir>/rank<r>`` (read by the launcher; ``set_comm`` records the kind), reports on stderr and ends the process with ``os._exit(42)``,
     so a rank stuck in a collective of a dead or stuck peer exits non-zero within the bound
     instead of holding the node until an outer timeout."""
 
@@ -122,6 +122,9 @@ class PhaseGuard:
         self.poll = poll_s
         self.name = "start"
         self.deadline = None
+        # the communicator this rank's collectives go through ("" until chosen); the status
+        # file carries it so the launcher can tell a native-communicator hang from any other
+        self.comm = ""
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
@@ -131,6 +134,10 @@ class PhaseGuard:
         with self._lock:
             self.name = name
             self.deadline = time.monotonic() + limit_s
+
+    def set_comm(self, kind: str):
+        with self._lock:
+            self.comm = kind
 
     def _write_status(self, text: str):
         if self.status_dir:
@@ -144,9 +151,9 @@ class PhaseGuard:
         import sys
         while not self._stop.wait(self.poll):
             with self._lock:
-                name, dl = self.name, self.deadline
+                name, dl, comm = self.name, self.deadline, self.comm
             if dl is not None and time.monotonic() > dl:
-                self._write_status(f"hang:{name}")
+                self._write_status(f"hang:{name}:{comm}")
                 sys.stderr.write(f"[guard] rank {self.rank}: phase '{name}' exceeded its "
                                  f"time limit: exiting {self.EXIT_CODE}\n")
                 sys.stderr.flush()

@@ -61,6 +61,51 @@ def test_hung_rank_is_bounded_by_the_phase_guard():
     wall = time.monotonic() - t0
     assert r.returncode != 0
     assert "phase 'timed' exceeded" in r.stderr
-    assert "'rank1': 'timed'" in r.stderr   # (rank 0, waiting in the barrier, may trip too)
+    assert "'rank1': ('timed'" in r.stderr   # (rank 0, waiting in the barrier, may trip too)
     assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
     assert wall < 150
+
+
+def test_comm_hang_is_bounded_and_falls_back():
+    # rank 1 hangs while setting up the native communicator (--comm auto; the CPU dry run
+    # rehearses that phase): its guard fires after --comm-timeout with hang:comm:native, the
+    # launcher re-runs with --comm torch (the hook does not fire on that kind) and relays the
+    # fallback run's JSON line, marked comm_fallback — all well inside the launch budget
+    import time
+    t0 = time.monotonic()
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "2", "--warmup", "1",
+               "--comm-timeout", "8", "--phase-timeout", "8", "--launch-budget", "200",
+               env={"DG_BENCH_HANG": "1:comm:native"}, timeout=240)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert "comm_fallback" in rec and rec["n_gpus"] == 2
+    assert rec["comm"].startswith("gloo (torch")
+    assert wall < 200
+
+
+def test_comm_hang_on_every_kind_fails_within_budget():
+    # the same hang on any communicator: the fallback run hangs too; the job still ends
+    # non-zero with no JSON line, bounded by the guards (not by an outer timeout)
+    import time
+    t0 = time.monotonic()
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "2", "--warmup", "1",
+               "--comm-timeout", "8", "--phase-timeout", "8", "--launch-budget", "200",
+               env={"DG_BENCH_HANG": "1:comm"}, timeout=240)
+    wall = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "re-run with --comm torch" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert wall < 200
+
+
+def test_non_native_hang_does_not_trigger_the_fallback():
+    # a hang while the rank is on torch.distributed (--comm torch) is not a native-communicator
+    # problem: no re-run, fail as is
+    r = _bench("--cpu-dry-run", "--gpus", "2", "--steps", "2", "--warmup", "1", "--comm", "torch",
+               "--comm-timeout", "6", "--phase-timeout", "6", env={"DG_BENCH_HANG": "1:comm"},
+               timeout=240)
+    assert r.returncode != 0
+    assert "re-run with --comm torch" not in r.stderr

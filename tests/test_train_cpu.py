@@ -181,8 +181,16 @@ def test_nan_policy_and_fault_injection(tmp_path, ref_data, monkeypatch):
     res = s.run(6)
     assert np.isfinite(res["train_cost"])
     monkeypatch.setenv("DG_FAULT", "0:2:raise")
+    # with a step watchdog armed: the raise must stop it too (else it would later
+    # os._exit() this process)
+    import threading
+    monkeypatch.setenv("DG_STEP_TIMEOUT", "30")
     with pytest.raises(RuntimeError, match="DG_FAULT"):
         Experiment(_cfg(tmp_path, ref_data), id="f").run(4)
+    for t in threading.enumerate():
+        if t.name == "dg-step-watchdog":
+            t.join(timeout=10)
+            assert not t.is_alive(), "the step watchdog outlived a failed run"
 
 
 def test_cli_train_resume_eval(tmp_path, ref_data):
