@@ -135,6 +135,11 @@ hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t n
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s);
+int dg_grad_update_cols();
+hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
+                          float* P, float* G, const void* G16, float* MS, float rms_decay,
+                          float gscale, const float* gate, double* lr, double decay,
+                          long long* step, unsigned* tickets, int* bad_steps, hipStream_t s);
 }
 
 namespace {
@@ -446,6 +451,18 @@ PYBIND11_MODULE(_dghip, m) {
                             S(stream)),
           "weight_refresh_decay");
   });
+  m.def("grad_update_cols", []() { return dg_grad_update_cols(); });
+  m.def("grad_update", [](uintptr_t table, int n, long long plain_off, long long plain_n,
+                          uintptr_t p, uintptr_t g, uintptr_t g16, uintptr_t ms, float rms_decay,
+                          float gscale, uintptr_t gate, uintptr_t lr, double decay,
+                          uintptr_t step, uintptr_t tickets, uintptr_t bad, uintptr_t stream) {
+    check(dg_grad_update(P<long long>(table), n, plain_off, plain_n, P<float>(p), P<float>(g),
+                         P<void>(g16), P<float>(ms), rms_decay, gscale, P<float>(gate),
+                         P<double>(lr), decay, P<long long>(step), P<unsigned>(tickets),
+                         P<int>(bad), S(stream)),
+          "grad_update");
+  }, "fused gradient pass 2 (slabs / bias partials, or the flat gradient) + SGD / RMSProp + "
+     "operand refresh + LR decay (elementwise.hip grad_update_kernel)");
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },

@@ -670,17 +670,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
   const int pos_blocks = bpart ? (NPTS * M + 255) / 256 : 0;
   if ((int)blockIdx.x >= main_blocks + pos_blocks + (bpart ? M : 0)) return;  // (shorter layer)
   if ((int)blockIdx.x >= main_blocks + pos_blocks) {
-    // gbias[c] = sum over (chunk, row) of rowpart; one workgroup per channel
-    __shared__ float s_r[4];
+    // gbias[c] = sum over (chunk, row) of rowpart (the fixed-order rows_sum, shared with the
+    // fused grad_update kernel); one workgroup per channel
     const int c = blockIdx.x - main_blocks - pos_blocks;
     const float* rp = bpart + (size_t)bchunks * NPTS * M;  // rowpart [bchunks][19][M]
-    float s0 = 0.f;
-    for (int r = threadIdx.x; r < bchunks * BOARD; r += 256) s0 += rp[(size_t)r * M + c];
-    s0 = wave_sum(s0);
-    if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = s0;
-    __syncthreads();
     if (threadIdx.x == 0) {
-      const float v = (s_r[0] + s_r[1]) + (s_r[2] + s_r[3]);
+      const float v = rows_sum(rp, bchunks * BOARD, M, c);
       gbias[c] = v;
       if (Ls.gbias16[ly]) Ls.gbias16[ly][c] = f2bf(v);
     }
@@ -692,15 +687,9 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
     const int j = (blockIdx.x - main_blocks) * 256 + threadIdx.x;
     const int np = NPTS * M;
     if (j < np) {
-      float s0 = 0.f, s1 = 0.f;
-      int z = 0;
-      for (; z + 2 <= bchunks; z += 2) {
-        s0 += bpart[(size_t)z * np + j];
-        s1 += bpart[(size_t)(z + 1) * np + j];
-      }
-      for (; z < bchunks; ++z) s0 += bpart[(size_t)z * np + j];
-      gposb[j] = s0 + s1;
-      if (Ls.gposb16[ly]) Ls.gposb16[ly][j] = f2bf(s0 + s1);
+      const float v = chunk_sum(bpart + j, bchunks, (size_t)np);
+      gposb[j] = v;
+      if (Ls.gposb16[ly]) Ls.gposb16[ly][j] = f2bf(v);
     }
     return;
   }
@@ -711,17 +700,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
        idx += main_blocks * blockDim.x) {
     const int co = idx / kq;
     const int k = (idx - co * kq) * 4;
-    const float* src = slab + (size_t)co * KP + k;
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
-    int z = 0;
-    for (; z + 4 <= splits; z += 4) {
-      s0 += *(const f32x4*)(src + (z + 0) * zstride);
-      s1 += *(const f32x4*)(src + (z + 1) * zstride);
-      s2 += *(const f32x4*)(src + (z + 2) * zstride);
-      s3 += *(const f32x4*)(src + (z + 3) * zstride);
-    }
-    for (; z < splits; ++z) s0 += *(const f32x4*)(src + z * zstride);
-    const f32x4 s = (s0 + s1) + (s2 + s3);
+    const f32x4 s = slab_sum4(slab + (size_t)co * KP + k, splits, zstride);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int kk = k + e;

@@ -94,6 +94,63 @@ DG_DEV void block_amax(float v, unsigned* amax, float* s_tmp) {
   }
 }
 
+// ---- deterministic second-pass sums of the weight / bias gradient partials -------------
+// Shared by the slab reduce (conv_mfma.hip wgrad_reduce_kernel) and the fused reduce +
+// update + refresh (elementwise.hip grad_update_kernel), so the two produce bit-identical
+// gradients: a fixed summation order that does not depend on the thread mapping.
+//
+// sum over split slabs z of src[z * zstride] (four interleaved accumulators, z mod 4, the tail
+// into the first, then (s0 + s1) + (s2 + s3)); element-wise identical for the f32x4 form
+DG_DEV f32x4 slab_sum4(const float* src, int splits, size_t zstride) {
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {
+    s0 += *(const f32x4*)(src + (z + 0) * zstride);
+    s1 += *(const f32x4*)(src + (z + 1) * zstride);
+    s2 += *(const f32x4*)(src + (z + 2) * zstride);
+    s3 += *(const f32x4*)(src + (z + 3) * zstride);
+  }
+  for (; z < splits; ++z) s0 += *(const f32x4*)(src + z * zstride);
+  return (s0 + s1) + (s2 + s3);
+}
+DG_DEV float slab_sum1(const float* src, int splits, size_t zstride) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {
+    s0 += src[(z + 0) * zstride];
+    s1 += src[(z + 1) * zstride];
+    s2 += src[(z + 2) * zstride];
+    s3 += src[(z + 3) * zstride];
+  }
+  for (; z < splits; ++z) s0 += src[z * zstride];
+  return (s0 + s1) + (s2 + s3);
+}
+// per-position bias gradient: sum over board chunks of part[chunk * np] (even / odd chunks)
+DG_DEV float chunk_sum(const float* part, int nchunks, size_t np) {
+  float s0 = 0.f, s1 = 0.f;
+  int z = 0;
+  for (; z + 2 <= nchunks; z += 2) {
+    s0 += part[(size_t)z * np];
+    s1 += part[(size_t)(z + 1) * np];
+  }
+  for (; z < nchunks; ++z) s0 += part[(size_t)z * np];
+  return s0 + s1;
+}
+// per-channel bias gradient of channel c: sum of the R = chunks x 19 row partials
+// rowpart[r][C] (r mod 4 accumulators)
+DG_DEV float rows_sum(const float* rowpart, int R, int C, int c) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int r = 0;
+  for (; r + 4 <= R; r += 4) {
+    s0 += rowpart[(size_t)(r + 0) * C + c];
+    s1 += rowpart[(size_t)(r + 1) * C + c];
+    s2 += rowpart[(size_t)(r + 2) * C + c];
+    s3 += rowpart[(size_t)(r + 3) * C + c];
+  }
+  for (; r < R; ++r) s0 += rowpart[(size_t)r * C + c];
+  return (s0 + s1) + (s2 + s3);
+}
+
 // Exact floor(n / d) for 0 <= n < 2^22 and 1 <= d <= 4096 via a 64-bit magic
 // m = floor(2^32 / d) + 1 (host computes it; checked exhaustively in tests/tools).
 DG_DEV uint32_t fastdiv(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }

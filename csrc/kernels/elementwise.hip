@@ -291,48 +291,30 @@ struct WRefreshArgs {
   WRefreshLayer L[MAX_REFRESH];
 };
 
-// Tiled: one block per (layer, tap, 64 co x 64 ci tile); wf rows are written along ci and
-// the flipped-tap transpose wd along co through a padded LDS tile, so every global store
-// is a coalesced 128-B row piece (the per-element version scattered 2-byte dgrad stores
-// and ran at ~12 us for 2.1M weights).  Block (0, 0) also applies the per-step learning
-// rate decay lr *= (1 - decay) (the reference's SGD, optimizer.lua:25-26) when lr != 0:
-// this kernel runs after the update kernel that reads lr, and nothing here reads it.
-__global__ void __launch_bounds__(256)
-weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step) {
-  if (lr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    *lr = *lr * (1.0 - decay);
-    if (step) *step += 1;
-  }
-  const WRefreshLayer L = a.L[blockIdx.y];
-  const int nct = (L.cout + 63) / 64, nit = (L.cin + 63) / 64;
-  const int tiles = L.taps * nct * nit;
-  __shared__ float tileS[64][65];
-  __shared__ float s_amax[4];
-  float wmax = 0.f;
-  for (int tix = blockIdx.x; tix < tiles; tix += gridDim.x) {
-    const int t = tix / (nct * nit);
-    const int r = tix - t * nct * nit;
-    const int cot = r / nit, cit = r - cot * nit;
-    const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
-    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-      const int rr = e >> 6, cc = e & 63;
-      const int co = cot * 64 + rr, ci = cit * 64 + cc;
-      float v = 0.f;
-      if (co < L.cout && ci < L.cin) {
-        v = L.w[((size_t)co * L.taps + t) * L.cin + ci];
-        if (L.wf) L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = f2bf(v);
-        if (L.s_w) {   // fp8 layer: |w| max for the next scale; the plain e4m3 copy if kept
-          if (L.wf8) {
-            const float q = fmaxf(fminf(v * inv8, 448.f), -448.f);
-            L.wf8[(size_t)co * L.kpf + t * L.cinp + ci] =
-                (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xFF);
-          }
-          wmax = fmaxf(wmax, fabsf(v));
-        }
-      }
-      tileS[rr][cc] = v;
+// Per-element part of a 64 x 64 (co, ci) tile's refresh at tap t: the plain bf16 forward
+// operand, the plain e4m3 copy, the |w| max (fp8 layers).
+DG_DEV void refresh_elem(const WRefreshLayer& L, int co, int ci, int t, float v, float inv8,
+                         float& wmax) {
+  if (L.wf) L.wf[(size_t)co * L.kpf + t * L.cinp + ci] = f2bf(v);
+  if (L.s_w) {   // fp8 layer: |w| max for the next scale; the plain e4m3 copy if kept
+    if (L.wf8) {
+      const float q = fmaxf(fminf(v * inv8, 448.f), -448.f);
+      L.wf8[(size_t)co * L.kpf + t * L.cinp + ci] =
+          (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xFF);
     }
-    if (L.wd || L.wf_frag || L.wd_frag || L.wf8_frag || L.wd8_frag) __syncthreads();
+    wmax = fmaxf(wmax, fabsf(v));
+  }
+}
+
+DG_DEV bool refresh_needs_tile(const WRefreshLayer& L) {
+  return L.wd || L.wf_frag || L.wd_frag || L.wf8_frag || L.wd8_frag;
+}
+
+// The whole-tile operand copies of tile (t, cot, cit) from tileS[co - 64 cot][ci - 64 cit]
+// (fp32 weights, written and made visible by the caller): the transposed / flipped dgrad
+// operand and the MFMA fragment orders of the stacks.  Ends with a barrier.
+DG_DEV void refresh_tile_copies(const WRefreshLayer& L, int t, int cot, int cit,
+                                float (*tileS)[65], float inv8) {
     if (L.wd) {
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
@@ -432,8 +414,11 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
                  lane] = uint4{q[0], q[1], q[2], q[3]};
     }
     __syncthreads();
-  }
-  if (L.s_w && L.amax_w) {   // uniform per block: this workgroup's slot (a plain store)
+}
+
+// this block's |w| max into its amax slot (fp8 layers; uniform per block, a plain store)
+DG_DEV void refresh_amax(const WRefreshLayer& L, float wmax, float* s_amax) {
+  if (L.s_w && L.amax_w) {
     wmax = wave_max(wmax);
     if ((threadIdx.x & 63) == 0) s_amax[threadIdx.x >> 6] = wmax;
     __syncthreads();
@@ -441,15 +426,62 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
       L.amax_w[blockIdx.x] =
           __float_as_uint(fmaxf(fmaxf(s_amax[0], s_amax[1]), fmaxf(s_amax[2], s_amax[3])));
   }
+}
+
+// pbias_frag unit of pixel q (0..383; pixels past 360 repeat 360) and channels c..c+3:
+// element (((h * 24 + jg) * 2 + wm) * 4 + i) * 64 + lane, pixel jg*16 + (lane & 15),
+// channels 128h + wm*64 + i*16 + (lane >> 4)*4 .. +3 — the stacks' accumulator-fragment
+// order (one coalesced 512-B load per epilogue fragment)
+DG_DEV size_t pbias_frag_index(int q, int c) {
+  const int h = c >> 7, wm = (c >> 6) & 1, i = (c >> 4) & 3, lg = (c >> 2) & 3;
+  return ((((size_t)h * 24 + (q >> 4)) * 2 + wm) * 4 + i) * 64 + lg * 16 + (q & 15);
+}
+
+// Tiled: one block per (layer, tap, 64 co x 64 ci tile); wf rows are written along ci and
+// the flipped-tap transpose wd along co through a padded LDS tile, so every global store
+// is a coalesced 128-B row piece (the per-element version scattered 2-byte dgrad stores
+// and ran at ~12 us for 2.1M weights).  Block (0, 0) also applies the per-step learning
+// rate decay lr *= (1 - decay) (the reference's SGD, optimizer.lua:25-26) when lr != 0:
+// this kernel runs after the update kernel that reads lr, and nothing here reads it.
+__global__ void __launch_bounds__(256)
+weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step) {
+  if (lr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    *lr = *lr * (1.0 - decay);
+    if (step) *step += 1;
+  }
+  const WRefreshLayer L = a.L[blockIdx.y];
+  const int nct = (L.cout + 63) / 64, nit = (L.cin + 63) / 64;
+  const int tiles = L.taps * nct * nit;
+  __shared__ float tileS[64][65];
+  __shared__ float s_amax[4];
+  float wmax = 0.f;
+  const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
+  for (int tix = blockIdx.x; tix < tiles; tix += gridDim.x) {
+    const int t = tix / (nct * nit);
+    const int r = tix - t * nct * nit;
+    const int cot = r / nit, cit = r - cot * nit;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      const int co = cot * 64 + rr, ci = cit * 64 + cc;
+      float v = 0.f;
+      if (co < L.cout && ci < L.cin) {
+        v = L.w[((size_t)co * L.taps + t) * L.cin + ci];
+        refresh_elem(L, co, ci, t, v, inv8, wmax);
+      }
+      tileS[rr][cc] = v;
+    }
+    if (refresh_needs_tile(L)) {
+      __syncthreads();
+      refresh_tile_copies(L, t, cot, cit, tileS, inv8);
+    }
+  }
+  refresh_amax(L, wmax, s_amax);
   if (L.pbias) {
     const int n = NPTS * L.cout;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256)
       L.pbias[e] = f2bf(L.bias[e % L.cout] + L.posb[e]);
   }
   if (L.pbias_frag) {
-    // element e = (((h * 24 + jg) * 2 + wm) * 4 + i) * 64 + lane: pixel jg*16 + (lane & 15),
-    // channels 128h + wm*64 + i*16 + (lane >> 4)*4 .. +3 (h: output pass of 128 channels)
-    // — one coalesced 512-B load per epilogue fragment
     const int ne = (L.cout / 128) * 24 * 2 * 4 * 64;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < ne; e += gridDim.x * 256) {
       const int lane = e & 63, i = (e >> 6) & 3, wm = (e >> 8) & 1, jg = (e >> 9) % 24,
@@ -464,6 +496,259 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
   }
 }
 
+// ------------------------------------------------------------------------------------
+// The end of a training step in ONE launch: gradient second pass + optimizer + operand
+// refresh + LR decay.  Replaces (slab reduce, bias pass 2, head-less SGD / RMSProp, weight
+// refresh) — three launches, their idle gaps and the fp32 gradient round trip between them.
+//
+// Per conv layer l (grid.y = l) the gradient comes either from the weight-gradient kernels'
+// split-K slabs and the bias partials (single-GPU training: nothing needs the reduced
+// gradient before the update) or from the flat gradient (data parallel: the all-reduced
+// buckets, fp32 or the bf16 wire twin).  The weight part runs on the weight_refresh tiling
+// (64 co x 64 ci at one tap per tile): sum the slabs (the same fixed order as
+// wgrad_reduce_kernel: bit-identical gradients), write the fp32 gradient, update the fp32
+// master weight, and write the tile's operand copies from the updated values.  The bias
+// part: every block recomputes the layer's new per-channel bias (C sums of R row partials)
+// and updates its share of the per-position biases, then writes the forward epilogue's bias
+// tables from the new values.  Readers of an old value and the writer of its new value must
+// not race: the per-channel biases and the learning rate are written by the LAST block to
+// finish (an atomic ticket per layer / for the grid, taken after the block's reads; the
+// counters are reset by that block, so the launch is graph-replayable).  grid.y = n: the
+// plain range (the head's parameters, whose gradient head_reduce already wrote).
+//
+// Non-finite gradient entries are not applied (the parameter keeps its value) and flag the
+// step (bad_steps += 1 once); gate (device, optional) = 0 skips every update (a non-finite
+// loss); the LR decays either way, as with the separate kernels.
+// Reference: SGD step + LR decay (optimizer.lua:24-27); AdagradOptimizer (:1-14).
+struct GUSrc {
+  const float* slab;    // [splits][Mpad][KP], k = t * cinp + ci; null: the flat gradient
+  const float* bpart;   // [bchunks][361][C] partials + [bchunks][19][C] row partials; or null
+  int splits, Mpad, KP, bchunks;
+  long long w_off, b_off, pos_off;   // element offsets into the flat P / G / MS
+};
+constexpr int MAX_GU = 20;
+struct GUArgs {
+  int n;
+  WRefreshLayer L[MAX_GU];
+  GUSrc S[MAX_GU];
+  long long plain_off, plain_n;
+  float* P;
+  float* G;            // fp32 gradient: read (no slab) or written (slab)
+  const bf16_t* G16;   // bf16 wire twin to read instead of G (data parallel), or null
+  float* MS;           // RMSProp mean square (same flat layout), or null: SGD
+  float rms_decay, gscale;
+  const float* gate;
+  const double* lr;
+  double decay;
+  long long* step;
+  unsigned* tickets;   // [n + 1]: per layer, then the grid's (+ non-finite flag << 16)
+  int* bad_steps;
+};
+
+// one parameter's update; ms (RMSProp only) is updated in place
+DG_DEV float gu_update(float p, float g, bool rms, float& ms, float l, float rms_decay,
+                       float gscale, bool apply, unsigned& bad) {
+  if (!isfinite(g)) {
+    bad = 1u;
+    return p;
+  }
+  if (!apply) return p;
+  if (rms) {
+    const float gi = g * gscale;
+    const float m = rms_decay * ms + (1.f - rms_decay) * gi * gi;
+    ms = m;
+    return p - l * gi * rsqrtf(m);
+  }
+  return p - l * g;
+}
+// the same on flat element o (P, MS in global memory)
+DG_DEV float gu_update_at(const GUArgs& a, long long o, float g, float l, bool apply,
+                          unsigned& bad) {
+  const bool rms = a.MS != nullptr;
+  float ms = rms ? a.MS[o] : 0.f;
+  const float v = gu_update(a.P[o], g, rms, ms, l, a.rms_decay, a.gscale, apply, bad);
+  if (rms) a.MS[o] = ms;
+  return v;
+}
+
+__global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
+  __shared__ float tileS[64][65];
+  __shared__ float s_amax[4];
+  __shared__ float s_b[256];       // the layer's new per-channel bias,
+  __shared__ float s_gb[256];      // its gradient
+  __shared__ float s_ms[256];      // and mean square (RMSProp)
+  __shared__ unsigned s_flag[2];
+  const int ly = blockIdx.y;
+  const int tid = threadIdx.x;
+  const bool apply = !(a.gate && *a.gate == 0.f);
+  // SGD: l = lr * gscale (as sgd_kernel); RMSProp: l = lr, gscale inside
+  const float l = a.MS ? (float)(*a.lr) : (float)(*a.lr) * a.gscale;
+  unsigned bad = 0u;
+  if (tid == 0) s_flag[0] = 0u;
+  __syncthreads();
+  if (ly == a.n) {
+    // the head: plain update from the flat gradient
+    for (long long i = blockIdx.x * 256LL + tid; i < a.plain_n; i += gridDim.x * 256LL) {
+      const long long o = a.plain_off + i;
+      const float g = a.G16 ? bf2f(a.G16[o]) : a.G[o];
+      a.P[o] = gu_update_at(a, o, g, l, apply, bad);
+    }
+  } else {
+    const WRefreshLayer L = a.L[ly];
+    const GUSrc S = a.S[ly];
+    float* Pw = a.P + S.w_off;
+    float* Gw = a.G + S.w_off;
+    float* MSw = a.MS ? a.MS + S.w_off : nullptr;
+    const int nct = (L.cout + 63) / 64, nit = (L.cin + 63) / 64;
+    const int tiles = L.taps * nct * nit;
+    float wmax = 0.f;
+    const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
+    const size_t zstride = (size_t)S.Mpad * S.KP;
+    const bool vec = S.slab && (L.cin & 3) == 0 && (L.cinp & 3) == 0 && (S.KP & 3) == 0;
+    for (int tix = blockIdx.x; tix < tiles; tix += gridDim.x) {
+      const int t = tix / (nct * nit);
+      const int r = tix - t * nct * nit;
+      const int cot = r / nit, cit = r - cot * nit;
+      if (vec) {
+        // 4 consecutive ci per thread: 16-B slab loads (a row of the tile = 256 B)
+        for (int e4 = tid; e4 < 64 * 16; e4 += 256) {
+          const int rr = e4 >> 4, cc = (e4 & 15) * 4;
+          const int co = cot * 64 + rr, ci = cit * 64 + cc;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (co < L.cout && ci < L.cin) {
+            const f32x4 g4 = slab_sum4(S.slab + (size_t)co * S.KP + t * L.cinp + ci, S.splits,
+                                       zstride);
+            const size_t o = ((size_t)co * L.taps + t) * L.cin + ci;
+            *(f32x4*)(Gw + o) = g4;
+            const f32x4 p4 = *(const f32x4*)(Pw + o);
+            f32x4 m4 = {0.f, 0.f, 0.f, 0.f};
+            if (MSw) m4 = *(const f32x4*)(MSw + o);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              float m = m4[k];
+              v[k] = gu_update(p4[k], g4[k], MSw != nullptr, m, l, a.rms_decay, a.gscale, apply,
+                               bad);
+              m4[k] = m;
+              refresh_elem(L, co, ci + k, t, v[k], inv8, wmax);
+            }
+            *(f32x4*)(Pw + o) = v;
+            if (MSw) *(f32x4*)(MSw + o) = m4;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tileS[rr][cc + k] = v[k];
+        }
+      } else {
+        for (int e = tid; e < 64 * 64; e += 256) {
+          const int rr = e >> 6, cc = e & 63;
+          const int co = cot * 64 + rr, ci = cit * 64 + cc;
+          float v = 0.f;
+          if (co < L.cout && ci < L.cin) {
+            const size_t o = ((size_t)co * L.taps + t) * L.cin + ci;
+            float g;
+            if (S.slab) {
+              g = slab_sum1(S.slab + (size_t)co * S.KP + t * L.cinp + ci, S.splits, zstride);
+              Gw[o] = g;
+            } else {
+              g = a.G16 ? bf2f(a.G16[S.w_off + o]) : Gw[o];
+            }
+            v = gu_update_at(a, S.w_off + o, g, l, apply, bad);
+            Pw[o] = v;
+            refresh_elem(L, co, ci, t, v, inv8, wmax);
+          }
+          tileS[rr][cc] = v;
+        }
+      }
+      __syncthreads();    // tileS complete (also orders the next tile's writes after reads)
+      if (refresh_needs_tile(L)) refresh_tile_copies(L, t, cot, cit, tileS, inv8);
+    }
+    refresh_amax(L, wmax, s_amax);
+    // ---- biases: the layer's new per-channel bias (every block), then this block's share of
+    // the per-position biases and the bias tables
+    const int C = L.cout;
+    const int R = S.bchunks * BOARD;
+    const float* rowpart = S.bpart ? S.bpart + (size_t)S.bchunks * NPTS * C : nullptr;
+    for (int c = tid; c < C; c += 256) {
+      float g;
+      if (S.bpart) {
+        g = rows_sum(rowpart, R, C, c);
+      } else {
+        const long long o = S.b_off + c;
+        g = a.G16 ? bf2f(a.G16[o]) : a.G[o];
+      }
+      float ms_v = a.MS ? a.MS[S.b_off + c] : 0.f;
+      s_b[c] = gu_update(a.P[S.b_off + c], g, a.MS != nullptr, ms_v, l, a.rms_decay, a.gscale,
+                         apply, bad);
+      // (the per-channel bias, its gradient and mean square are written by the layer's last
+      // block below: other blocks still read the old values here)
+      s_gb[c] = g;
+      s_ms[c] = ms_v;
+    }
+    __syncthreads();
+    const int C4 = C / 4;
+    const size_t np = (size_t)NPTS * C;
+    for (int it = blockIdx.x * 256 + tid; it < NPTS * C4; it += gridDim.x * 256) {
+      const int p = it / C4, c = (it - p * C4) * 4;
+      float nb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const size_t j = (size_t)p * C + c + k;
+        float g;
+        if (S.bpart) {
+          g = chunk_sum(S.bpart + j, S.bchunks, np);
+          a.G[S.pos_off + j] = g;
+        } else {
+          g = a.G16 ? bf2f(a.G16[S.pos_off + j]) : a.G[S.pos_off + j];
+        }
+        const float v = gu_update_at(a, S.pos_off + j, g, l, apply, bad);
+        a.P[S.pos_off + j] = v;
+        nb[k] = s_b[c + k] + v;
+        if (L.pbias) L.pbias[j] = f2bf(nb[k]);
+      }
+      if (L.pbias_frag) {
+        const uint2 u = uint2{pack_bf16x2(nb[0], nb[1]), pack_bf16x2(nb[2], nb[3])};
+        L.pbias_frag[pbias_frag_index(p, c)] = u;
+        if (p == NPTS - 1)
+          for (int q = NPTS; q < 24 * 16; ++q) L.pbias_frag[pbias_frag_index(q, c)] = u;
+      }
+    }
+  }
+  // ---- tickets: the layer's last block writes its per-channel biases; the grid's last block
+  // decays the LR, counts a step with a non-finite gradient entry and resets the counters.
+  // No fences: every block's reads of an old value (lr, the per-channel biases) have returned
+  // before its ticket is taken (their values were consumed before the barrier), and the
+  // writers act only after seeing the final ticket; the new values are read by later
+  // launches.  The grid ticket carries the non-finite flag in its high half (one atomic).
+  if (bad) s_flag[0] = 1u;     // (benign same-value race)
+  __syncthreads();
+  if (tid == 0) {
+    unsigned last_layer = 0u;
+    if (ly < a.n) last_layer = atomicAdd(&a.tickets[ly], 1u) == gridDim.x - 1 ? 1u : 0u;
+    s_flag[1] = last_layer;
+  }
+  __syncthreads();
+  if (s_flag[1]) {
+    const WRefreshLayer L = a.L[ly];
+    const GUSrc S = a.S[ly];
+    for (int c = tid; c < L.cout; c += 256) {
+      a.P[S.b_off + c] = s_b[c];
+      if (S.bpart) a.G[S.b_off + c] = s_gb[c];
+      if (a.MS) a.MS[S.b_off + c] = s_ms[c];
+    }
+    if (tid == 0) a.tickets[ly] = 0u;
+  }
+  if (tid == 0) {
+    const unsigned total = gridDim.x * gridDim.y;   // < 2^16 (host check)
+    const unsigned old = atomicAdd(&a.tickets[a.n], 1u + (s_flag[0] ? 0x10000u : 0u));
+    if ((old & 0xFFFFu) == total - 1) {
+      double* lrw = const_cast<double*>(a.lr);
+      *lrw = *lrw * (1.0 - a.decay);
+      if (a.step) *a.step += 1;
+      const bool flagged = (old >> 16) != 0u || s_flag[0];
+      if (flagged && a.bad_steps && apply) *a.bad_steps += 1;
+      a.tickets[a.n] = 0u;
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------
 // Stand-in for a ring all-reduce on ONE GPU (bench.py --force-dp --comm proxy; the real
@@ -612,6 +897,46 @@ hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s)
 //    pbias, wf_frag, wd_frag, wf8_frag, wd8_frag}  (pbias_frag / *_frag: stack-order tables,
 //    or 0)
 // lr (optional): fused per-step decay lr *= (1 - decay), step += 1 (see the kernel).
+static hipError_t parse_refresh_row(const long long* t, WRefreshLayer& L) {
+  L.w = (const float*)t[0];
+  L.wf = (bf16_t*)t[1];
+  L.wd = (bf16_t*)t[2];
+  L.cout = (int)t[3];
+  L.cin = (int)t[4];
+  L.taps = (int)t[5];
+  L.cinp = (int)t[6];
+  L.kpf = (int)t[7];
+  L.kpd = (int)t[8];
+  L.wf8 = (uint8_t*)t[10];
+  L.s_w = (const float*)t[11];
+  L.amax_w = (unsigned*)t[12];
+  L.bias = (const float*)t[13];
+  L.posb = (const float*)t[14];
+  L.pbias = (bf16_t*)t[15];
+  L.pbias_frag = (uint2*)t[9];
+  if (L.pbias_frag && L.cout != 128 && L.cout != 256) return hipErrorInvalidValue;
+  L.wf_frag = (uint4*)t[16];
+  L.wd_frag = (uint4*)t[17];
+  if (L.wf8 && !L.s_w) return hipErrorInvalidValue;
+  if (L.wf_frag && L.taps != 9 &&   // the fused-first-layer layout (l1 mode)
+      (L.wd_frag || (L.cout != 128 && L.cout != 256) || L.cin > 64 || L.cinp % 8 != 0 ||
+       L.taps * L.cinp > 1024))
+    return hipErrorInvalidValue;
+  L.wf8_frag = (uint4*)t[18];
+  L.wd8_frag = (uint4*)t[19];
+  if ((L.wf8_frag || L.wd8_frag) &&
+      (!L.s_w || L.taps != 9 || L.cout != L.cin || (L.cout != 128 && L.cout != 256)))
+    return hipErrorInvalidValue;
+  if (L.wd_frag && L.taps != 9) return hipErrorInvalidValue;
+  if ((L.wf_frag || L.wd_frag) && L.taps == 9 &&
+      (L.cout != L.cin || (L.cout != 128 && L.cout != 256)))
+    return hipErrorInvalidValue;
+  return hipSuccess;
+}
+static int refresh_tiles(const WRefreshLayer& L) {
+  return L.taps * ((L.cout + 63) / 64) * ((L.cin + 63) / 64);
+}
+
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s) {
   if (n <= 0 || n > MAX_REFRESH) return hipErrorInvalidValue;
@@ -619,47 +944,74 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
   a.n = n;
   int maxtotal = 1;
   for (int i = 0; i < n; ++i) {
-    const long long* t = table + 20 * i;
-    a.L[i].w = (const float*)t[0];
-    a.L[i].wf = (bf16_t*)t[1];
-    a.L[i].wd = (bf16_t*)t[2];
-    a.L[i].cout = (int)t[3];
-    a.L[i].cin = (int)t[4];
-    a.L[i].taps = (int)t[5];
-    a.L[i].cinp = (int)t[6];
-    a.L[i].kpf = (int)t[7];
-    a.L[i].kpd = (int)t[8];
-    a.L[i].wf8 = (uint8_t*)t[10];
-    a.L[i].s_w = (const float*)t[11];
-    a.L[i].amax_w = (unsigned*)t[12];
-    a.L[i].bias = (const float*)t[13];
-    a.L[i].posb = (const float*)t[14];
-    a.L[i].pbias = (bf16_t*)t[15];
-    a.L[i].pbias_frag = (uint2*)t[9];
-    if (a.L[i].pbias_frag && a.L[i].cout != 128 && a.L[i].cout != 256) return hipErrorInvalidValue;
-    a.L[i].wf_frag = (uint4*)t[16];
-    a.L[i].wd_frag = (uint4*)t[17];
-    if (a.L[i].wf8 && !a.L[i].s_w) return hipErrorInvalidValue;
-    if (a.L[i].wf_frag && a.L[i].taps != 9 &&   // the fused-first-layer layout (l1 mode)
-        (a.L[i].wd_frag || (a.L[i].cout != 128 && a.L[i].cout != 256) || a.L[i].cin > 64 ||
-         a.L[i].cinp % 8 != 0 ||
-         a.L[i].taps * a.L[i].cinp > 1024))
-      return hipErrorInvalidValue;
-    a.L[i].wf8_frag = (uint4*)t[18];
-    a.L[i].wd8_frag = (uint4*)t[19];
-    if ((a.L[i].wf8_frag || a.L[i].wd8_frag) &&
-        (!a.L[i].s_w || a.L[i].taps != 9 || a.L[i].cout != a.L[i].cin ||
-                            (a.L[i].cout != 128 && a.L[i].cout != 256)))
-      return hipErrorInvalidValue;
-    if (a.L[i].wd_frag && a.L[i].taps != 9) return hipErrorInvalidValue;
-    if ((a.L[i].wf_frag || a.L[i].wd_frag) && a.L[i].taps == 9 &&
-        (a.L[i].cout != a.L[i].cin || (a.L[i].cout != 128 && a.L[i].cout != 256)))
-      return hipErrorInvalidValue;
-    const int tiles = a.L[i].taps * ((a.L[i].cout + 63) / 64) * ((a.L[i].cin + 63) / 64);
+    const hipError_t e = parse_refresh_row(table + 20 * i, a.L[i]);
+    if (e != hipSuccess) return e;
+    const int tiles = refresh_tiles(a.L[i]);
     if (tiles > maxtotal) maxtotal = tiles;
   }
   const int blocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
   hipLaunchKernelGGL(weight_refresh_kernel, dim3(blocks, n), dim3(256), 0, s, a, lr, decay, step);
+  return hipGetLastError();
+}
+
+// The fused gradient pass 2 + optimizer + refresh (grad_update_kernel).  table: n rows of
+// GU_COLS int64 = the 20 weight_refresh columns, then {slab, bpart, splits, Mpad, KP,
+// bchunks, w_off, b_off, pos_off} (slab / bpart 0: the layer's gradient is read from G / G16).
+// plain_off / plain_n: a flat range updated from G only (the head).  tickets: n + 1 zeroed
+// uint32 (left zeroed).  Same block count per layer as dg_weight_refresh (the fp8 |w| max
+// slots).
+constexpr int GU_COLS = 29;
+int dg_grad_update_cols() { return GU_COLS; }
+hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
+                          float* P, float* G, const void* G16, float* MS, float rms_decay,
+                          float gscale, const float* gate, double* lr, double decay,
+                          long long* step, unsigned* tickets, int* bad_steps, hipStream_t s) {
+  if (n <= 0 || n > MAX_GU || !P || !G || !lr || !tickets || plain_n < 0)
+    return hipErrorInvalidValue;
+  GUArgs a;
+  a.n = n;
+  int maxtotal = 1;
+  for (int i = 0; i < n; ++i) {
+    const long long* t = table + GU_COLS * i;
+    WRefreshLayer& L = a.L[i];
+    const hipError_t e = parse_refresh_row(t, L);
+    if (e != hipSuccess) return e;
+    if (L.cout > 256 || L.cout % 4 != 0) return hipErrorInvalidValue;
+    GUSrc& S = a.S[i];
+    S.slab = (const float*)t[20];
+    S.bpart = (const float*)t[21];
+    S.splits = (int)t[22];
+    S.Mpad = (int)t[23];
+    S.KP = (int)t[24];
+    S.bchunks = (int)t[25];
+    S.w_off = t[26];
+    S.b_off = t[27];
+    S.pos_off = t[28];
+    if (S.slab && (S.splits <= 0 || S.Mpad < L.cout || S.KP < L.taps * L.cinp))
+      return hipErrorInvalidValue;
+    if (S.bpart && S.bchunks <= 0) return hipErrorInvalidValue;
+    if (L.w != P + S.w_off || L.bias != P + S.b_off || L.posb != P + S.pos_off)
+      return hipErrorInvalidValue;   // the refresh row must describe the same parameters
+    const int tiles = refresh_tiles(L);
+    if (tiles > maxtotal) maxtotal = tiles;
+  }
+  a.plain_off = plain_off;
+  a.plain_n = plain_n;
+  a.P = P;
+  a.G = G;
+  a.G16 = (const bf16_t*)G16;
+  a.MS = MS;
+  a.rms_decay = rms_decay;
+  a.gscale = gscale;
+  a.gate = gate;
+  a.lr = lr;
+  a.decay = decay;
+  a.step = step;
+  a.tickets = tickets;
+  a.bad_steps = bad_steps;
+  const int blocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
+  if (blocks * (n + 1) >= 0x10000) return hipErrorInvalidValue;   // the packed grid ticket
+  hipLaunchKernelGGL(grad_update_kernel, dim3(blocks, n + 1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

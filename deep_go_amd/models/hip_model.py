@@ -119,6 +119,12 @@ class HipGoNet:
         # non-finite loss guard (cfg.nan_policy == "skip"): device gate read by the optimizer
         self.gate = torch.ones(1, dtype=torch.float32, device=dev)
         self.bad_steps = torch.zeros(1, dtype=torch.int32, device=dev)
+        # fused end of step (grad_update): per-layer + grid tickets, zero between launches
+        self.gu_tickets = torch.zeros(cfg.numLayers + 1, dtype=torch.int32, device=dev)
+        # True while a step is issued whose gradient pass 2 is deferred into the fused update
+        # (train_step / SegmentedStep's whole-step graph; see can_defer)
+        self._defer = False
+        self._red_src = {}    # layer -> (slab, bpart, splits, Mpad, KP, bchunks) of its pass 2
 
         # ---- per-layer plans + bf16 operand weights ----
         self.plans: List[ConvPlan] = []
@@ -506,6 +512,7 @@ class HipGoNet:
             red = (slab, G + spec.w_off * f4, p.splits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
                    p.cin, p.cinp, bpart, self.bchunks, G + spec.pos_off * f4,
                    G + spec.b_off * f4)
+            self._red_src[i] = (slab, bpart, p.splits, p.Mpad_w, p.KPw, self.bchunks)
             if self.grads16 is not None:
                 ops.append((h.wgrad_reduce_w, red + (self._g16(spec.w_off),
                                                      self._g16(spec.pos_off),
@@ -976,6 +983,7 @@ class HipGoNet:
                              + ([self._g16(spec.w_off), self._g16(spec.pos_off),
                                  self._g16(spec.b_off)] if self.grads16 is not None else []))
                 self.plans[i].splits = S
+                self._red_src[i] = (slab, bpart, S, p0.Mpad_w, p0.KPw, self.bchunks_g)
                 # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
                 # launches all three passes for the whole group
                 self._bwd[i][0:3] = [(self._noop, ())] * 3
@@ -1148,7 +1156,7 @@ class HipGoNet:
         so with a side stream the weight-gradient chain runs beside the dgrad chain — the
         critical path is the dgrad sequence, and each kernel's ramp/tail is filled by the
         other stream's work.  Callers end the backward with ``join_side()``."""
-        ops = self._bwd[i]
+        ops = self._layer_ops(i)
         main = torch.cuda.current_stream()
         if self.side_mode == "none":
             self._run(ops[:3], main.cuda_stream)
@@ -1169,13 +1177,44 @@ class HipGoNet:
                 # third stream beside the grouped launch, is 5-6% slower at 12x128 and
                 # 0.3-1.6% at 12x256 — compute beside the window kernel slows it
                 if l0_side:
-                    self._run(self._l0_dgrad + self._bwd[0][:3], side.cuda_stream)
+                    self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
                 self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
                 fn()
         self._run(ops[3:], main.cuda_stream)
+
+    def _layer_ops(self, i: int):
+        """Layer i's backward ops [bias partial, wgrad, pass 2, (dgrad)]; with the step's
+        gradient pass 2 deferred into the fused update, the pass-2 launch (the slab reduce
+        that also finishes the bias gradients) is left out."""
+        ops = self._bwd[i]
+        if self._defer and len(ops) >= 3:
+            ops = ops[:2] + [(self._noop, ())] + ops[3:]
+        return ops
+
+    def can_defer(self) -> bool:
+        """Whether a training step may leave its gradients as split-K slabs and bias partials
+        for the fused update (grad_update: pass 2 + SGD / RMSProp + operand refresh + LR decay
+        in one launch) instead of reducing them first.  Needs a single-GPU step (a collective
+        needs the reduced gradient; the bf16 wire twin is a DP format), no gradient hooks, and
+        every layer's slabs / partials in buffers of their own: one grouped weight-gradient
+        launch, plus at most the first layer's own chain.  DG_FUSED_UPDATE=0: never (and the
+        optimizer keeps the separate SGD + refresh launches)."""
+        if os.environ.get("DG_FUSED_UPDATE", "1") == "0":
+            return False
+        if self.global_batch != self.B or self.grads16 is not None or self.grad_hooks:
+            return False
+        if len(self.wgroups) != 1:
+            return False
+        rest = set(range(len(self.plans))) - set(self.wgroups[0])
+        return rest <= {0} and all(i in self._red_src for i in range(len(self.plans)))
+
+    def set_defer(self, on: bool):
+        """Issue the following backward + optimizer_step with the gradient pass 2 deferred
+        into the fused update (see can_defer; ignored when it does not hold)."""
+        self._defer = bool(on) and self.can_defer()
 
     def join_side(self):
         self._flush_head_reduce(stream_handle())
@@ -1190,32 +1229,69 @@ class HipGoNet:
         f(*a, s)
 
     def optimizer_step(self, grad_scale: float = 1.0):
+        """The update: [finite gate] -> [fp8 scale update] -> ONE fused launch (grad_update:
+        the gradient's pass 2 when the step deferred it, SGD / RMSProp on every parameter,
+        the operand copies the next step reads, LR decay).  DG_FUSED_UPDATE=0: the separate
+        SGD / RMSProp and weight-refresh launches."""
         s = stream_handle()
         n = self.layout.numel
         gate = 0
+        slabs = self._defer
         # (bf16 wire: the optimizer reads the all-reduced bf16 twin)
         w16 = self.grads16 is not None
         g = self.grads16.data_ptr() if w16 else self.grads.data_ptr()
-        if self.cfg.nan_policy == "skip":
-            # gate = finite(gradients) [and finite(local loss) on one rank]: under DP every
-            # rank sees the same all-reduced gradient, so all ranks skip together
+        if self.cfg.nan_policy != "raise":
+            # gate = finite(loss) [and finite(gradients)]: under DP every rank sees the same
+            # all-reduced gradient, so all ranks skip together.  With the pass 2 deferred the
+            # gradient does not exist yet: the gate is the loss, and the fused update leaves
+            # any non-finite gradient entry unapplied (and counts the step in bad_steps)
             dp = self.global_batch != self.B
             (self.h.finite_gate_bf16 if w16 else self.h.finite_gate)(
-                0 if dp else self.loss.data_ptr(), self.B, g, n, self.gate.data_ptr(),
-                self.bad_steps.data_ptr(), s)
+                0 if dp else self.loss.data_ptr(), self.B, 0 if slabs else g,
+                0 if slabs else n, self.gate.data_ptr(), self.bad_steps.data_ptr(), s)
             gate = self.gate.data_ptr()
-        if self.ms is not None:
-            (self.h.rmsprop_bf16 if w16 else self.h.rmsprop)(
-                self.params.data_ptr(), g, self.ms.data_ptr(), n, self.lr.data_ptr(),
-                float(self.cfg.rmsprop_decay), grad_scale, gate, s)
-        else:
-            (self.h.sgd_bf16 if w16 else self.h.sgd)(self.params.data_ptr(), g, n,
-                                                     self.lr.data_ptr(), grad_scale, gate, s)
         self._fp8_update(s)
-        # bf16 (+ e4m3) operand copies of the updated weights + lr *= (1 - rateDecay)
-        t = self._step_refresh_table()
-        self.h.weight_refresh_decay(t.ctypes.data, len(t), self.lr.data_ptr(),
-                                    float(self.cfg.rateDecay), self.step_count.data_ptr(), s)
+        if os.environ.get("DG_FUSED_UPDATE", "1") == "0":
+            if self.ms is not None:
+                (self.h.rmsprop_bf16 if w16 else self.h.rmsprop)(
+                    self.params.data_ptr(), g, self.ms.data_ptr(), n, self.lr.data_ptr(),
+                    float(self.cfg.rmsprop_decay), grad_scale, gate, s)
+            else:
+                (self.h.sgd_bf16 if w16 else self.h.sgd)(self.params.data_ptr(), g, n,
+                                                         self.lr.data_ptr(), grad_scale, gate, s)
+            # bf16 (+ e4m3) operand copies of the updated weights + lr *= (1 - rateDecay)
+            t = self._step_refresh_table()
+            self.h.weight_refresh_decay(t.ctypes.data, len(t), self.lr.data_ptr(),
+                                        float(self.cfg.rateDecay), self.step_count.data_ptr(), s)
+            return
+        t = self._gu_table(slabs)
+        hd = self.head
+        self.h.grad_update(t.ctypes.data, len(t), hd.w_off, n - hd.w_off,
+                           self.params.data_ptr(), self.grads.data_ptr(),
+                           self.grads16.data_ptr() if w16 else 0,
+                           self.ms.data_ptr() if self.ms is not None else 0,
+                           float(self.cfg.rmsprop_decay), grad_scale, gate, self.lr.data_ptr(),
+                           float(self.cfg.rateDecay), self.step_count.data_ptr(),
+                           self.gu_tickets.data_ptr(), self.bad_steps.data_ptr(), s)
+
+    def _gu_table(self, slabs: bool) -> np.ndarray:
+        """grad_update's table: the per-step refresh row of every conv layer + where its
+        gradient comes from (slabs: the split-K slabs / bias partials of its pass 2; else the
+        flat gradient) and its parameter offsets."""
+        key = "_gu_tab_slabs" if slabs else "_gu_tab_grads"
+        t = getattr(self, key, None)
+        if t is None:
+            ref = self._step_refresh_table()
+            rows = []
+            for r, p in zip(ref, self.plans):
+                spec = self.layout.layers[p.index]
+                src = self._red_src[p.index] if slabs else (0, 0, 0, 0, 0, 0)
+                rows.append([int(x) for x in r] + [int(x) for x in src]
+                            + [spec.w_off, spec.b_off, spec.pos_off])
+            t = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+            assert t.shape[1] == self.h.grad_update_cols()
+            setattr(self, key, t)
+        return t
 
     def _op_pointers(self, exclude=()) -> set:
         """Every integer argument (and int64 table entry) of the launches the model issues:
@@ -1237,7 +1313,8 @@ class HipGoNet:
         # every int64 launch table the model holds (stack / dgrad-stack / layer-run / grouped
         # weight-gradient / fp8 copy-out tables), except the refresh tables (operand copies
         # are what _step_refresh_table decides about) and any passed in `exclude`
-        skip = {id(getattr(self, "_refresh_table", None)), id(getattr(self, "_step_refresh", None))}
+        skip = {id(getattr(self, "_refresh_table", None)), id(getattr(self, "_step_refresh", None)),
+                id(getattr(self, "_gu_tab_slabs", None)), id(getattr(self, "_gu_tab_grads", None))}
         skip.update(id(t) for t in exclude)
         for name, v in vars(self).items():
             for t in (v if isinstance(v, (list, tuple)) else [v]):
@@ -1298,8 +1375,14 @@ class HipGoNet:
         self._fp8_calibrated = True
 
     def train_step(self):
-        self.forward_backward()
-        self.optimizer_step()
+        """forward + backward + update; the gradient pass 2 deferred into the fused update
+        when can_defer() holds (self.grads is then written by that launch)."""
+        self.set_defer(True)
+        try:
+            self.forward_backward()
+            self.optimizer_step()
+        finally:
+            self._defer = False
 
     # ------------------------------------------------------------------ helpers
     def mean_loss(self) -> torch.Tensor:
@@ -1465,11 +1548,16 @@ class SegmentedStep:
                 assert net.launches > n0, "segment capture recorded no launch"
                 self.graphs.append(g)
             if self.mode == "graph":
+                # the whole step: its gradient pass 2 deferred into the fused update
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for fns, _ in self.segments:
-                        self._call_all(fns)
-                    self.net.optimizer_step()
+                net.set_defer(True)
+                try:
+                    with torch.cuda.graph(g):
+                        for fns, _ in self.segments:
+                            self._call_all(fns)
+                        self.net.optimizer_step()
+                finally:
+                    net.set_defer(False)
                 self.full_graph = g
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -1514,6 +1602,16 @@ class SegmentedStep:
         if self.full_graph is not None:
             with trace.range("step_graph"):
                 self.full_graph.replay()
+            return
+        if not self.use_graphs and self.bucketer is None:
+            # eager whole step: the same launches as the whole-step graph
+            self.net.set_defer(True)
+            try:
+                for fns, _ in self.segments:
+                    self._call_all(fns)
+                self.net.optimizer_step()
+            finally:
+                self.net.set_defer(False)
             return
         self.forward_backward()
         self.optimizer()

@@ -494,6 +494,92 @@ def test_grouped_wgrads_match_per_layer(layers, group, ch, dstack, win, monkeypa
     assert torch.allclose(n0.grads, n1.grads, rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("layers,ch,dtype,opt", [
+    (12, 128, "bf16", "sgd"), (12, 256, "bf16", "sgd"), (6, 128, "fp8", "sgd"),
+    (5, 256, "fp8", "sgd"), (5, 128, "bf16", "rmsprop"), (4, 64, "bf16", "sgd")])
+def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypatch):
+    """grad_update (elementwise.hip): the gradient pass 2 read straight from the split-K slabs
+    and bias partials + SGD / RMSProp + operand refresh + LR decay in ONE launch, against the
+    separate slab-reduce / SGD / refresh launches (DG_FUSED_UPDATE=0).  Same fixed summation
+    order and update expressions: parameters, gradients, every operand copy and the LR are
+    bit-identical after 3 steps (eager, then graph-replayed)."""
+    from deep_go_amd.models.hip_model import SegmentedStep
+    kw = dict(dtype=dtype, rateDecay=1e-3)
+    if opt == "rmsprop":
+        kw.update(optimizer="rmsprop", rate=1e-3)
+    nets = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DG_FUSED_UPDATE", fused)
+        nets.append(_setup(layers, ch, 4, seed=2, **kw)[1])
+    net0, net1 = nets
+    assert net1.can_defer() and not net0.can_defer()
+
+    def copies(n):
+        return [t for t in (*n.wfrag, *n.wdfrag, *n.wf8frag, *n.wd8frag, *n.pbias_frag,
+                            *n.pbias) if t is not None]
+
+    def check():
+        torch.cuda.synchronize()
+        assert torch.equal(net0.params, net1.params)
+        assert torch.equal(net0.grads, net1.grads)
+        assert net0.lr.item() == net1.lr.item()
+        assert int(net0.step_count.item()) == int(net1.step_count.item())
+        for a, b in zip(copies(net0), copies(net1)):
+            assert torch.equal(a, b)
+        if dtype == "fp8":
+            assert torch.equal(net0.fp8_scales, net1.fp8_scales)
+        assert int(net1.gu_tickets.abs().sum().item()) == 0    # tickets left zeroed
+    for _ in range(3):
+        monkeypatch.setenv("DG_FUSED_UPDATE", "0")
+        net0.train_step()
+        monkeypatch.setenv("DG_FUSED_UPDATE", "1")
+        net1.train_step()
+    check()
+    steps = []
+    for fused, net in (("0", net0), ("1", net1)):
+        monkeypatch.setenv("DG_FUSED_UPDATE", fused)
+        steps.append(SegmentedStep(net, None, use_graphs=True))
+    for _ in range(2):
+        monkeypatch.setenv("DG_FUSED_UPDATE", "0")
+        steps[0]()
+        monkeypatch.setenv("DG_FUSED_UPDATE", "1")
+        steps[1]()
+    check()
+
+
+def test_fused_update_skips_non_finite_gradient_entries():
+    """With the pass 2 deferred the gradient does not exist before the update: a non-finite
+    gradient entry is left unapplied (that parameter keeps its value), the step is counted
+    in bad_steps, every other parameter still updates."""
+    cfg, net, _ = _setup(4, 128, 4, seed=1)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    g_ref = net.grads.clone()
+    p0 = net.params.clone()
+    # poison one slab entry of a hidden layer's pass 2 (the group's slab region)
+    i = net.wgroups[0][0]
+    slab, _, S, Mpad, KP, _ = net._red_src[i]
+    spec = net.layout.layers[i]
+    net.set_defer(True)
+    try:
+        net.forward_backward()
+        torch.cuda.synchronize()
+        view = torch.as_strided(net.gslab, (1,), (1,),
+                                (slab - net.gslab.data_ptr()) // 4)
+        view.fill_(float("nan"))        # co 0, tap 0, ci 0 of the first split
+        net.optimizer_step()
+    finally:
+        net._defer = False
+    torch.cuda.synchronize()
+    w0 = spec.w_off
+    assert torch.isnan(net.grads[w0])
+    assert net.params[w0].item() == p0[w0].item()
+    assert torch.isfinite(net.params).all()
+    assert net.bad_steps.item() == 1
+    moved = (net.params - p0).abs() > 0
+    assert moved.sum().item() > 0.9 * (g_ref != 0).sum().item()
+
+
 def test_lr_decay_fused_into_weight_refresh():
     """lr_t = lr0 * (1 - decay)^t (optimizer.lua:25-26), applied by the refresh launch."""
     cfg, net, data = _setup(3, 64, 4, rateDecay=1e-3)
