@@ -37,7 +37,7 @@ hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, cons
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, hipStream_t stream);
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
-hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
+hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
@@ -84,6 +84,11 @@ void dg_conv_wgrad_win_set_swp(int on);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void* X, void* Y,
                           void* mask, int C, int B, hipStream_t stream);
+hipError_t dg_conv_layer2_multi_head(const long long* table, int nl, int B, const float* w,
+                                     const float* bias, const float* posb, const int* labels,
+                                     float* loss, int* pred, void* dZ, float* gw_part,
+                                     float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream);
 hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
                                 hipStream_t stream);
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
@@ -258,26 +263,26 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_wgrad_win8_splits", [](int nl, int M, int Cx, int B, int num_cus) {
     return dg_conv_wgrad_win8_splits(nl, M, Cx, B, num_cus);
   });
-  m.def("conv_stack_f8_fwd_head", [](uintptr_t table, int nl, uintptr_t X0,
+  m.def("conv_stack_f8_fwd_head", [](int C, uintptr_t table, int nl, uintptr_t X0,
                                      uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t w,
                                      uintptr_t bias, uintptr_t posb, uintptr_t labels,
                                      uintptr_t loss, uintptr_t pred, uintptr_t dZ,
                                      uintptr_t gw_part, uintptr_t dzb, int head_relu,
                                      float grad_scale, uintptr_t stream) {
-    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+    check(dg_conv_stack_f8_fwd_head(C, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
                                     P<unsigned>(amax_x0), B, P<float>(w), P<float>(bias),
                                     P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
                                     P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
                                     grad_scale, nullptr, S(stream)),
           "conv_stack_f8_fwd_head");
-  }, "fp8 forward stack + the fused 3x3/128 policy head");
-  m.def("conv_stack_f8_fwd_head_y8", [](uintptr_t table, int nl, uintptr_t X0,
+  }, "fp8 forward stack + the fused 3x3 policy head (C = 128 | 256)");
+  m.def("conv_stack_f8_fwd_head_y8", [](int C, uintptr_t table, int nl, uintptr_t X0,
                                      uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t w,
                                      uintptr_t bias, uintptr_t posb, uintptr_t labels,
                                      uintptr_t loss, uintptr_t pred, uintptr_t dZ,
                                      uintptr_t gw_part, uintptr_t dzb, int head_relu,
                                      float grad_scale, uintptr_t y8, uintptr_t stream) {
-    check(dg_conv_stack_f8_fwd_head(P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+    check(dg_conv_stack_f8_fwd_head(C, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
                                     P<unsigned>(amax_x0), B, P<float>(w), P<float>(bias),
                                     P<float>(posb), P<int>(labels), P<float>(loss), P<int>(pred),
                                     P<void>(dZ), P<float>(gw_part), P<float>(dzb), head_relu,
@@ -509,6 +514,17 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_layer2");
   }, "one hidden 3x3 C -> C layer (C = 256 | 128) on conv_stack2's K loop: epi 1 forward "
      "(fragment weights, pbias_frag, mask written), 2 backward-data (mask of the layer below)");
+  m.def("conv_layer2_multi_head", [](uintptr_t table, int nl, int B, uintptr_t w,
+                                     uintptr_t bias, uintptr_t posb, uintptr_t labels,
+                                     uintptr_t loss, uintptr_t pred, uintptr_t dZ,
+                                     uintptr_t gw_part, uintptr_t dzb, int head_relu,
+                                     float grad_scale, uintptr_t stream) {
+    check(dg_conv_layer2_multi_head(P<long long>(table), nl, B, P<float>(w), P<float>(bias),
+                                    P<float>(posb), P<int>(labels), P<float>(loss),
+                                    P<int>(pred), P<void>(dZ), P<float>(gw_part),
+                                    P<float>(dzb), head_relu, grad_scale, S(stream)),
+          "conv_layer2_multi_head");
+  }, "d = 256 forward run + the fused 3x3/256 policy head on its last output");
   m.def("conv_layer2_multi", [](int epi, uintptr_t table, int nl, int C, int B,
                                uintptr_t stream) {
     check(dg_conv_layer2_multi(epi, P<long long>(table), nl, C, B, S(stream)),

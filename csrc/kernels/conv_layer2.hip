@@ -17,6 +17,7 @@
 // Reference ops: SpatialConvolutionMM + Add + ReLU (experiments.lua:137-147) and their
 // backward (train.lua:10).
 #include "dg_common.h"
+#include "head_body.h"
 
 #include <cstdlib>
 
@@ -246,12 +247,18 @@ constexpr int MAXL2 = 16;
 struct MultiArgs {
   LayerArgs L[MAXL2];
   int nl;
+  dghead::HeadMArgs head;   // HEAD: the policy head on the run's last output (X = last Y)
 };
 constexpr int STG_OFF = H_BYTES;                       // epilogue staging: buffer 1 + ext
 constexpr int LDS_MULTI = H_BYTES + NPTS * 256;        // 149760 B
 static_assert(LDS_MULTI <= 160 * 1024, "LDS");
+static_assert(dghead::frame_head_lds(256) <= LDS_MULTI, "fused head LDS");
 
-template <int EPI, int BPF>
+// HEAD (forward, C = 256): after the run's last layer the workgroup runs the policy head of
+// its board (head_body.h: forward, log-softmax / NLL / argmax, and the head's backward) on
+// the output frame it has just written — no separate head launch (its 56 us at 12x256 sat
+// between the forward and backward-data runs) and the frame is read back from L2 / MALL.
+template <int EPI, int BPF, bool HEAD>
 __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -434,18 +441,23 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
     lds_barrier();
     staged = pf_next;
   }
+  if constexpr (HEAD) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // this workgroup's last-layer stores retired
+    __syncthreads();
+    dghead::head_from_frame<256>(m.head, b, smem);
+  }
 }
 
-template <int EPI, int BPF>
+template <int EPI, int BPF, bool HEAD = false>
 hipError_t launch_layer2_multi(const MultiArgs& m, int B, hipStream_t stream) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI, BPF>,
+    (void)hipFuncSetAttribute((const void*)conv_layer2_multi_kernel<EPI, BPF, HEAD>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MULTI);
     done = true;
   }
-  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI, BPF>), dim3(B), dim3(NT), LDS_MULTI, stream,
-                     m);
+  hipLaunchKernelGGL((conv_layer2_multi_kernel<EPI, BPF, HEAD>), dim3(B), dim3(NT), LDS_MULTI,
+                     stream, m);
   return hipGetLastError();
 }
 
@@ -472,10 +484,13 @@ hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void*
 }
 
 // nl layers in one launch: table = nl rows of {A, pbias, X, Y, mask} (int64); row l + 1's X
-// must be row l's Y (checked).  C = 256 | 128 as above.
-hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
-                                hipStream_t stream) {
+// must be row l's Y (checked).  C = 256 | 128 as above.  head (forward, C = 256 only, or
+// null): the fused policy head on the last Y (head->X is set here).
+static hipError_t layer2_multi(int epi, const long long* table, int nl, int C, int B,
+                               const dghead::HeadMArgs* head, hipStream_t stream) {
   if ((C != 128 && C != 256) || B <= 0 || nl <= 0 || nl > MAXL2) return hipErrorInvalidValue;
+  if (head && (epi != EPI_FWD || C != 256 || !head->dZ || !head->gw_part || !head->dzb))
+    return hipErrorInvalidValue;
   MultiArgs m{};
   m.nl = nl;
   for (int i = 0; i < nl; ++i) {
@@ -488,9 +503,30 @@ hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, 
     if (epi == EPI_DGRAD && !a.mask) return hipErrorInvalidValue;
     if (i > 0 && a.X != m.L[i - 1].Y) return hipErrorInvalidValue;
   }
+  if (head) {
+    m.head = *head;
+    m.head.X = m.L[nl - 1].Y;
+    return launch_layer2_multi<EPI_FWD, 1, true>(m, B, stream);
+  }
   if (epi == EPI_FWD) return launch_layer2_multi<EPI_FWD, 1>(m, B, stream);
   if (epi == EPI_DGRAD) return launch_layer2_multi<EPI_DGRAD, 1>(m, B, stream);
   return hipErrorInvalidValue;
+}
+
+hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
+                                hipStream_t stream) {
+  return layer2_multi(epi, table, nl, C, B, nullptr, stream);
+}
+
+// the forward run + the fused policy head (3x3 / 256-channel head on the run's last output)
+hipError_t dg_conv_layer2_multi_head(const long long* table, int nl, int B, const float* w,
+                                     const float* bias, const float* posb, const int* labels,
+                                     float* loss, int* pred, void* dZ, float* gw_part,
+                                     float* dzb, int head_relu, float grad_scale,
+                                     hipStream_t stream) {
+  const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
+                            gw_part, dzb, head_relu, grad_scale};
+  return layer2_multi(EPI_FWD, table, nl, 256, B, &h, stream);
 }
 
 }  // extern "C"

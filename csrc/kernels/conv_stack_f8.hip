@@ -539,6 +539,17 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     }
     if (a.fuse_head) dghead::head_body<C>(a.head, b, sI, smem, [](int) {});
   }
+  if constexpr (C == 256 && EPI == EPI_FWD) {
+    // the 256-channel image does not stay in LDS as bf16: the fused head reads the last
+    // layer's bf16 frame back (this workgroup's stores, retired here) — no head launch
+    if (a.fuse_head) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
+      dghead::HeadMArgs h = a.head;
+      h.X = a.L[a.nl - 1].Y;
+      dghead::head_from_frame<256>(h, b, smem);
+    }
+  }
 }
 
 int g_f8_mode = 0;
@@ -584,7 +595,7 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
                      const long long* y8, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || B <= 0 || !s_x0 || !amax_x0) return hipErrorInvalidValue;
   if ((C != 128 && C != 256) || (epi != EPI_FWD && epi != EPI_DGRAD)) return hipErrorInvalidValue;
-  if (head && (C != 128 || epi != EPI_FWD)) return hipErrorInvalidValue;
+  if (head && epi != EPI_FWD) return hipErrorInvalidValue;
   F8Args a;
   a.X0 = (const char*)X0;
   a.s_x0 = s_x0;
@@ -633,7 +644,8 @@ hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, cons
   return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, y8, stream);
 }
 
-hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void* X0,
+// C = 128: the head on the last layer's LDS image; 256: on its bf16 frame, read back
+hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
                                      float* loss, int* pred, void* dZ, float* gw_part,
@@ -641,7 +653,7 @@ hipError_t dg_conv_stack_f8_fwd_head(const long long* table, int nl, const void*
                                      const long long* y8, hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return f8_launch(128, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, y8, stream);
+  return f8_launch(C, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, y8, stream);
 }
 
 }  // extern "C"

@@ -297,5 +297,30 @@ DG_DEV void head_body(const HeadMArgs& a, int b, char* sX, char* scratch, StageF
   }  // halves
 }
 
+// The head for board b on the activation frame a.X in global memory (the standalone
+// head_mfma kernel, and the forward launches at d = 256 that run it after their last layer:
+// conv_layer2_multi / conv_stack_f8, whose 256-channel image does not stay in LDS): channel
+// half hf staged by LDS-DMA into the two-image layout at smem, scratch after it (2 HB +
+// scratch_bytes(C) of LDS).  The caller has retired its own stores to a.X (vmcnt(0)) and
+// synchronised the workgroup.
+template <int C>
+DG_DEV void head_from_frame(const HeadMArgs& a, int b, char* smem) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const char* Xb = a.X + (size_t)b * FF * C * 2;
+  auto stage = [&](int hf) {
+    for (int j = wave; j < 2 * (HROWS / 8); j += HT / 64) {
+      const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
+      const int rl = jj * 8 + (lane >> 3);
+      const int r = rl < FF ? rl : FF - 1;  // rows 441.. duplicate the (zero) border row 440
+      const int g = (lane & 7) ^ fsig(rl);
+      glds16(Xb + ((size_t)r * C + hf * 128 + c * 64 + g * 8) * 2,
+             (LDS_AS void*)(smem + c * HB + jj * 1024));
+    }
+  };
+  stage(0);
+  head_body<C>(a, b, smem, smem + 2 * HB, stage);
+}
+constexpr size_t frame_head_lds(int C) { return 2 * (size_t)HB + scratch_bytes(C); }
 
 }  // namespace dghead

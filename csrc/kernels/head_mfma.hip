@@ -35,31 +35,14 @@ namespace {
 template <int C>
 __global__ void __launch_bounds__(HT) head_mfma_kernel(HeadMArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sX = smem;  // 2 images, then the head scratch
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const char* Xb = a.X + (size_t)b * FF * C * 2;
-  // ---- stage: image of channel half hf (LDS-DMA, swizzled) ----
-  auto stage = [&](int hf) {
-    for (int j = wave; j < 2 * (HROWS / 8); j += 8) {
-      const int c = j / (HROWS / 8), jj = j - c * (HROWS / 8);
-      const int rl = jj * 8 + (lane >> 3);
-      const int r = rl < FF ? rl : FF - 1;  // rows 441.. duplicate the (zero) border row 440
-      const int g = (lane & 7) ^ fsig(rl);
-      glds16(Xb + ((size_t)r * C + hf * 128 + c * 64 + g * 8) * 2,
-             (LDS_AS void*)(sX + c * HB + jj * 1024));
-    }
-  };
-  stage(0);
-  head_body<C>(a, b, sX, smem + 2 * HB, stage);
+  head_from_frame<C>(a, blockIdx.x, smem);
 }
 
 }  // namespace
 
 template <int C>
 static hipError_t launch(int B, const HeadMArgs& a, hipStream_t stream) {
-  constexpr size_t lds = 2 * (size_t)HB + T * C * 2 + T * C * 4 + 384 * 4 + DZN * 4 + 32 * 4;
+  constexpr size_t lds = frame_head_lds(C);
   static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;
   if (!done) {

@@ -459,23 +459,27 @@ class HipGoNet:
         # last hidden layer (its image is already in LDS; conv_stack2.hip + head_body.h);
         # evaluation keeps the standalone head.  DG_FUSE_HEAD=0 keeps the separate launch.
         self._fwd_train = self._fwd
-        if (self.stack and self.stack[-1] == len(self.plans) - 1 and hd.k == 3
-                and hd.cin == 128 and hd.pad == 1 and self.dzp[-1] == 1
-                and os.environ.get("DG_FUSE_HEAD", "1") != "0"):
+        head_ok = (hd.k == 3 and hd.pad == 1 and self.dzp[-1] == 1
+                   and os.environ.get("DG_FUSE_HEAD", "1") != "0")
+        head_tail = (P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
+                     self.labels.data_ptr(), self.loss.data_ptr(), self.pred.data_ptr(),
+                     self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
+                     self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch)
+        last = len(self.plans) - 1
+        if (head_ok and self.stack and self.stack[-1] == last
+                and (hd.cin == 128 or (hd.cin == 256 and self.stack_fp8))):
             first = self.stack[0]
             fused = (h.conv_stack2_fwd_head, (
                 self._stack_table.ctypes.data, len(self._stack_table),
-                self._stack_x0.data_ptr(), int(self.stack_l1), self.B,
-                P + hd.w_off * f4, P + hd.b_off * f4,
-                P + hd.pos_off * f4, self.labels.data_ptr(), self.loss.data_ptr(),
-                self.pred.data_ptr(), self.dz[-1].data_ptr(), self.head_gw_part.data_ptr(),
-                self.head_dzb.data_ptr(), int(self.cfg.head_relu), 1.0 / self.global_batch))
+                self._stack_x0.data_ptr(), int(self.stack_l1), self.B) + head_tail)
             if self.stack_fp8:
+                # C = 128: the head on the last layer's LDS image; C = 256: on its bf16 frame,
+                # read back at the end of the same launch (conv_stack_f8.hip)
                 S, AM = self.fp8_scales.data_ptr(), self.fp8_amax.data_ptr()
                 fused = (h.conv_stack_f8_fwd_head, (
-                    self._stack_table.ctypes.data, len(self.stack),
+                    hd.cin, self._stack_table.ctypes.data, len(self.stack),
                     self.act[first - 1].data_ptr(), S + 4 * (2 * (first - 1) + 1),
-                    AM + 4 * (first - 1), self.B) + fused[1][5:])
+                    AM + 4 * (first - 1), self.B) + head_tail)
                 if self.fp8_wgrad:
                     fused = (h.conv_stack_f8_fwd_head_y8, fused[1] + (self._fwd_y8.ctypes.data,))
             elif self.stack_l1 and self._stack_x0 is self.x0:
@@ -486,15 +490,26 @@ class HipGoNet:
                 fused = (h.conv_stack2_fwd_head_x, (
                     self._stack_table.ctypes.data, len(self._stack_table), self.x0.data_ptr(),
                     self.B, self.planes.data_ptr(), self.player.data_ptr(),
-                    self.rank.data_ptr()) + fused[1][5:])
+                    self.rank.data_ptr()) + head_tail)
                 self._pre_train = [op for op in self._pre if op[0] is not h.expand_features]
             self._fwd_train = [fused if f in (h.conv_stack2_fwd, h.conv_stack_f8,
                                               h.conv_stack_f8_y8) else (f, a)
                                for f, a in self._fwd]
-            if any(f in (h.conv_stack2_fwd_head, h.conv_stack2_fwd_head_x,
-                         h.conv_stack_f8_fwd_head, h.conv_stack_f8_fwd_head_y8)
-                   for f, _ in self._fwd_train):
-                self._head_train = (self._noop, ())
+        elif (head_ok and hd.cin == 256 and self._fwd
+              and self._fwd[-1][0] is h.conv_layer2_multi
+              and self._fwd[-1][1][0] == h.EPI_FWD
+              and any(t.ctypes.data == self._fwd[-1][1][1]
+                      and int(t[-1, 3]) == self.act[-1].data_ptr() for t in self._l2_tables)):
+            # d = 256 bf16: the policy head at the end of the forward run's launch
+            # (conv_layer2_multi HEAD: each board's head on the frame its workgroup just wrote)
+            _, a = self._fwd[-1]
+            self._fwd_train = self._fwd[:-1] + [(h.conv_layer2_multi_head,
+                                                 (a[1], a[2], self.B) + head_tail)]
+        if any(f in (h.conv_stack2_fwd_head, h.conv_stack2_fwd_head_x,
+                     h.conv_stack_f8_fwd_head, h.conv_stack_f8_fwd_head_y8,
+                     h.conv_layer2_multi_head)
+               for f, _ in self._fwd_train):
+            self._head_train = (self._noop, ())
         for p in self.plans:
             spec = lay.layers[p.index]
             i = p.index

@@ -448,6 +448,33 @@ def test_head_fused_into_forward_stack(layers, monkeypatch):
     assert torch.equal(n1.eval_loss, n1.loss)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_head_fused_into_d256_forward(dtype, monkeypatch):
+    """d = 256: the policy head runs at the end of the forward launch (conv_layer2_multi HEAD
+    for bf16, conv_stack_f8 for fp8) on the last layer's frame its workgroup just wrote —
+    the standalone MFMA head's loss, predictions, dZ and gradients bit for bit, and no head
+    launch in the training step."""
+    monkeypatch.setenv("DG_FUSE_HEAD", "0")
+    _, n0, _ = _setup(5, 256, 4, seed=13, dtype=dtype)
+    monkeypatch.setenv("DG_FUSE_HEAD", "1")
+    _, n1, _ = _setup(5, 256, 4, seed=13, dtype=dtype)
+    if dtype == "fp8":
+        n0.fp8_scales.copy_(n1.fp8_scales)
+        n0.fp8_gscales.copy_(n1.fp8_gscales)
+    want = n1.h.conv_stack_f8_fwd_head_y8 if dtype == "fp8" else n1.h.conv_layer2_multi_head
+    assert any(f is want for f, _ in n1._fwd_train)
+    assert n1._head_train[0] is n1._noop and n0._head_train[0] is not n0._noop
+    n0.forward_backward()
+    n1.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.equal(n0.loss, n1.loss) and torch.equal(n0.pred, n1.pred)
+    assert torch.equal(n0.dz[-1], n1.dz[-1])
+    assert torch.equal(n0.grads, n1.grads)
+    n1.evaluate()
+    torch.cuda.synchronize()
+    assert torch.equal(n1.eval_loss, n1.loss)
+
+
 @pytest.mark.parametrize("l0_mask", ["0", "1"])
 @pytest.mark.parametrize("layers", [5, 7])
 def test_fused_dgrad_stack_matches_per_layer(layers, l0_mask, monkeypatch):
