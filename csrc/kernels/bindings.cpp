@@ -62,14 +62,12 @@ hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int 
                             const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
 int dg_conv_wgrad_wgs_per_cu();
-void dg_conv_wgrad_set_t3(int on);
 int dg_conv_wgrad_ktile(int KP);
 int dg_conv_wgrad_wgs_per_cu_for(int KP);
 hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pad, int M,
                                int Mpad, int x_pad, int x_C, int B, int KP, int splits,
                                hipStream_t stream);
 int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
-void dg_conv_l1_set_nw(int nw);
 int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad);
 hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
                            void* Y, void* mask, const void* planes, const void* player,
@@ -78,9 +76,6 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
                       int x_C, int B, void* Y, int y_pad, const float* bias, const float* posb,
                       void* mask, const void* pbias, hipStream_t stream);
 void dg_conv_wgrad_win_set_ablate(int mode);
-void dg_conv_wgrad_win_set_pd(int pd);
-void dg_conv_wgrad_win_set_nw(int nw);
-void dg_conv_wgrad_win_set_swp(int on);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void* X, void* Y,
                           void* mask, int C, int B, hipStream_t stream);
@@ -117,7 +112,6 @@ hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int
 hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n, float* gw,
                           float* gbias, float* gposb, void* gw16, void* gbias16, void* gposb16,
                           hipStream_t stream);
-void dg_head_set_mfma(int on);
 hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                    const float* bias, const float* posb, const int* labels, float* loss,
                    int* pred, float* logp_out, void* dZ, int dz_pad, float* gw_part,
@@ -470,12 +464,8 @@ PYBIND11_MODULE(_dghip, m) {
      "operand refresh + LR decay (elementwise.hip grad_update_kernel)");
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
-  m.def("head_set_mfma", [](int on) { dg_head_set_mfma(on); },
-        "3x3/128- and 256-channel head on MFMA (head_mfma.hip, default) or the VALU kernel");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
-  m.def("conv_wgrad_set_t3", [](int on) { dg_conv_wgrad_set_t3(on); },
-        "three-slice (128 x 384) wgrad tiles on/off (default on)");
   m.def("conv_wgrad_multi", [](int kw, uintptr_t table, int nl, int dz_pad, int M, int Mpad,
                                int x_pad, int x_C, int B, int KP, int splits, uintptr_t stream) {
     check(dg_conv_wgrad_multi(kw, P<long long>(table), nl, dz_pad, M, Mpad, x_pad, x_C, B, KP,
@@ -490,8 +480,6 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_l1");
   }, "board-resident first-layer forward (conv_l1.hip): bias + position bias (fp32, or the "
      "bf16 pbias table when given) + ReLU");
-  m.def("conv_l1_set_nw", [](int nw) { dg_conv_l1_set_nw(nw); },
-        "conv_l1 workgroup: 4 waves / half a board, 2 per CU (default) or 8 waves / a board");
   m.def("conv_l1_ok", [](int kw, int x_pad, int x_C, int Mpad, int KP) {
     return dg_conv_l1_ok(kw, x_pad, x_C, Mpad, KP);
   });
@@ -540,12 +528,6 @@ PYBIND11_MODULE(_dghip, m) {
     return dg_conv_wgrad_win_splits(nl, M, Cx, B, num_cus);
   });
   m.def("conv_wgrad_win_set_ablate", [](int mode) { dg_conv_wgrad_win_set_ablate(mode); });
-  m.def("conv_wgrad_win_set_pd", [](int pd) { dg_conv_wgrad_win_set_pd(pd); },
-        "LDS-DMA prefetch distance of conv_wgrad_win in K-steps (2 or 4, default 4)");
-  m.def("conv_wgrad_win_set_swp", [](int on) { dg_conv_wgrad_win_set_swp(on); },
-        "software-pipelined conv_wgrad_win K-loop (default 0: measured slower with 4-wave workgroups)");
-  m.def("conv_wgrad_win_set_nw", [](int nw) { dg_conv_wgrad_win_set_nw(nw); },
-        "waves per conv_wgrad_win workgroup: 4 (64-co chunks, 2 per CU; default) or 8");
   m.def("conv_wgrad_ktile", [](int KP) { return dg_conv_wgrad_ktile(KP); });
   m.def("conv_wgrad_wgs_per_cu_for", [](int KP) { return dg_conv_wgrad_wgs_per_cu_for(KP); });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });

@@ -205,7 +205,6 @@ hipError_t launch_l1(const L1Args& a, int Mpad, hipStream_t stream) {
   return hipGetLastError();
 }
 
-int g_l1_nw = 4;
 
 // ---- the 5x5 / 40-channel first layer on the forward stack's K loop (conv_l1_frag) ----
 // The generic kernel above stages the weights through an LDS ring (one barrier per K-step)
@@ -408,13 +407,11 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
            (const bf16_t*)pbias};
   if (!pbias && (!bias || !posb)) return hipErrorInvalidValue;
   // 4-wave half-board workgroups when two fit on a CU
-  const bool w4 = g_l1_nw == 4 && 2 * (a.img_bytes + 2 * A_BYTES) <= 160 * 1024;
+  const bool w4 = 2 * (a.img_bytes + 2 * A_BYTES) <= 160 * 1024;
   if (kw == 5) return w4 ? launch_l1<5, 4>(a, Mpad, stream) : launch_l1<5, 8>(a, Mpad, stream);
   return w4 ? launch_l1<3, 4>(a, Mpad, stream) : launch_l1<3, 8>(a, Mpad, stream);
 }
 
-void dg_conv_l1_set_nw(int nw) { g_l1_nw = nw == 8 ? 8 : 4;
-}
 
 // conv_l1_frag: 5x5 over the [B][23][23][40] input frame -> [B][21][21][M] (pad 1), M a
 // multiple of 128; A = weight_refresh's fragment-ordered first-layer operand, pbias = its

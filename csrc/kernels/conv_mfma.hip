@@ -824,16 +824,9 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
 static int g_wgrad_ablate = 0;
 void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
 int dg_conv_wgrad_wgs_per_cu() { return 2; }
-static int g_wgrad_t3 = -1;
-static bool wgrad_t3_enabled() {
-  if (g_wgrad_t3 < 0) g_wgrad_t3 = 1;
-  return g_wgrad_t3 != 0;
-}
-void dg_conv_wgrad_set_t3(int on) { g_wgrad_t3 = on; }
-// k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K
-int dg_conv_wgrad_ktile(int KP) {
-  return (wgrad_t3_enabled() && KP % 384 == 0) ? 384 : 128;
-}
+// k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K: the
+// three-slice kernel wherever K is a multiple of 384
+int dg_conv_wgrad_ktile(int KP) { return KP % 384 == 0 ? 384 : 128; }
 int dg_conv_wgrad_wgs_per_cu_for(int KP) {
   return dg_conv_wgrad_ktile(KP) == 384 ? 1 : dg_conv_wgrad_wgs_per_cu();
 }

@@ -16,9 +16,9 @@
 // of the useful products.  Both operands are read with transposing LDS reads
 // (ds_read_b64_tr_b16): rows = pixels (K), columns = channels.
 //
-// Workgroup = 8 waves, tile 128 co x 9 taps x 64 ci (wave (wm, wn): 64 co x 9 taps x 16 ci,
-// 4 x 9 accumulator fragments); grid = layers x co-chunks x ci-chunks x pixel splits, one
-// workgroup per CU, XCD-remapped so the chunks of one (layer, split) share an L2.  Output:
+// Workgroup = 4 waves, tile 64 co x 9 taps x 64 ci (wave wn: 64 co x 9 taps x 16 ci, 4 x 9
+// accumulator fragments); grid = layers x co-chunks x ci-chunks x pixel splits, two
+// workgroups per CU, XCD-remapped so the chunks of one (layer, split) share an L2.  Output:
 // fp32 split slabs slab[z][co][t*Cx + ci] in the layout wgrad_reduce_multi sums.
 //
 // Reference semantics: SpatialConvolutionMM accGradParameters (experiments.lua:138, EXTERNAL
@@ -56,8 +56,6 @@ struct WinArgs {
 // {s..s+3, s+8..s+11} for ANY shift s (the 9 taps); this keeps its 256 B on 64 distinct
 // banks (checked exhaustively over s and the chunk pair).
 DG_DEV int xswz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
-// 256-B dZ rows (step-local, 8-aligned groups): same swizzle as conv_wgrad_kernel.
-DG_DEV int dswz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
 DG_DEV int step_g0(int s) {
   const int b = s / STEPS_PER_BOARD;
@@ -74,18 +72,18 @@ DG_DEV int step_g0(int s) {
 // new X block re-loads one that another wave loads, same bytes), so "DMAs of step st+1
 // landed" = vmcnt(2 (PD - 1)).
 //
-// NW: waves per workgroup.  8: 128-co chunks, one workgroup per CU; 4: 64-co chunks, two
-// independent workgroups per CU (their K-step barriers are not in lockstep, so one's LDS
-// reads overlap the other's MFMAs).  Every wave owns 64 co x 9 taps x 16 ci either way.
-template <int ABL, int PD, int NW, bool SWP>
+// NW = 4 waves per workgroup: 64-co chunks, two independent workgroups per CU (their K-step
+// barriers are not in lockstep, so one's LDS reads overlap the other's MFMAs); every wave
+// owns 64 co x 9 taps x 16 ci.  (Measured and removed in round 4: 8-wave / 128-co
+// workgroups, a software-pipelined K loop and prefetch distance 2 — all slower or equal,
+// profiles/r1_kbench_wgrad_win_v5_swp.json, r3_wgrad_win_stream_experiments.txt.)
+template <int ABL, int PD, int NW>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs a, WinLayers Ls) {
   static_assert(PD >= 1 && PD <= 4, "prefetch distance");
-  static_assert(NW == 4 || NW == 8, "waves");
+  static_assert(NW == 4, "waves");
   constexpr int COCH = 16 * NW;        // co per workgroup (64 or 128)
   constexpr int DZR = 2 * COCH;        // dZ LDS row bytes
   constexpr int DZB = 32 * DZR;        // one dZ step (32 rows); NW 1-KB blocks
-  constexpr int XPW = 8 / (NW / 4) / 4 * 1;  // X blocks per wave per step: NW 8 -> 1, 4 -> 2
-  static_assert(XPW * NW >= 8, "steady-state X blocks");
   __shared__ __attribute__((aligned(16))) char smem[XRING + (PD + 1) * DZB];
   char* xring = smem;
   char* dzbuf = smem + XRING;
@@ -95,7 +93,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;  // wm = 0 when NW = 4
+  const int wm = 0, wn = wave;
 
   const int nci = a.Cx / 64, nco = a.M / COCH;
   const int nwg = a.nl * nco * nci * a.splits;
@@ -131,37 +129,24 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
   // 32 dZ rows of step g0 into buffer buf: one 1-KB block per wave
   auto dz_block = [&](int buf, int g0) {
     if constexpr (ABL & 4) return;
-    int r, c;
-    if constexpr (NW == 8) {
-      r = wave * 4 + (lane >> 4);
-      c = (lane & 15) ^ dswz(r);
-    } else {
-      r = wave * 8 + (lane >> 3);
-      c = (lane & 7) ^ xswz(r);
-    }
+    const int r = wave * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ xswz(r);
     dma16(dZl + (size_t)(g0 + r) * Mb + c * 16,
           __builtin_amdgcn_readfirstlane(dz_u + buf * DZB + wave * 1024));
   };
   int loaded_hi = 0;
-  // steady-state issue for step sn into dZ buffer buf: exactly XPW + 1 DMAs per wave
+  // steady-state issue for step sn into dZ buffer buf: 2 DMAs per wave (3 at a board's
+  // first step)
   auto issue = [&](int sn, int buf) {
     const int g0n = step_g0(sn);
     int lo = (g0n - 22) & ~7;
     if (lo < loaded_hi) lo = loaded_hi;
     const int hi = (g0n + 54 + 7) & ~7;
     const int nblk = (hi - lo) >> 3;  // 4 .. 8 (4 inside a board, 7-8 across boards)
-    if constexpr (NW == 4) {
-      // 1 X block per wave inside a board, 2 at a board's first step (7-8 new blocks;
-      // a wave without an 8th block re-loads block 0, same bytes)
-      x_block(lo + 8 * wave);
-      if (nblk > 4) x_block(lo + 8 * (wave + 4 < nblk ? wave + 4 : 0));
-    } else {
-#pragma unroll
-      for (int u = 0; u < XPW; ++u) {
-        const int k = wave + NW * u;
-        x_block(lo + 8 * (k < nblk ? k : k - nblk));
-      }
-    }
+    // 1 X block per wave inside a board, 2 at a board's first step (7-8 new blocks; a wave
+    // without an 8th block re-loads block 0, same bytes)
+    x_block(lo + 8 * wave);
+    if (nblk > 4) x_block(lo + 8 * (wave + 4 < nblk ? wave + 4 : 0));
     loaded_hi = hi;
     dz_block(buf, g0n);
   };
@@ -197,7 +182,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int rl = 8 * g + 4 * h + q;
-    const int sw = NW == 8 ? dswz(rl) : xswz(rl);
+    const int sw = xswz(rl);
 #pragma unroll
     for (int i = 0; i < 4; ++i) rel_d[h][i] = rl * DZR + (((8 * wm + 2 * i + p1) ^ sw) * 16) + p0;
   }
@@ -220,99 +205,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
   // this wave's DMAs of step st+1 landed: the DMAs of steps st+2 .. st+PD may remain
   auto wait_next = [&](int st) {
     if (st + PD < s1) {
-      if constexpr (NW == 4) {
-        // 2 per step, 3 at a board's first step (at most one in any 3 consecutive steps)
-        const int r = (st + 2) % STEPS_PER_BOARD;
-        if (r == 0 || r + PD - 2 >= STEPS_PER_BOARD)
-          dma_wait<2 * (PD - 1) + 1>();
-        else
-          dma_wait<2 * (PD - 1)>();
-      } else {
-        dma_wait<(XPW + 1) * (PD - 1)>();
-      }
+      // 2 per step, 3 at a board's first step (at most one in any 3 consecutive steps)
+      const int r = (st + 2) % STEPS_PER_BOARD;
+      if (r == 0 || r + PD - 2 >= STEPS_PER_BOARD)
+        dma_wait<2 * (PD - 1) + 1>();
+      else
+        dma_wait<2 * (PD - 1)>();
     } else {
       dma_wait<0>();
     }
   };
-  if constexpr (SWP) {
-    // Software-pipelined K-steps: the taps run as three kernel-row groups, each group's B
-    // fragments read under the previous group's MFMAs, and the NEXT step's A fragments and
-    // first group read under the last group's MFMAs (after a mid-step barrier that makes
-    // the next step's DMA data visible), so no MFMA waits on a fresh LDS read.
-    // half h = 1 is rows +4: bits 1 and 3 of the row (the swizzle) are unchanged, so its
-    // address is h = 0's + 4 rows (an immediate offset)
-    auto readA = [&](s16x4 (&ta)[2][4], int bf) {
-      const char* sD = dzbuf + bf * DZB;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ta[0][i] = lds_read_tr((const LDS_AS char*)(sD + rel_d[0][i]));
-        ta[1][i] = lds_read_tr((const LDS_AS char*)(sD + rel_d[0][i] + 4 * DZR));
-      }
-    };
-    auto readB = [&](s16x4 (&tb)[2][3], int dy, int jo) {
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          tb[h][u] = lds_read_tr(
-              (const LDS_AS char*)(xring + ((rel_x[3 * dy + u][h] + jo) & (XRING - 1))));
-    };
-    auto mm = [&](const s16x4 (&ta)[2][4], const s16x4 (&tb)[2][3], int dy) {
-      bf16x8 af[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const s16x4 lo = ta[0][i], hi = ta[1][i];
-        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const s16x4 lo = tb[0][u], hi = tb[1][u];
-        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][3 * dy + u] = mfma16(af[i], bfr, acc[i][3 * dy + u]);
-      }
-    };
-    s16x4 ta[2][4], tn[2][4], b0[2][3], b1[2][3], b2[2][3];
-    int jo = j * 4096;
-    if (s0 < s1) {
-      readA(ta, 0);
-      readB(b0, 0, jo);
-    }
-    for (int st = s0; st < s1; ++st) {
-      if (st + PD < s1) issue(st + PD, buf_pd);
-      readB(b1, 1, jo);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(ta, b0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      readB(b2, 2, jo);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(ta, b1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      wait_next(st);
-      __builtin_amdgcn_s_barrier();
-      buf = buf == PD ? 0 : buf + 1;
-      buf_pd = buf_pd == PD ? 0 : buf_pd + 1;
-      if (++j == STEPS_PER_BOARD) {
-        j = 0;
-        ++bsteps;
-        board_rel(bsteps * WFF + WF);
-      }
-      jo = j * 4096;
-      if (st + 1 < s1) {
-        readA(tn, buf);
-        readB(b0, 0, jo);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mm(ta, b2, 2);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ta[h][i] = tn[h][i];
-    }
-  } else {
   for (int st = s0; st < s1; ++st) {
     if (st + PD < s1) issue(st + PD, buf_pd);
     if (j == STEPS_PER_BOARD) {
@@ -369,8 +271,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
     ++j;
   }
 
-  }
-
   float* slab = Ls.slab[layer] + (size_t)zsplit * a.Mpad * a.KP;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -387,14 +287,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
 }
 
 int g_win_ablate = 0;
-int g_win_pd = 4;
-int g_win_nw = 4;
-int g_win_swp = 0;
+constexpr int WIN_NW = 4;
+constexpr int WIN_PD = 4;
 
-template <int ABL, int PD, int NW, bool SWP = false>
+template <int ABL>
 void launch_win(dim3 grid, const WinArgs& a, const WinLayers& Ls, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, PD, NW, SWP>), grid, dim3(64 * NW), 0, stream,
-                     a, Ls);
+  hipLaunchKernelGGL((conv_wgrad_win_kernel<ABL, WIN_PD, WIN_NW>), grid, dim3(64 * WIN_NW), 0,
+                     stream, a, Ls);
 }
 
 }  // namespace
@@ -402,15 +301,12 @@ void launch_win(dim3 grid, const WinArgs& a, const WinLayers& Ls, hipStream_t st
 extern "C" {
 
 void dg_conv_wgrad_win_set_ablate(int mode) { g_win_ablate = mode; }
-void dg_conv_wgrad_win_set_pd(int pd) { g_win_pd = pd == 2 ? 2 : 4; }
-void dg_conv_wgrad_win_set_nw(int nw) { g_win_nw = nw == 8 ? 8 : 4; }
-void dg_conv_wgrad_win_set_swp(int on) { g_win_swp = on; }
 
 // Splits per (layer, chunk pair) that fill num_cus CUs in one round (8 / NW workgroups per
 // CU).  At least 8 K-steps per split (the prologue loads a full window).
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
-  const int pairs = nl * (M / (16 * g_win_nw)) * (Cx / 64);
-  int s = pairs > 0 ? num_cus * (8 / g_win_nw) / pairs : 1;
+  const int pairs = nl * (M / (16 * WIN_NW)) * (Cx / 64);
+  int s = pairs > 0 ? num_cus * (8 / WIN_NW) / pairs : 1;
   const int smax = B * STEPS_PER_BOARD / 8;
   if (s > smax) s = smax;
   return s < 1 ? 1 : s;
@@ -419,7 +315,7 @@ int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
 // table = nl rows of {dZ frame (pad 1, M channels), X frame (pad 1, Cx channels), slab}.
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                              int KP, int splits, hipStream_t stream) {
-  const int coch = 16 * g_win_nw;
+  const int coch = 16 * WIN_NW;
   if (nl <= 0 || nl > MAXL || M % coch != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || splits <= 0 || splits > B * STEPS_PER_BOARD)
     return hipErrorInvalidValue;
@@ -432,20 +328,11 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
   }
   WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / coch) * (Cx / 64) * splits);
-  const bool w8 = g_win_nw == 8;
   switch (g_win_ablate & 31) {
-    case 0:
-      if (g_win_swp)
-        w8 ? launch_win<0, 4, 8, true>(grid, a, Ls, stream)
-           : launch_win<0, 4, 4, true>(grid, a, Ls, stream);
-      else if (g_win_pd == 2)
-        w8 ? launch_win<0, 2, 8>(grid, a, Ls, stream) : launch_win<0, 2, 4>(grid, a, Ls, stream);
-      else
-        w8 ? launch_win<0, 4, 8>(grid, a, Ls, stream) : launch_win<0, 4, 4>(grid, a, Ls, stream);
-      break;
-#define WIN_CASE(n)                                                                     \
-  case n:                                                                               \
-    w8 ? launch_win<n, 4, 8>(grid, a, Ls, stream) : launch_win<n, 4, 4>(grid, a, Ls, stream); \
+    case 0: launch_win<0>(grid, a, Ls, stream); break;
+#define WIN_CASE(n) \
+  case n:           \
+    launch_win<n>(grid, a, Ls, stream); \
     break;
       WIN_CASE(1) WIN_CASE(2) WIN_CASE(3) WIN_CASE(4) WIN_CASE(5) WIN_CASE(6) WIN_CASE(7)
       WIN_CASE(8) WIN_CASE(12) WIN_CASE(16) WIN_CASE(20) WIN_CASE(22)

@@ -404,8 +404,6 @@ extern "C" hipError_t dg_head_mfma(int C, const void* X, int B, const float* w, 
                                    const float* posb, const int* labels, float* loss, int* pred,
                                    float* logp_out, void* dZ, float* gw_part, float* dzb,
                                    int head_relu, float grad_scale, hipStream_t stream);
-static int g_head_mfma = 1;   // (tests: 0 runs the VALU head on MFMA shapes too)
-extern "C" void dg_head_set_mfma(int on) { g_head_mfma = on; }
 
 extern "C" hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                               const float* bias, const float* posb, const int* labels,
@@ -414,7 +412,7 @@ extern "C" hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, co
                               float grad_scale, hipStream_t stream) {
   if (C % 8 != 0 || B <= 0) return hipErrorInvalidValue;
   // 3x3 head over a 128/256-channel pad-1 frame: the MFMA kernel (head_mfma.hip)
-  if (g_head_mfma && kw == 3 && (C == 128 || C == 256) && x_pad == 1 && (!dZ || dz_pad == 1))
+  if (kw == 3 && (C == 128 || C == 256) && x_pad == 1 && (!dZ || dz_pad == 1))
     return dg_head_mfma(C, X, B, w, bias, posb, labels, loss, pred, logp_out, dZ, gw_part, dzb,
                         head_relu, grad_scale, stream);
   if (C > CCH && C % CCH != 0) return hipErrorInvalidValue;

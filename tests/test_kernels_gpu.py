@@ -199,20 +199,14 @@ def test_conv_board_dgrad(B, cin, cout, k, bm, monkeypatch):
                                                  (2, 40, 128, 5, 3), (5, 256, 256, 3, None),
                                                  (1, 16, 16, 3, 1), (2, 128, 128, 1, 2),
                                                  (3, 128, 128, 3, 7), (2, 128, 256, 3, None)])
-@pytest.mark.parametrize("variant", ["plain", "t3"])
-def test_conv_wgrad(B, cin, cout, k, splits, variant):
-    """im2col wgrad: 2-stage 128x128 and three-slice 128x384 tiles (the t3 kernel runs where
-    K % 384 == 0, else the 2-stage one)."""
+def test_conv_wgrad(B, cin, cout, k, splits):
+    """im2col wgrad: the three-slice 128x384 tiles where K % 384 == 0 (9 x 128 / 256), else
+    the 2-stage 128x128 kernel (the first layer's 5 x 5 x 40, d = 64 / 16 layers, 1 x 1)."""
     torch.manual_seed(3)
     from deep_go_amd.ops import functional as Fn
-    from deep_go_amd.ops.native import hip
-    hip().conv_wgrad_set_t3(1 if variant == "t3" else 0)
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    try:
-        got, gp, gb = Fn.conv_wgrad(dz, x, k, splits=splits, with_bias=True, algo="im2col")
-    finally:
-        hip().conv_wgrad_set_t3(1)
+    got, gp, gb = Fn.conv_wgrad(dz, x, k, splits=splits, with_bias=True, algo="im2col")
     w0 = torch.zeros(cout, k, k, cin, device=DEV, requires_grad=True)
     y = conv_ref(x, w0, k)
     (gw,) = torch.autograd.grad(y, w0, dz)
@@ -224,22 +218,17 @@ def test_conv_wgrad(B, cin, cout, k, splits, variant):
 
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),
                                          (4, 64, 128, 3), (5, 16, 128, 5)])
-@pytest.mark.parametrize("nw", [4, 8])
-def test_conv_l1(B, cin, cout, k, nw):
+def test_conv_l1(B, cin, cout, k):
     """Board-resident first-layer forward (conv_l1.hip: whole input frame in LDS, K over
-    8-channel (tap, chunk) groups) vs the fp32 reference."""
+    8-channel (tap, chunk) groups; half-board 4-wave workgroups, or whole-board 8-wave ones
+    where two do not fit on a CU — the 64-channel 3x3 shape) vs the fp32 reference."""
     torch.manual_seed(8)
     from deep_go_amd.ops import functional as Fn
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     w = bf(torch.randn(cout, k, k, cin, device=DEV) * 0.1)
     b = torch.randn(cout, device=DEV) * 0.1
     pb = torch.randn(361, cout, device=DEV) * 0.1
-    from deep_go_amd.ops.native import hip
-    hip().conv_l1_set_nw(nw)
-    try:
-        y, mask = Fn.conv_l1(x, w, b, pb, with_mask=cout % 8 == 0)
-    finally:
-        hip().conv_l1_set_nw(4)
+    y, mask = Fn.conv_l1(x, w, b, pb, with_mask=cout % 8 == 0)
     ref = torch.relu(conv_ref(x, w, k) + b[None, :, None, None]
                      + pb.t().reshape(1, cout, 19, 19))
     assert rel_err(y, ref) < 1e-2
@@ -272,50 +261,33 @@ def test_conv_l1_frag(B, cin, cout):
 @pytest.mark.parametrize("B,cin,cout,splits", [
     (3, 128, 128, None), (1, 128, 128, 1), (2, 128, 128, 26), (5, 256, 256, None),
     (4, 64, 128, 7), (3, 192, 256, 2), (6, 128, 128, 5), (3, 128, 64, None)])
-@pytest.mark.parametrize("nw,swp", [(4, 1), (8, 1), (4, 0)])
-def test_conv_wgrad_win(B, cin, cout, splits, nw, swp):
+def test_conv_wgrad_win(B, cin, cout, splits):
     """Sliding-window 3x3 wgrad (conv_wgrad_win.hip: frame-linear K, one X window for all 9
-    taps, split ranges that start / end inside a board; 4- and 8-wave workgroups, pipelined
-    and plain K-loops) vs the fp32 reference."""
-    if cout % (16 * nw):
-        pytest.skip("co chunk")
+    taps, split ranges that start / end inside a board) vs the fp32 reference."""
     torch.manual_seed(6)
     from deep_go_amd.ops import functional as Fn
-    from deep_go_amd.ops.native import hip
     x = bf(torch.randn(B, cin, 19, 19, device=DEV))
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    hip().conv_wgrad_win_set_nw(nw)
-    hip().conv_wgrad_win_set_swp(swp)
-    try:
-        got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
-    finally:
-        hip().conv_wgrad_win_set_nw(4)
-        hip().conv_wgrad_win_set_swp(0)
+    got = Fn.conv_wgrad(dz, x, 3, splits=splits, algo="win")
     w0 = torch.zeros(cout, 3, 3, cin, device=DEV, requires_grad=True)
     (gw,) = torch.autograd.grad(conv_ref(x, w0, 3), w0, dz)
     assert rel_err(got, gw) < 1e-3
 
 
-@pytest.mark.parametrize("B,C,k,relu,mfma", [(3, 64, 3, True, 1), (7, 128, 3, True, 1),
-                                             (7, 128, 3, True, 0), (5, 128, 3, False, 1),
-                                             (2, 32, 1, False, 1), (4, 256, 3, True, 1),
-                                             (4, 256, 3, True, 0), (5, 256, 3, False, 1)])
-def test_head(B, C, k, relu, mfma):
-    """Fused head (3x3/128 and /256: MFMA kernel unless mfma=0; other shapes: VALU kernel) vs fp32
+@pytest.mark.parametrize("B,C,k,relu", [(3, 64, 3, True), (7, 128, 3, True),
+                                        (5, 128, 3, False), (2, 32, 1, False), (4, 256, 3, True),
+                                        (5, 256, 3, False)])
+def test_head(B, C, k, relu):
+    """Fused head (3x3/128 and /256: the MFMA kernel; other shapes: the VALU kernel) vs fp32
     autograd."""
     torch.manual_seed(4)
     from deep_go_amd.ops import functional as Fn
-    from deep_go_amd.ops.native import hip
-    hip().head_set_mfma(mfma)
     x = bf(torch.relu(torch.randn(B, C, 19, 19, device=DEV)))
     w = bf(torch.randn(1, k, k, C, device=DEV) * 0.05)  # fwd dots use bf16 weights
     b = torch.randn(1, device=DEV) * 0.1
     pb = torch.randn(361, device=DEV) * 0.1
     labels = torch.randint(0, 361, (B,), device=DEV)
-    try:
-        out = Fn.head(x, w, b, pb, labels, head_relu=relu)
-    finally:
-        hip().head_set_mfma(1)
+    out = Fn.head(x, w, b, pb, labels, head_relu=relu)
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)

@@ -57,21 +57,7 @@ def main():
             h.conv_wgrad_win_set_ablate(mode)
             res.setdefault(f"win_nw4_abl{mode}", []).append(round(timeit(win), 2))
         h.conv_wgrad_win_set_ablate(0)
-        for nw, swp in ((8, 0), (4, 0), (8, 1), (4, 1)):
-            h.conv_wgrad_win_set_nw(nw)
-            h.conv_wgrad_win_set_swp(swp)
-            for pd in ((2, 4) if not swp else (4,)):
-                h.conv_wgrad_win_set_pd(pd)
-                Sn = h.conv_wgrad_win_splits(NL, C, C, B, ncu)
-                if Sn * C * KPw * NL > slab_w.numel():
-                    continue
-
-                def winn():
-                    h.conv_wgrad_win(tw.ctypes.data, NL, C, C, C, B, KPw, Sn, s)
-                res.setdefault(f"win_nw{nw}_pd{pd}_swp{swp}_S{Sn}", []).append(
-                    round(timeit(winn), 2))
-        h.conv_wgrad_win_set_pd(4)
-        h.conv_wgrad_win_set_swp(0)
+        res.setdefault(f"win_S{Sw}", []).append(round(timeit(win), 2))
         res.setdefault("t3_multi", []).append(round(timeit(t3), 2))
     out = {k: {"us": v, "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}
     out["config"] = cfg
