@@ -56,18 +56,23 @@ class ExperimentConfig:
     rmsprop_decay: float = 0.9
     bucket_mb: float = 6.0         # DP gradient bucket size (12x128: head + hidden layers | layer 0)
     grad_dtype: str = "fp32"       # all-reduce dtype: fp32 | bf16
-    # DP gradient collectives in the trainer: torch (torch.distributed between graph
-    # segments) | auto (native in-graph RCCL when every rank's self-test passes, else torch)
-    # | native.  bench.py uses auto; the trainer stays on torch by default until a
-    # multi-GPU hardware run has confirmed the in-graph mode (README, DP section)
-    comm: str = "torch"
+    # DP gradient collectives in the trainer: auto (the native in-graph RCCL communicator when
+    # every rank's set-up and in-graph self-test pass, else torch — a collective decision,
+    # parallel/dp.py make_communicator; what bench.py measures) | native | torch
+    # (torch.distributed's process group between graph segments)
+    comm: str = "auto"
     reference_validation_quirks: bool = False  # train.lua:23-44 floor/off-by-one
     sampling: str = "game"         # game (reference, data.lua:29-37) | position
     loader_threads: int = 8
     prefetch: int = 4
     checkpoint_dir: str = "."
     metrics_path: Optional[str] = None
-    nan_policy: str = "raise"      # raise | skip
+    # non-finite loss / gradient: guard (default: the device gate skips the update, the host
+    # checks at log intervals and raises — dumping the batch — after nan_max_skips
+    # consecutive skipped steps; the training step stays one fused graph) | skip (never
+    # raises) | raise (host check every step, unfused; the reference's pcall dump)
+    nan_policy: str = "guard"
+    nan_max_skips: int = 10
     log_interval: int = 10         # train.lua:119
     id: Optional[str] = None
 
@@ -153,12 +158,20 @@ def _coerce(name: str, value: Any, current: Any) -> Any:
     return value
 
 
+_CHOICES = {"nan_policy": ("guard", "skip", "raise"), "comm": ("auto", "native", "torch"),
+            "optimizer": ("sgd", "rmsprop"), "grad_dtype": ("fp32", "bf16"),
+            "sampling": ("game", "position")}
+
+
 def override(cfg: ExperimentConfig, kw: Dict[str, Any]) -> ExperimentConfig:
     """Return a copy with overrides; unknown keys raise (fixes localtest.lua:8 typo class)."""
     unknown = [k for k in kw if k not in _FIELD_TYPES]
     if unknown:
         raise KeyError(f"unknown config key(s): {unknown}; valid: {sorted(_FIELD_TYPES)}")
     vals = {k: _coerce(k, v, getattr(cfg, k)) for k, v in kw.items()}
+    for k, v in vals.items():
+        if k in _CHOICES and v not in _CHOICES[k]:
+            raise ValueError(f"{k}={v!r}: expected one of {_CHOICES[k]}")
     return dataclasses.replace(cfg, **vals)
 
 

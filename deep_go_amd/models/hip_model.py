@@ -124,6 +124,7 @@ class HipGoNet:
         # True while a step is issued whose gradient pass 2 is deferred into the fused update
         # (train_step / SegmentedStep's whole-step graph; see can_defer)
         self._defer = False
+        self._gate_issued = False   # this step's loss gate already issued (side stream)
         self._red_src = {}    # layer -> (slab, bpart, splits, Mpad, KP, bchunks) of its pass 2
 
         # ---- per-layer plans + bf16 operand weights ----
@@ -1185,6 +1186,7 @@ class HipGoNet:
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
                 self._flush_head_reduce(side.cuda_stream)
+                self._issue_loss_gate(side.cuda_stream)
                 self._run(ops[:1], side.cuda_stream)
                 ev = side.record_event()         # partials ready for the reduce
                 # then dZ_0 and the first layer's whole chain, joined at layer 0.  Measured
@@ -1199,6 +1201,17 @@ class HipGoNet:
             for fn in hooks:
                 fn()
         self._run(ops[3:], main.cuda_stream)
+
+    def _issue_loss_gate(self, stream):
+        """With the gradient pass 2 deferred the update's gate is the loss alone: issue it on
+        the side stream as soon as the loss exists (beside the weight-gradient launch), not
+        in front of the fused update."""
+        if (self._defer and not self._gate_issued and self.cfg.nan_policy != "raise"
+                and self.grads16 is None):
+            self._run([(self.h.finite_gate, (self.loss.data_ptr(), self.B, 0, 0,
+                                             self.gate.data_ptr(), self.bad_steps.data_ptr()))],
+                      stream)
+            self._gate_issued = True
 
     def _layer_ops(self, i: int):
         """Layer i's backward ops [bias partial, wgrad, pass 2, (dgrad)]; with the step's
@@ -1255,7 +1268,7 @@ class HipGoNet:
         # (bf16 wire: the optimizer reads the all-reduced bf16 twin)
         w16 = self.grads16 is not None
         g = self.grads16.data_ptr() if w16 else self.grads.data_ptr()
-        if self.cfg.nan_policy != "raise":
+        if self.cfg.nan_policy != "raise" and not (slabs and self._gate_issued):
             # gate = finite(loss) [and finite(gradients)]: under DP every rank sees the same
             # all-reduced gradient, so all ranks skip together.  With the pass 2 deferred the
             # gradient does not exist yet: the gate is the loss, and the fused update leaves
@@ -1265,6 +1278,9 @@ class HipGoNet:
                 0 if dp else self.loss.data_ptr(), self.B, 0 if slabs else g,
                 0 if slabs else n, self.gate.data_ptr(), self.bad_steps.data_ptr(), s)
             gate = self.gate.data_ptr()
+        if self.cfg.nan_policy != "raise":
+            gate = self.gate.data_ptr()
+        self._gate_issued = False
         self._fp8_update(s)
         if os.environ.get("DG_FUSED_UPDATE", "1") == "0":
             if self.ms is not None:

@@ -105,7 +105,7 @@ class CPUBackend:
     def optimizer_step(self):
         # skip on non-finite (all-reduced) gradients: every rank sees the same reduced
         # gradient, so all ranks skip together (a rank-local loss check would not)
-        if self.cfg.nan_policy == "skip" and not (
+        if self.cfg.nan_policy != "raise" and not (
                 np.isfinite(self._loss_sum) if self.world == 1
                 else bool(torch.isfinite(self.params.grad).all())):
             self.nan_skipped += 1
@@ -130,6 +130,10 @@ class CPUBackend:
 
     def correct(self) -> int:
         return self._eval[1] if self._last == "eval" else self._correct
+
+    def bad_steps(self) -> int:
+        """Updates skipped for a non-finite loss / gradient so far."""
+        return self.nan_skipped
 
     def flat_params(self) -> torch.Tensor:
         return self.params.detach()
@@ -236,6 +240,10 @@ class HIPBackend:
             n = self._eval_n
             return int((self.net.eval_pred[:n] == self.net.labels[:n]).sum().item())
         return int((self.net.pred == self.net.labels).sum().item())
+
+    def bad_steps(self) -> int:
+        """Updates the device gate / fused update skipped so far (syncs)."""
+        return int(self.net.bad_steps.item())
 
     def flat_params(self) -> torch.Tensor:
         return self.net.params.detach().cpu()

@@ -30,7 +30,8 @@ from ..data.loader import BatchLoader
 from ..parallel import dp
 from ..utils import trace
 from ..utils import checkpoint as ckpt
-from ..utils.faults import StepWatchdog, check_finite, maybe_inject, parse_fault
+from ..utils.faults import (NonFiniteLoss, SkipGuard, StepWatchdog, check_finite, dump_batch,
+                            maybe_inject, parse_fault)
 from ..utils.metrics import MetricsSink
 
 # step timeout (seconds) armed under the native RCCL communicator when DG_STEP_TIMEOUT is
@@ -173,6 +174,8 @@ class Experiment:
         watchdog = (StepWatchdog(float(timeout or 0), comm=comm)
                     if timeout or comm is not None else None)
         ema = self.train_costs[-1] if self.train_costs else None
+        skipguard = (SkipGuard(cfg.nan_max_skips, be.bad_steps())
+                     if cfg.nan_policy == "guard" else None)
         t_start = time.perf_counter()
         t_log = t_start
         n_log = 0
@@ -236,6 +239,16 @@ class Experiment:
                 if not fused:
                     with trace.range("optimizer"):
                         be.optimizer_step()
+                # (after the update: the device's skip counter then includes this step)
+                if skipguard is not None:
+                    skipguard.step()
+                    if need_cost:
+                        try:
+                            skipguard.check(be.bad_steps(), step)
+                        except NonFiniteLoss:
+                            dump_batch(batch if batch is not None else be.current_batch(),
+                                       step, cfg.checkpoint_dir)
+                            raise
                 if save_now:
                     with trace.range("checkpoint"):
                         self.save()

@@ -54,15 +54,49 @@ def maybe_inject(rank: int, step: int, spec=None):
     return kind
 
 
+def dump_batch(batch, step: int, dump_dir: str = ".") -> Optional[str]:
+    if batch is None:
+        return None
+    path = os.path.join(dump_dir, f"bad_batch_{step}.npz")
+    np.savez(path, *[np.asarray(b) for b in batch])
+    return path
+
+
 def check_finite(loss_sum: float, step: int, policy: str, batch=None, dump_dir: str = "."):
+    """True if the loss is finite.  Policies ``skip`` / ``guard`` return False (the device
+    gate skipped the update; ``guard`` raises later through SkipGuard); ``raise`` dumps the
+    batch and raises."""
     if np.isfinite(loss_sum):
         return True
-    if policy == "skip":
+    if policy in ("skip", "guard"):
         return False
-    if batch is not None:
-        path = os.path.join(dump_dir, f"bad_batch_{step}.npz")
-        np.savez(path, *[np.asarray(b) for b in batch])
+    dump_batch(batch, step, dump_dir)
     raise NonFiniteLoss(f"non-finite loss {loss_sum} at step {step}")
+
+
+class SkipGuard:
+    """nan_policy ``guard``: the device gate skips updates on its own (no host sync per
+    step); at the host's log-interval syncs this reads the device's skipped-step counter
+    and raises NonFiniteLoss once ``max_skips`` consecutive steps were skipped — whole check
+    windows of skipped steps add up, a window with any applied step resets the run (a skip
+    run that started mid-window is counted from the next window: never a false alarm)."""
+
+    def __init__(self, max_skips: int, bad_now: int = 0):
+        self.max_skips = max(1, int(max_skips))
+        self.prev = bad_now
+        self.since = 0
+        self.run = 0
+
+    def step(self):
+        self.since += 1
+
+    def check(self, bad_now: int, step: int) -> None:
+        d = bad_now - self.prev
+        self.run = self.run + d if (d == self.since and d > 0) else 0
+        self.prev, self.since = bad_now, 0
+        if self.run >= self.max_skips:
+            raise NonFiniteLoss(f"{self.run} consecutive training steps were skipped for "
+                                f"non-finite loss / gradients (last at step {step})")
 
 
 class StepWatchdog:

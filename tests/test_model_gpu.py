@@ -539,7 +539,9 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
         monkeypatch.setenv("DG_FUSED_UPDATE", fused)
         nets.append(_setup(layers, ch, 4, seed=2, **kw)[1])
     net0, net1 = nets
-    assert net1.can_defer()
+    # (d = 64: no grouped weight-gradient launch, so the step reduces first and the fused
+    # launch reads the flat gradient — still one update launch)
+    assert net1.can_defer() == (ch >= 128)
     monkeypatch.setenv("DG_FUSED_UPDATE", "0")
     assert not net0.can_defer()
 

@@ -281,3 +281,36 @@ def test_cpu_1layer_k16_preset_trains(tmp_path, ref_data):
     res = e.run(40)
     assert np.isfinite(res["train_cost"]) and len(e.validation_costs) == 1
     assert np.isfinite(e.validation_costs[0])
+
+
+def test_skip_guard_counts_consecutive_windows():
+    from deep_go_amd.utils.faults import NonFiniteLoss, SkipGuard
+    g = SkipGuard(10)
+    for bad in (0, 3, 3):            # a partial window, then a clean one: no run
+        for _ in range(5):
+            g.step()
+        g.check(bad, 0)
+    assert g.run == 0
+    for k in range(1, 3):            # two fully skipped windows of 5
+        for _ in range(5):
+            g.step()
+        if k < 2:
+            g.check(3 + 5 * k, k)
+        else:
+            with pytest.raises(NonFiniteLoss, match="10 consecutive"):
+                g.check(3 + 5 * k, k)
+
+
+def test_guard_policy_skips_then_raises_with_dump(tmp_path, ref_data):
+    """Default nan_policy='guard': a diverged run (every update skipped from some step on) is
+    not stopped per step, but the host check at the log interval raises after nan_max_skips
+    consecutive skipped steps and dumps the batch."""
+    from deep_go_amd.train.experiment import Experiment
+    from deep_go_amd.utils.faults import NonFiniteLoss
+    cfg = _cfg(tmp_path, ref_data, rate=1e38, log_interval=4, nan_max_skips=8, head_relu=False)
+    assert cfg.nan_policy == "guard"
+    e = Experiment(cfg, id="g")
+    with pytest.raises(NonFiniteLoss, match="consecutive"):
+        e.run(40)
+    assert e.backend.bad_steps() >= 8
+    assert any(f.startswith("bad_batch_") for f in os.listdir(tmp_path))
