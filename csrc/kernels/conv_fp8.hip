@@ -233,10 +233,17 @@ conv_board_fp8_kernel(Fp8Args a) {
 // gradients), incremented when the amax just observed exceeds the range of the scale that
 // was in use (448 s; e5m2 57344 s): values of that tensor were clamped in the last refresh /
 // forward / backward.  gscales / gamax (optional): the e5m2 gradient scales of dz[l] (fp8
-// backward-data stack), powers of two with 1.25x headroom like the activation scales.
+// backward-data stack), powers of two with the activation scales' headroom (FP8_HEADROOM).
 // One wave per layer l.  amax_w: nparts_w per-workgroup |w| maxima per layer (float bits,
 // written by weight_refresh with plain stores — one same-address atomic per workgroup
 // serialised at the memory side and cost the fp8 refresh ~20 us), max-reduced here.
+// Headroom of the delayed power-of-two activation / gradient scales over the last observed
+// |x| max: the scale is the smallest power of two with HEADROOM * amax / s <= the format's
+// max.  1.25 left 0.8% of layer-steps saturated in the slow 1000-step stress run but 2-9%
+// per layer in a memorisation run (rate 0.1, loss falling > 1 nat: amax grows faster than
+// 25% per step); 2.0 (one more power of two, one less e4m3 binade at the bottom) keeps
+// that regime under 1%.  Weights use their own margin (w_margin, host).
+constexpr float FP8_HEADROOM = 2.0f;
 __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* scales,
                                                                unsigned* amax_w, int nparts_w,
                                                                unsigned* amax_y, float w_margin,
@@ -263,7 +270,7 @@ __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* sca
     const float mg = __uint_as_float(gamax[l]);
     const bool ok = __builtin_isfinite(mg);
     if (sat && (!ok || mg > 57344.f * gscales[l])) sat[2 * n + l] += 1;
-    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(1.25f * mg / 57344.f)));
+    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(FP8_HEADROOM * mg / 57344.f)));
     gamax[l] = 0u;
   }
   const float mw = __uint_as_float(mwb);
@@ -274,11 +281,10 @@ __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* sca
     if (!oky || my > FP8_MAX * scales[2 * l + 1]) sat[2 * l + 1] += 1;
   }
   if (okw && mw > 0.f) scales[2 * l] = mw * w_margin / FP8_MAX;
-  // activation scales are powers of two (the smallest with 1.25 amax / s <= 448: headroom
-  // for the next step's growth — without it 0.8% of layer-steps saturated in the 1000-step
-  // stress test); e4m3 <-> bf16 conversions then scale exactly (conv_stack_f8's
-  // v_cvt_scalef32_pk_bf16_fp8 copy-out)
-  if (oky && my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(1.25f * my / FP8_MAX)));
+  // activation scales are powers of two (the smallest with FP8_HEADROOM amax / s <= 448:
+  // headroom for the next step's growth); e4m3 <-> bf16 conversions then scale exactly
+  // (conv_stack_f8's v_cvt_scalef32_pk_bf16_fp8 copy-out)
+  if (oky && my > 0.f) scales[2 * l + 1] = exp2f(ceilf(log2f(FP8_HEADROOM * my / FP8_MAX)));
   amax_y[l] = 0u;
 }
 

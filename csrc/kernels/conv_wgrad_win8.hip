@@ -24,22 +24,21 @@
 // (probed on gfx950, tools/tr8_probe.hip: per 16-lane group, lane 2q + p supplies the
 // address of row q, bytes 8p..8p+7; lane i receives byte i of rows 0..7).
 //
-// LDS (one 4-wave workgroup = 64 co x 9 taps x 64 ci; wave wn owns ci 16 wn .. +16):
-//   X ring   512 rows x 64 B (64 ci), slot = G & 511, 16-B chunk c at c ^ ((slot >> 2) & 3):
-//            any 16 consecutive rows hit 16 distinct 16-B bank groups per chunk (the two
-//            tr-groups of a 32-lane half read rows 8g + q of one sub-step = 16 consecutive
-//            rows), and +32 rows (the next sub-step of a board) keeps the swizzle;
-//   dZ       3 buffers (prefetch distance 2) of 128 rows x 64 B (64 co), row R = 32 r + i,
-//            the same swizzle.
-// 56 KB per workgroup, ONE per CU: one wave per SIMD, so the kernel has the whole 512-entry
-// register file (144 accumulators in AGPRs, two super-steps of fp8 operands in VGPRs; at two
-// waves per SIMD the 2x larger fp8 operands spilled) and the compiler overlaps a super-step's
-// MFMAs with the next one's LDS reads and DMA issue.  DMA: every wave issues exactly 5 LDS-DMAs per super-step
-// (2 dZ + 3 X blocks of 1 KB; a super-step needs at most 11 new X blocks: 128 rows, +32 across
-// a board edge, +16 alignment — a wave without a block re-loads the first one, same bytes),
-// so "super-step S+1 landed" = vmcnt(5).  Ring capacity at prefetch distance 2: the rows of
-// super-steps S .. S+2 span at most 11 x 32 + 32 + 76 + 30 = 490 < 512.
-//
+// LDS (one 8-wave workgroup = 64 co x 9 taps x 64 ci; wave (wm, wn) owns co half wm (32 co)
+// x ci 16 wn .. +16; ~96 KB, one workgroup per CU, two waves per SIMD):
+//   X ring   XR = 1024 rows x 64 B (64 ci) = 64 KB, slot = G & 1023, 16-B chunk c at
+//            c ^ ((slot >> 2) & 3): any 16 consecutive rows hit 16 distinct 16-B bank groups
+//            per chunk (the two tr-groups of a 32-lane half read rows 8g + q of one sub-step
+//            = 16 consecutive rows), and +32 rows (the next sub-step of a board) keeps the
+//            swizzle;
+//   dZ       PD + 1 = 4 buffers of 128 rows x 64 B (64 co), row R = 32 r + i, same swizzle.
+// DMA: every wave issues exactly PER = 3 LDS-DMAs per super-step (1 dZ + 2 X blocks of 1 KB;
+// 8 dZ + 16 X blocks per workgroup, and a super-step needs at most 11 new X blocks: 128 rows,
+// +32 across a board edge, +16 alignment — a wave without a block re-loads the first one,
+// same bytes), so "super-step S+1 landed" with S+2 .. S+PD-1 still in flight =
+// vmcnt(PER * (PD - 1)).  Prefetch distance PD = 3: the ring holds super-steps S .. S+3,
+// whose rows span at most 4 x (128 + 32) + 76 + 30 = 746 < 1024 rows (static_assert below),
+// so a DMA never overwrites rows a wave may still read.
 // Output: fp32 split slabs slab[z][co][t*Cx + ci], the layout wgrad_reduce_multi sums (the
 // bf16 kernel's), so the reduce, the bias gradients and the DP buckets are unchanged.
 //
@@ -64,6 +63,9 @@ constexpr int XRING = XR * 64;    // 64 KB
 constexpr int DZB = 128 * 64;     // one super-step of dZ rows: 8 KB
 constexpr int PD = 3;             // DMA distance (super-steps): 2 in flight beyond the next
 constexpr int MAXL = 16;
+// ring capacity at prefetch distance PD (see the header): PD + 1 super-steps of at most
+// 128 + 32 rows each, plus the 76-row tap window and 30 rows of block alignment
+static_assert((PD + 1) * (128 + 32) + 76 + 30 <= XR, "X ring capacity");
 
 struct Win8Layers {
   const uint8_t* dZ[MAXL];   // e5m2 [B][448][M]

@@ -549,14 +549,20 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
         return [t for t in (*n.wfrag, *n.wdfrag, *n.wf8frag, *n.wd8frag, *n.pbias_frag,
                             *n.pbias) if t is not None]
 
+    def eq(a, b):
+        # (d = 64 runs the VALU head, whose weight-gradient partials sum through LDS atomics:
+        # its gradients are reproducible to rounding only — compare to that)
+        return torch.equal(a, b) if ch >= 128 else torch.allclose(a, b, rtol=1e-5, atol=1e-7)
+
     def check():
         torch.cuda.synchronize()
-        assert torch.equal(net0.params, net1.params)
-        assert torch.equal(net0.grads, net1.grads)
+        assert eq(net0.params, net1.params)
+        assert eq(net0.grads, net1.grads)
         assert net0.lr.item() == net1.lr.item()
         assert int(net0.step_count.item()) == int(net1.step_count.item())
         for a, b in zip(copies(net0), copies(net1)):
-            assert torch.equal(a, b)
+            assert torch.equal(a, b) if ch >= 128 else torch.allclose(
+                a.float(), b.float(), rtol=1e-2, atol=1e-6)
         if dtype == "fp8":
             assert torch.equal(net0.fp8_scales, net1.fp8_scales)
         assert int(net1.gu_tickets.abs().sum().item()) == 0    # tickets left zeroed
@@ -892,3 +898,33 @@ def test_fp8_weight_gradient_teacher_forced(ch, layers):
         # the fp64 order): ~1e-4 of the largest entry, against ~0.06-0.125 per-element
         # quantization steps the oracle already contains
         assert err < 5e-4, (i, err)
+
+
+@pytest.mark.parametrize("dtype,ch", [("fp8", 128), ("fp8", 256), ("bf16", 128)])
+def test_dropped_frames_and_operand_copies_over_many_steps(dtype, ch):
+    """frames and operand copies that HipGoNet decides nothing reads
+    (_drop_unread_act_frames: the fp8 stacks' non-last bf16 frames; _step_refresh_table: the
+    plain / untaken-path weight copies the per-step refresh skips) must stay unread across
+    optimizer steps too.  A model with every frame written and the full refresh table
+    (keep_act_frames, the init-time refresh table) follows the default one bit for bit over
+    several whole steps (graph-replayed, the deferred fused update)."""
+    from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep
+    _, net0, data = _setup(6, ch, 8, seed=51, dtype=dtype)
+    net1 = HipGoNet(net0.cfg, 8, device="cuda", keep_act_frames=True)
+    planes, player, rank, labels = data
+    net1.set_batch(torch.from_numpy(planes).cuda(), torch.from_numpy(player).cuda(),
+                   torch.from_numpy(rank).cuda(), torch.from_numpy(labels).cuda())
+    net1._step_refresh = net1._refresh_table.copy()   # refresh every operand copy each step
+    if dtype == "fp8":
+        assert net0.act_frames_dropped and not net1.act_frames_dropped
+        net1.fp8_scales.copy_(net0.fp8_scales)
+        net1.fp8_gscales.copy_(net0.fp8_gscales)
+        net1.fp8_amax_w.copy_(net0.fp8_amax_w)
+    s0 = SegmentedStep(net0, None, use_graphs=True)
+    s1 = SegmentedStep(net1, None, use_graphs=True)
+    for k in range(6):
+        s0()
+        s1()
+        torch.cuda.synchronize()
+        assert torch.equal(net0.loss, net1.loss), k
+        assert torch.equal(net0.params, net1.params), k
