@@ -113,6 +113,34 @@ DG_DEV f32x4 slab_sum4(const float* src, int splits, size_t zstride) {
   for (; z < splits; ++z) s0 += *(const f32x4*)(src + z * zstride);
   return (s0 + s1) + (s2 + s3);
 }
+// NU independent slab_sum4's with all their loads interleaved (more loads in flight per
+// thread); element-wise the same order as slab_sum4
+template <int NU>
+DG_DEV void slab_sums4(const float* const (&src)[NU], int splits, size_t zstride,
+                       f32x4 (&out)[NU]) {
+  f32x4 s[NU][4];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[u][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {
+    f32x4 v[NU][4];
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[u][q] = *(const f32x4*)(src[u] + (z + q) * zstride);
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[u][q] += v[u][q];
+  }
+  for (; z < splits; ++z)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) s[u][0] += *(const f32x4*)(src[u] + z * zstride);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) out[u] = (s[u][0] + s[u][1]) + (s[u][2] + s[u][3]);
+}
 DG_DEV float slab_sum1(const float* src, int splits, size_t zstride) {
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int z = 0;

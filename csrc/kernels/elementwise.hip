@@ -610,14 +610,28 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
       const int r = tix - t * nct * nit;
       const int cot = r / nit, cit = r - cot * nit;
       if (vec) {
-        // 4 consecutive ci per thread: 16-B slab loads (a row of the tile = 256 B)
-        for (int e4 = tid; e4 < 64 * 16; e4 += 256) {
+        // 4 consecutive ci per thread and unit, the tile's 4 units per thread summed together
+        // (16 16-B slab loads in flight per thread; slab_sums4 = slab_sum4's order per element)
+        const float* src[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + 256 * u;
+          const int rr = e4 >> 4, cc = (e4 & 15) * 4;
+          const int co = cot * 64 + rr, ci = cit * 64 + cc;
+          ok[u] = co < L.cout && ci < L.cin;
+          src[u] = S.slab + (ok[u] ? (size_t)co * S.KP + t * L.cinp + ci : 0);
+        }
+        f32x4 gs[4];
+        slab_sums4<4>(src, S.splits, zstride, gs);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + 256 * u;
           const int rr = e4 >> 4, cc = (e4 & 15) * 4;
           const int co = cot * 64 + rr, ci = cit * 64 + cc;
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          if (co < L.cout && ci < L.cin) {
-            const f32x4 g4 = slab_sum4(S.slab + (size_t)co * S.KP + t * L.cinp + ci, S.splits,
-                                       zstride);
+          if (ok[u]) {
+            const f32x4 g4 = gs[u];
             const size_t o = ((size_t)co * L.taps + t) * L.cin + ci;
             *(f32x4*)(Gw + o) = g4;
             const f32x4 p4 = *(const f32x4*)(Pw + o);

@@ -1222,9 +1222,18 @@ class HipGoNet:
         gradient pass 2 deferred into the fused update, the pass-2 launch (the slab reduce
         that also finishes the bias gradients) is left out."""
         ops = self._bwd[i]
-        if self._defer and len(ops) >= 3:
+        if self._defer and len(ops) >= 3 and i in self._defer_layers():
             ops = ops[:2] + [(self._noop, ())] + ops[3:]
         return ops
+
+    def _defer_layers(self) -> set:
+        """Layers whose pass 2 the fused update takes over when deferred: the grouped
+        weight-gradient launch's layers (their slabs / partials are regions of their own, ~12
+        splits each).  A layer outside it (the first layer's side-stream chain: 64 splits of
+        a 5x5 x 40 K) keeps its own slab reduce — its wide split-K sum is a poor fit for the
+        update's per-tile blocks (measured: 128 us for the fused kernel with it, the reduce
+        alone 10 us)."""
+        return set(self.wgroups[0]) if len(self.wgroups) == 1 else set()
 
     def can_defer(self) -> bool:
         """Whether a training step may leave its gradients as split-K slabs and bias partials
@@ -1240,8 +1249,7 @@ class HipGoNet:
             return False
         if len(self.wgroups) != 1:
             return False
-        rest = set(range(len(self.plans))) - set(self.wgroups[0])
-        return rest <= {0} and all(i in self._red_src for i in range(len(self.plans)))
+        return all(i in self._red_src for i in self.wgroups[0])
 
     def set_defer(self, on: bool):
         """Issue the following backward + optimizer_step with the gradient pass 2 deferred
@@ -1320,7 +1328,8 @@ class HipGoNet:
             rows = []
             for r, p in zip(ref, self.plans):
                 spec = self.layout.layers[p.index]
-                src = self._red_src[p.index] if slabs else (0, 0, 0, 0, 0, 0)
+                src = (self._red_src[p.index] if slabs and p.index in self._defer_layers()
+                       else (0, 0, 0, 0, 0, 0))
                 rows.append([int(x) for x in r] + [int(x) for x in src]
                             + [spec.w_off, spec.b_off, spec.pos_off])
             t = np.ascontiguousarray(np.array(rows, dtype=np.int64))

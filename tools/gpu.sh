@@ -52,7 +52,9 @@ for step in "$@"; do
         python3 $R/bench.py ${arg:---steps 10 --warmup 3} > $R/gpurun_out/prof_$n.log 2>&1)
       rc=$? ;;
     pmc)
-      C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+      # 8 SQ counters (the per-pass limit) + 1 GRBM: MFMA busy, waits, LDS conflicts and the
+      # LDS-wait / LDS-active columns (SQ_WAIT_INST_LDS, SQ_LDS_IDX_ACTIVE)
+      C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C \
         --output-format csv -d $R/gpurun_out/pmc_$n -o run -- \
         python3 $R/bench.py --steps 3 --warmup 1 --no-graph $arg > $R/gpurun_out/pmc_$n.log 2>&1)
