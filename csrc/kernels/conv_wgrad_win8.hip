@@ -93,7 +93,9 @@ DG_DEV i32x2 tr8(const LDS_AS char* p) {
 // NW = 8: two waves per SIMD, each 32 co (co half wm) x 9 taps x 16 ci — a partner wave
 // on the SIMD covers one wave's LDS reads / barrier.  The workgroup tile (64 co x 64 ci) and
 // the DMA schedule (20 1-KB blocks per super-step: 8 dZ + 12 X) are the same.
-template <int NW>
+// RA: B (X) fragments read RA taps ahead of their MFMAs (each tap's 4 tr8 reads then have
+// RA x MI MFMAs to land)
+template <int NW, int RA>
 __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Args a, Win8Layers Ls) {
   constexpr int MI = 16 / NW;            // 16-co accumulator fragments per wave (4 | 2)
   constexpr int XPW = NW == 4 ? 3 : 2;   // X blocks per wave per super-step (12 | 16 >= 11)
@@ -235,21 +237,20 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
         v[r] = tr8((const LDS_AS char*)(xring + ((rel[t] + so[r]) & (XRING - 1))));
       return i32x8{v[0].x, v[0].y, v[1].x, v[1].y, v[2].x, v[2].y, v[3].x, v[3].y};
     };
-    // one tap's B reads issued ahead of the previous tap's MFMAs (pinned by sched_barriers:
-    // left alone the scheduler hoists all 36 reads to the top), so with one wave per SIMD
-    // each read has the 4 MFMAs of the tap before it (~128 cycles) to land
-    i32x8 bcur = read_b(0);
+    // a tap's B reads issued RA taps ahead of its MFMAs (pinned by sched_barriers: left
+    // alone the scheduler hoists all 36 reads to the top)
+    i32x8 bb[9];
+#pragma unroll
+    for (int t = 0; t < RA; ++t) bb[t] = read_b(t);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      i32x8 bnext;
-      if (t + 1 < 9) bnext = read_b(t + 1);
+      if (t + RA < 9) bb[t + RA] = read_b(t + RA);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
-        acc[i][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bcur, acc[i][t],
+        acc[i][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bb[t], acc[i][t],
                                                                      1, 0, 0, 127, 0, 127);
       __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < 9) bcur = bnext;
     }
     // this wave's DMAs of super-step S + 1 landed (those of S + 2 .. S + PD may remain),
     // then every wave's (barrier): the next super-step's rows are visible and S's free
@@ -327,7 +328,11 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   const dim3 grid(nl * (M / 64) * (Cx / 64) * splits);
   // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
   // the same — profiles/r3_fp8_wgrad_ab.txt)
-  hipLaunchKernelGGL(conv_wgrad_win8_kernel<8>, grid, dim3(512), 0, stream, a, Ls);
+  static const int ra = getenv("DG_WIN8_RA") ? atoi(getenv("DG_WIN8_RA")) : 1;   // (A/B)
+  if (ra == 2)
+    hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 2>), grid, dim3(512), 0, stream, a, Ls);
+  else
+    hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1>), grid, dim3(512), 0, stream, a, Ls);
   return hipGetLastError();
 }
 

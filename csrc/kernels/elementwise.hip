@@ -527,6 +527,10 @@ struct GUSrc {
   long long w_off, b_off, pos_off;   // element offsets into the flat P / G / MS
 };
 constexpr int MAX_GU = 20;
+// bias work in channel blocks of GU_BCH (or all C when C is smaller): C <= 256 -> at most 4
+// blocks per layer, one ticket each
+constexpr int GU_BCH = 64;
+DG_DEV int gu_bch(int C) { return C < GU_BCH ? C : GU_BCH; }
 struct GUArgs {
   int n;
   WRefreshLayer L[MAX_GU];
@@ -541,7 +545,9 @@ struct GUArgs {
   const double* lr;
   double decay;
   long long* step;
-  unsigned* tickets;   // [n + 1]: per layer, then the grid's (+ non-finite flag << 16)
+  unsigned* tickets;   // [4n + 1]: per (layer, channel block), then the grid's (+ the
+                       // non-finite flag << 16)
+  int write_grads;     // slab mode: also write the reduced fp32 gradient (tests / tools)
   int* bad_steps;
 };
 
@@ -633,7 +639,7 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
           if (ok[u]) {
             const f32x4 g4 = gs[u];
             const size_t o = ((size_t)co * L.taps + t) * L.cin + ci;
-            *(f32x4*)(Gw + o) = g4;
+            if (a.write_grads) *(f32x4*)(Gw + o) = g4;
             const f32x4 p4 = *(const f32x4*)(Pw + o);
             f32x4 m4 = {0.f, 0.f, 0.f, 0.f};
             if (MSw) m4 = *(const f32x4*)(MSw + o);
@@ -661,7 +667,7 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
             float g;
             if (S.slab) {
               g = slab_sum1(S.slab + (size_t)co * S.KP + t * L.cinp + ci, S.splits, zstride);
-              Gw[o] = g;
+              if (a.write_grads) Gw[o] = g;
             } else {
               g = a.G16 ? bf2f(a.G16[S.w_off + o]) : Gw[o];
             }
@@ -676,90 +682,110 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
       if (refresh_needs_tile(L)) refresh_tile_copies(L, t, cot, cit, tileS, inv8);
     }
     refresh_amax(L, wmax, s_amax);
-    // ---- biases: the layer's new per-channel bias (every block), then this block's share of
-    // the per-position biases and the bias tables
+    // ---- biases, in channel blocks of 64: bias block (cb, pb) = channels 64 cb .. +63 over
+    // position range pb.  Each recomputes the NEW per-channel bias of its 64 channels only (64
+    // sums of R row partials), updates its positions' per-position biases and writes those
+    // entries of the bias tables.
     const int C = L.cout;
-    const int R = S.bchunks * BOARD;
-    const float* rowpart = S.bpart ? S.bpart + (size_t)S.bchunks * NPTS * C : nullptr;
-    for (int c = tid; c < C; c += 256) {
-      float g;
-      if (S.bpart) {
-        g = rows_sum(rowpart, R, C, c);
-      } else {
-        const long long o = S.b_off + c;
-        g = a.G16 ? bf2f(a.G16[o]) : a.G[o];
-      }
-      float ms_v = a.MS ? a.MS[S.b_off + c] : 0.f;
-      s_b[c] = gu_update(a.P[S.b_off + c], g, a.MS != nullptr, ms_v, l, a.rms_decay, a.gscale,
-                         apply, bad);
-      // (the per-channel bias, its gradient and mean square are written by the layer's last
-      // block below: other blocks still read the old values here)
-      s_gb[c] = g;
-      s_ms[c] = ms_v;
-    }
-    __syncthreads();
-    const int C4 = C / 4;
-    const size_t np = (size_t)NPTS * C;
-    for (int it = blockIdx.x * 256 + tid; it < NPTS * C4; it += gridDim.x * 256) {
-      const int p = it / C4, c = (it - p * C4) * 4;
-      float nb[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const size_t j = (size_t)p * C + c + k;
+    const int bch = gu_bch(C);
+    const int ncb = C / bch;
+    const int npb = gridDim.x / ncb > 0 ? (int)gridDim.x / ncb : 1;
+    const int cb = blockIdx.x % ncb, pb = blockIdx.x / ncb;
+    if (pb < npb) {
+      const int c0 = cb * bch;
+      const int R = S.bchunks * BOARD;
+      const float* rowpart = S.bpart ? S.bpart + (size_t)S.bchunks * NPTS * C : nullptr;
+      if (tid < bch) {
+        const int c = c0 + tid;
         float g;
         if (S.bpart) {
-          g = chunk_sum(S.bpart + j, S.bchunks, np);
-          a.G[S.pos_off + j] = g;
+          g = rows_sum(rowpart, R, C, c);
         } else {
-          g = a.G16 ? bf2f(a.G16[S.pos_off + j]) : a.G[S.pos_off + j];
+          const long long o = S.b_off + c;
+          g = a.G16 ? bf2f(a.G16[o]) : a.G[o];
         }
-        const float v = gu_update_at(a, S.pos_off + j, g, l, apply, bad);
-        a.P[S.pos_off + j] = v;
-        nb[k] = s_b[c + k] + v;
-        if (L.pbias) L.pbias[j] = f2bf(nb[k]);
+        float ms_v = a.MS ? a.MS[S.b_off + c] : 0.f;
+        s_b[tid] = gu_update(a.P[S.b_off + c], g, a.MS != nullptr, ms_v, l, a.rms_decay,
+                             a.gscale, apply, bad);
+        // (the per-channel bias, its gradient and mean square are written by the last block
+        // of this channel block below: the others still read the old values here)
+        s_gb[tid] = g;
+        s_ms[tid] = ms_v;
       }
-      if (L.pbias_frag) {
-        const uint2 u = uint2{pack_bf16x2(nb[0], nb[1]), pack_bf16x2(nb[2], nb[3])};
-        L.pbias_frag[pbias_frag_index(p, c)] = u;
-        if (p == NPTS - 1)
-          for (int q = NPTS; q < 24 * 16; ++q) L.pbias_frag[pbias_frag_index(q, c)] = u;
+      __syncthreads();
+      const size_t np = (size_t)NPTS * C;
+      const int p0 = pb * NPTS / npb, p1 = (pb + 1) * NPTS / npb;
+      for (int it = tid; it < (p1 - p0) * (bch / 4); it += 256) {
+        const int p = p0 + it / (bch / 4), cl = (it % (bch / 4)) * 4, c = c0 + cl;
+        const size_t j = (size_t)p * C + c;
+        f32x4 g4;
+        if (S.bpart) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) g4[k] = chunk_sum(S.bpart + j + k, S.bchunks, np);
+          if (a.write_grads) *(f32x4*)(a.G + S.pos_off + j) = g4;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            g4[k] = a.G16 ? bf2f(a.G16[S.pos_off + j + k]) : a.G[S.pos_off + j + k];
+        }
+        float nb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v = gu_update_at(a, S.pos_off + j + k, g4[k], l, apply, bad);
+          a.P[S.pos_off + j + k] = v;
+          nb[k] = s_b[cl + k] + v;
+          if (L.pbias) L.pbias[j + k] = f2bf(nb[k]);
+        }
+        if (L.pbias_frag) {
+          const uint2 u = uint2{pack_bf16x2(nb[0], nb[1]), pack_bf16x2(nb[2], nb[3])};
+          L.pbias_frag[pbias_frag_index(p, c)] = u;
+          if (p == NPTS - 1)
+            for (int q = NPTS; q < 24 * 16; ++q) L.pbias_frag[pbias_frag_index(q, c)] = u;
+        }
       }
     }
   }
-  // ---- tickets: the layer's last block writes its per-channel biases; the grid's last block
-  // decays the LR, counts a step with a non-finite gradient entry and resets the counters.
-  // No fences: every block's reads of an old value (lr, the per-channel biases) have returned
-  // before its ticket is taken (their values were consumed before the barrier), and the
-  // writers act only after seeing the final ticket; the new values are read by later
-  // launches.  The grid ticket carries the non-finite flag in its high half (one atomic).
+  // ---- tickets: the last block of each (layer, channel block) writes its per-channel biases;
+  // the grid's last block decays the LR, counts a step with a non-finite gradient entry and
+  // resets the flag.  No fences: every block's reads of an old value (lr, the per-channel
+  // biases) have returned before its ticket is taken (their values were consumed before the
+  // barrier), and the writers act only after seeing the final ticket; the new values are read
+  // by later launches.  The grid ticket carries the non-finite flag in its high half.
   if (bad) s_flag[0] = 1u;     // (benign same-value race)
   __syncthreads();
-  if (tid == 0) {
-    unsigned last_layer = 0u;
-    if (ly < a.n) last_layer = atomicAdd(&a.tickets[ly], 1u) == gridDim.x - 1 ? 1u : 0u;
-    s_flag[1] = last_layer;
-  }
-  __syncthreads();
-  if (s_flag[1]) {
-    const WRefreshLayer L = a.L[ly];
-    const GUSrc S = a.S[ly];
-    for (int c = tid; c < L.cout; c += 256) {
-      a.P[S.b_off + c] = s_b[c];
-      if (S.bpart) a.G[S.b_off + c] = s_gb[c];
-      if (a.MS) a.MS[S.b_off + c] = s_ms[c];
+  int cbw = -1;   // the channel block this block closes (last of its position blocks)
+  if (ly < a.n) {
+    const int ncb = a.L[ly].cout / gu_bch(a.L[ly].cout);
+    const int npb = gridDim.x / ncb > 0 ? (int)gridDim.x / ncb : 1;
+    const int cb = blockIdx.x % ncb, pb = blockIdx.x / ncb;
+    if (pb < npb) {
+      if (tid == 0)
+        s_flag[1] = atomicAdd(&a.tickets[4 * ly + cb], 1u) == (unsigned)npb - 1 ? 1u : 0u;
+      __syncthreads();
+      if (s_flag[1]) cbw = cb;
     }
-    if (tid == 0) a.tickets[ly] = 0u;
+  }
+  if (cbw >= 0) {
+    const GUSrc S = a.S[ly];
+    const int bch = gu_bch(a.L[ly].cout);
+    if (tid < bch) {
+      const int c = cbw * bch + tid;
+      a.P[S.b_off + c] = s_b[tid];
+      if (S.bpart && a.write_grads) a.G[S.b_off + c] = s_gb[tid];
+      if (a.MS) a.MS[S.b_off + c] = s_ms[tid];
+    }
+    if (tid == 0) a.tickets[4 * ly + cbw] = 0u;
   }
   if (tid == 0) {
     const unsigned total = gridDim.x * gridDim.y;   // < 2^16 (host check)
-    const unsigned old = atomicAdd(&a.tickets[a.n], 1u + (s_flag[0] ? 0x10000u : 0u));
+    const unsigned old = atomicAdd(&a.tickets[4 * a.n], 1u + (s_flag[0] ? 0x10000u : 0u));
     if ((old & 0xFFFFu) == total - 1) {
       double* lrw = const_cast<double*>(a.lr);
       *lrw = *lrw * (1.0 - a.decay);
       if (a.step) *a.step += 1;
       const bool flagged = (old >> 16) != 0u || s_flag[0];
       if (flagged && a.bad_steps && apply) *a.bad_steps += 1;
-      a.tickets[a.n] = 0u;
+      a.tickets[4 * a.n] = 0u;
     }
   }
 }
@@ -971,15 +997,16 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
 // The fused gradient pass 2 + optimizer + refresh (grad_update_kernel).  table: n rows of
 // GU_COLS int64 = the 20 weight_refresh columns, then {slab, bpart, splits, Mpad, KP,
 // bchunks, w_off, b_off, pos_off} (slab / bpart 0: the layer's gradient is read from G / G16).
-// plain_off / plain_n: a flat range updated from G only (the head).  tickets: n + 1 zeroed
-// uint32 (left zeroed).  Same block count per layer as dg_weight_refresh (the fp8 |w| max
+// plain_off / plain_n: a flat range updated from G only (the head).  tickets: 4n + 1 zeroed
+// uint32 (left zeroed).  write_grads: with slabs, also store the reduced gradient in G.  Same block count per layer as dg_weight_refresh (the fp8 |w| max
 // slots).
 constexpr int GU_COLS = 29;
 int dg_grad_update_cols() { return GU_COLS; }
 hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
-                          long long* step, unsigned* tickets, int* bad_steps, hipStream_t s) {
+                          long long* step, unsigned* tickets, int* bad_steps, int write_grads,
+                          hipStream_t s) {
   if (n <= 0 || n > MAX_GU || !P || !G || !lr || !tickets || plain_n < 0)
     return hipErrorInvalidValue;
   GUArgs a;
@@ -990,7 +1017,8 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
     WRefreshLayer& L = a.L[i];
     const hipError_t e = parse_refresh_row(t, L);
     if (e != hipSuccess) return e;
-    if (L.cout > 256 || L.cout % 4 != 0) return hipErrorInvalidValue;
+    if (L.cout > 256 || L.cout % 4 != 0 || (L.cout > GU_BCH && L.cout % GU_BCH != 0))
+      return hipErrorInvalidValue;
     GUSrc& S = a.S[i];
     S.slab = (const float*)t[20];
     S.bpart = (const float*)t[21];
@@ -1023,6 +1051,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
   a.step = step;
   a.tickets = tickets;
   a.bad_steps = bad_steps;
+  a.write_grads = write_grads;
   const int blocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
   if (blocks * (n + 1) >= 0x10000) return hipErrorInvalidValue;   // the packed grid ticket
   hipLaunchKernelGGL(grad_update_kernel, dim3(blocks, n + 1), dim3(256), 0, s, a);

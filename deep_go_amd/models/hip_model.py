@@ -124,7 +124,10 @@ class HipGoNet:
         self.gate = torch.ones(1, dtype=torch.float32, device=dev)
         self.bad_steps = torch.zeros(1, dtype=torch.int32, device=dev)
         # fused end of step (grad_update): per-layer + grid tickets, zero between launches
-        self.gu_tickets = torch.zeros(cfg.numLayers + 1, dtype=torch.int32, device=dev)
+        self.gu_tickets = torch.zeros(4 * cfg.numLayers + 1, dtype=torch.int32, device=dev)
+        # the fused update with the pass 2 deferred writes the reduced gradient to self.grads
+        # only when asked (tests, tools): nothing in the step reads it
+        self.keep_grads = False
         # True while a step is issued whose gradient pass 2 is deferred into the fused update
         # (train_step / SegmentedStep's whole-step graph; see can_defer)
         self._defer = False
@@ -1315,7 +1318,8 @@ class HipGoNet:
                            self.ms.data_ptr() if self.ms is not None else 0,
                            float(self.cfg.rmsprop_decay), grad_scale, gate, self.lr.data_ptr(),
                            float(self.cfg.rateDecay), self.step_count.data_ptr(),
-                           self.gu_tickets.data_ptr(), self.bad_steps.data_ptr(), s)
+                           self.gu_tickets.data_ptr(), self.bad_steps.data_ptr(),
+                           int(self.keep_grads), s)
 
     def _gu_table(self, slabs: bool) -> np.ndarray:
         """grad_update's table: the per-step refresh row of every conv layer + where its

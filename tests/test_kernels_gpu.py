@@ -391,11 +391,12 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     torch.cuda.synchronize()
     assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
     assert scales[2].item() == s0[2].item()          # layer 1 s_w: amax_w inf -> unchanged
-    assert scales[3].item() == 0.25                  # layer 1 s_y from amax_y 64: 2^-2
+    H = 2.0                                          # conv_fp8.hip FP8_HEADROOM
+    assert scales[3].item() == 2.0 ** np.ceil(np.log2(H * 64.0 / 448.0))   # 2^-1
     assert scales[1].item() == s0[1].item()          # layer 0 s_y: amax_y NaN -> unchanged
     assert gscales[0].item() == g0[0].item() and gscales[2].item() == g0[2].item()
     assert abs(scales[0].item() - 100.0 * 1.05 / 448.0) < 1e-6      # finite ones update
-    assert gscales[1].item() == 2.0 ** np.ceil(np.log2(1.25 * 1000.0 / 57344.0))
+    assert gscales[1].item() == 2.0 ** np.ceil(np.log2(H * 1000.0 / 57344.0))
     s = sat.tolist()
     assert s[2 * 1] == 1 and s[2 * 0 + 1] == 1        # weights l1, activations l0
     assert s[2 * n + 0] == 1 and s[2 * n + 2] == 1    # gradients l0 (inf), l2 (NaN)

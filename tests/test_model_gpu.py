@@ -539,6 +539,7 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
         monkeypatch.setenv("DG_FUSED_UPDATE", fused)
         nets.append(_setup(layers, ch, 4, seed=2, **kw)[1])
     net0, net1 = nets
+    net1.keep_grads = True       # (the deferred update writes the gradient only on request)
     # (d = 64: no grouped weight-gradient launch, so the step reduces first and the fused
     # launch reads the flat gradient — still one update launch)
     assert net1.can_defer() == (ch >= 128)
@@ -589,6 +590,7 @@ def test_fused_update_skips_non_finite_gradient_entries():
     gradient entry is left unapplied (that parameter keeps its value), the step is counted
     in bad_steps, every other parameter still updates."""
     cfg, net, _ = _setup(4, 128, 4, seed=1)
+    net.keep_grads = True
     net.forward_backward()
     torch.cuda.synchronize()
     g_ref = net.grads.clone()

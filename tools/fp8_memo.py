@@ -1,0 +1,70 @@
+"""fp8 training fidelity bisection in the memorisation regime (tests/test_train_gpu.py
+test_fp8_stress_vs_bf16_memorisation): the same init and batch stream (a 256-position subset
+of the real fixture, cycled) through bf16 and through the fp8 path with each fp8 stage
+switched back to bf16 in turn — forward stack (always fp8 with dtype=fp8), e5m2 backward-data
+stack (DG_FP8_DGRAD), MX-fp8 weight gradients (DG_FP8_WGRAD).  Prints the 100-step window
+mean losses per variant as one JSON line (and writes gpurun_out/fp8_memo_12x<ch>.json).
+Usage: python tools/fp8_memo.py [CH] [STEPS] [RATE]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from deep_go_amd.config import ExperimentConfig
+    from deep_go_amd.data.dataset import PackedDataset
+    from deep_go_amd.data.loader import BatchLoader
+    from deep_go_amd.train.backends import HIPBackend
+    ch = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 800
+    rate = float(sys.argv[3]) if len(sys.argv) > 3 else 0.1
+    B = 64
+    fix = os.path.join(ROOT, "tests", "fixtures")
+    pk = PackedDataset.load(os.path.join(fix, "train.dgpack.npz"))
+    ld = BatchLoader(pk, B, threads=2, prefetch=4, seed=9, pin=False)
+    subset = [ld.next_numpy() for _ in range(256 // B)]
+    ld.close()
+    variants = [("bf16", "bf16", {}),
+                ("fp8", "fp8", {}),
+                ("fp8 bf16-wgrad", "fp8", {"DG_FP8_WGRAD": "0"}),
+                ("fp8 bf16-dgrad", "fp8", {"DG_FP8_DGRAD": "0", "DG_FP8_WGRAD": "0"}),
+                ]
+    out, flat0 = {}, None
+    for name, dt, env in variants:
+        for k in ("DG_FP8_WGRAD", "DG_FP8_DGRAD"):
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        cfg = ExperimentConfig(numLayers=12, channelSize=ch, batchSize=B, rate=rate,
+                               rateDecay=1e-5, head_relu=False, useCuda=True, seed=13,
+                               dtype=dt, checkpoint_dir="/tmp", data_root=fix)
+        be = HIPBackend(cfg, B, flat=flat0)
+        if flat0 is None:
+            flat0 = be.flat_params().clone()
+        ls = []
+        for k in range(N):
+            be.set_batch(*subset[k % len(subset)])
+            be.train_step()
+            ls.append(be.loss_sum() / B)
+        ls = np.array(ls)
+        rec = {"windows": [round(float(ls[w:w + 100].mean()), 4) for w in range(0, N, 100)]}
+        if dt == "fp8":
+            rec["sat"] = be.net.fp8_sat.cpu().tolist()
+            rec["scales"] = be.net.fp8_scales.cpu().tolist()
+            rec["gscales"] = be.net.fp8_gscales.cpu().tolist()
+        out[name] = rec
+        print(name, rec["windows"], flush=True)
+        del be
+        torch.cuda.empty_cache()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"fp8_memo_12x{ch}.json"), "w") as f:
+        json.dump(out, f)
+
+
+if __name__ == "__main__":
+    main()
