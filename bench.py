@@ -90,7 +90,12 @@ def parse(argv=None):
                          "proxy), at d = 128 one launch (the split doubles the split-K slab "
                          "traffic: +6%% compute for ~5 us less exposed comm); "
                          "profiles/r3_dp_overlap_proxy.txt")
-    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--grad-dtype", default="bf16", choices=["fp32", "bf16"],
+                    help="DP gradient wire format (the bucket all-reduces): bf16 halves the "
+                         "bytes on xGMI; every gradient pass 2 writes the bf16 twin itself "
+                         "and the fused update reads it (no conversion kernels).  Bounded "
+                         "against the fp32 wire by tests/test_train_gpu.py "
+                         "test_bf16_gradient_wire_200_step_curve")
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
                          "torch = torch.distributed between graph segments, proxy = world-1 "

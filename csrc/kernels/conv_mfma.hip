@@ -670,14 +670,16 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
   const int pos_blocks = bpart ? (NPTS * M + 255) / 256 : 0;
   if ((int)blockIdx.x >= main_blocks + pos_blocks + (bpart ? M : 0)) return;  // (shorter layer)
   if ((int)blockIdx.x >= main_blocks + pos_blocks) {
-    // gbias[c] = sum over (chunk, row) of rowpart (the fixed-order rows_sum, shared with the
-    // fused grad_update kernel); one workgroup per channel
+    // gbias[c] = sum over (chunk, row) of rowpart (the fixed-order rows_sum4 on one lane
+    // quad, shared with the fused grad_update kernel); one workgroup per channel
     const int c = blockIdx.x - main_blocks - pos_blocks;
     const float* rp = bpart + (size_t)bchunks * NPTS * M;  // rowpart [bchunks][19][M]
-    if (threadIdx.x == 0) {
-      const float v = rows_sum(rp, bchunks * BOARD, M, c);
-      gbias[c] = v;
-      if (Ls.gbias16[ly]) Ls.gbias16[ly][c] = f2bf(v);
+    if (threadIdx.x < 4) {
+      const float v = rows_sum4(rp, bchunks * BOARD, M, c, threadIdx.x);
+      if (threadIdx.x == 0) {
+        gbias[c] = v;
+        if (Ls.gbias16[ly]) Ls.gbias16[ly][c] = f2bf(v);
+      }
     }
     return;
   }

@@ -165,18 +165,27 @@ DG_DEV float chunk_sum(const float* part, int nchunks, size_t np) {
   return s0 + s1;
 }
 // per-channel bias gradient of channel c: sum of the R = chunks x 19 row partials
-// rowpart[r][C] (r mod 4 accumulators)
-DG_DEV float rows_sum(const float* rowpart, int R, int C, int c) {
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int r = 0;
-  for (; r + 4 <= R; r += 4) {
-    s0 += rowpart[(size_t)(r + 0) * C + c];
-    s1 += rowpart[(size_t)(r + 1) * C + c];
-    s2 += rowpart[(size_t)(r + 2) * C + c];
-    s3 += rowpart[(size_t)(r + 3) * C + c];
+// rowpart[r][C], as four partial sums (rows r = q mod 4 below 4 floor(R / 4), in increasing
+// r; the tail rows into partial 0) computed by 4 ADJACENT lanes q = lane & 3, combined as
+// (p0 + p1) + (p2 + p3) by two xor shuffles — every one of the 4 lanes returns the total.
+// All 4 lanes of a quad must call it.
+DG_DEV float rows_sum4(const float* rowpart, int R, int C, int c, int q) {
+  const int R4 = R & ~3;
+  float s = 0.f;
+  int r = q;
+  for (; r + 60 < R4; r += 64) {   // 16 rows of this lane per iteration, loads first
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = rowpart[(size_t)(r + 4 * k) * C + c];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += v[k];
   }
-  for (; r < R; ++r) s0 += rowpart[(size_t)r * C + c];
-  return (s0 + s1) + (s2 + s3);
+  for (; r < R4; r += 4) s += rowpart[(size_t)r * C + c];
+  if (q == 0)
+    for (int t = R4; t < R; ++t) s += rowpart[(size_t)t * C + c];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  return s;
 }
 
 // Exact floor(n / d) for 0 <= n < 2^22 and 1 <= d <= 4096 via a 64-bit magic

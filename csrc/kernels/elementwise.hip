@@ -695,22 +695,24 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
       const int c0 = cb * bch;
       const int R = S.bchunks * BOARD;
       const float* rowpart = S.bpart ? S.bpart + (size_t)S.bchunks * NPTS * C : nullptr;
-      if (tid < bch) {
-        const int c = c0 + tid;
+      if (tid < 4 * bch) {            // one lane quad per channel (rows_sum4)
+        const int cl = tid >> 2, c = c0 + cl;
         float g;
         if (S.bpart) {
-          g = rows_sum(rowpart, R, C, c);
+          g = rows_sum4(rowpart, R, C, c, tid & 3);
         } else {
           const long long o = S.b_off + c;
           g = a.G16 ? bf2f(a.G16[o]) : a.G[o];
         }
-        float ms_v = a.MS ? a.MS[S.b_off + c] : 0.f;
-        s_b[tid] = gu_update(a.P[S.b_off + c], g, a.MS != nullptr, ms_v, l, a.rms_decay,
-                             a.gscale, apply, bad);
-        // (the per-channel bias, its gradient and mean square are written by the last block
-        // of this channel block below: the others still read the old values here)
-        s_gb[tid] = g;
-        s_ms[tid] = ms_v;
+        if ((tid & 3) == 0) {
+          float ms_v = a.MS ? a.MS[S.b_off + c] : 0.f;
+          s_b[cl] = gu_update(a.P[S.b_off + c], g, a.MS != nullptr, ms_v, l, a.rms_decay,
+                              a.gscale, apply, bad);
+          // (the per-channel bias, its gradient and mean square are written by the last
+          // block of this channel block below: the others still read the old values here)
+          s_gb[cl] = g;
+          s_ms[cl] = ms_v;
+        }
       }
       __syncthreads();
       const size_t np = (size_t)NPTS * C;
