@@ -201,14 +201,14 @@ std::string read_text(const std::string& path) {
 // Returns number of positions written, 0 if the game has no dan ranks (dropped like
 // transcribe_from_to, makedata.lua:550), -1 on an illegal move.  A ".done" marker file is
 // written on success (the reference used "file 100 exists" as its only resume marker).
-int transcribe_one(const std::string& src, const std::string& dst, bool skip_done) {
+int transcribe_one(const std::string& src, const std::string& dst, bool skip_done, bool mark_ko) {
   if (skip_done && (file_exists(dst + "/.done") || file_exists(dst + "/100"))) return -2;
   const SgfGame g = parse_sgf(read_text(src));
   if (!g.has_ranks()) return 0;
   std::vector<uint8_t> planes(g.moves.size() * NUM_STORED * NN);
   int n;
   try {
-    n = game_positions(g.handicap, g.moves, planes.data());
+    n = game_positions(g.handicap, g.moves, planes.data(), mark_ko);
   } catch (const IllegalMove&) {
     return -1;
   }
@@ -280,17 +280,33 @@ PYBIND11_MODULE(_dgcpu, m) {
 
   m.def("game_positions",
         [](const std::vector<std::tuple<int, int, int>>& handicap,
-           const std::vector<std::tuple<int, int, int>>& moves) {
+           const std::vector<std::tuple<int, int, int>>& moves, bool mark_ko) {
           const auto h = to_moves(handicap), mv = to_moves(moves);
           py::array_t<uint8_t> out({(py::ssize_t)mv.size(), (py::ssize_t)9, (py::ssize_t)19,
                                     (py::ssize_t)19});
           {
             py::gil_scoped_release nogil;
-            game_positions(h, mv, out.mutable_data());
+            game_positions(h, mv, out.mutable_data(), mark_ko);
           }
           return out;
         },
-        "stored planes [n,9,19,19] of the position before each move (0-based x,y)");
+        py::arg("handicap"), py::arg("moves"), py::arg("mark_ko") = false,
+        "stored planes [n,9,19,19] of the position before each move (0-based x,y); mark_ko: "
+        "the simple-ko point as KO_MARK in the liberty plane");
+  m.def("game_ko_points",
+        [](const std::vector<std::tuple<int, int, int>>& handicap,
+           const std::vector<std::tuple<int, int, int>>& moves) {
+          Board b;
+          for (const Move& m : to_moves(handicap)) b.play(m);
+          std::vector<int> ko;
+          for (const Move& m : to_moves(moves)) {
+            ko.push_back(b.ko());
+            b.play(m);
+          }
+          return ko;
+        },
+        "simple-ko point (x*19+y, -1 none) of the position before each move");
+  m.attr("KO_MARK") = (int)KO_MARK;
   m.def("summarize",
         [](u8arr stones, py::object ages) {
           if (stones.size() != NN) throw std::runtime_error("stones must have 361 entries");
@@ -324,21 +340,21 @@ PYBIND11_MODULE(_dgcpu, m) {
     d["white_rank"] = g.white_rank;
     return d;
   });
-  m.def("transcribe_sgf", [](const std::string& text) -> py::object {
+  m.def("transcribe_sgf", [](const std::string& text, bool mark_ko) -> py::object {
     const SgfGame g = parse_sgf(text);
     if (!g.has_ranks()) return py::none();
     py::array_t<uint8_t> planes({(py::ssize_t)g.moves.size(), (py::ssize_t)9, (py::ssize_t)19,
                                  (py::ssize_t)19});
-    game_positions(g.handicap, g.moves, planes.mutable_data());
+    game_positions(g.handicap, g.moves, planes.mutable_data(), mark_ko);
     py::dict d;
     d["planes"] = planes;
     d["moves"] = moves_py(g.moves);
     d["ranks"] = py::make_tuple(g.black_rank, g.white_rank);
     return d;
-  });
+  }, py::arg("text"), py::arg("mark_ko") = false);
   m.def("transcribe_files",
         [](const std::vector<std::pair<std::string, std::string>>& jobs, int threads,
-           bool skip_done) {
+           bool skip_done, bool mark_ko) {
           std::vector<int> result(jobs.size(), 0);
           std::atomic<size_t> next{0};
           {
@@ -348,7 +364,7 @@ PYBIND11_MODULE(_dgcpu, m) {
               pool.emplace_back([&] {
                 for (size_t i = next++; i < jobs.size(); i = next++) {
                   try {
-                    result[i] = transcribe_one(jobs[i].first, jobs[i].second, skip_done);
+                    result[i] = transcribe_one(jobs[i].first, jobs[i].second, skip_done, mark_ko);
                   } catch (const std::exception&) {
                     result[i] = -3;
                   }
@@ -359,6 +375,7 @@ PYBIND11_MODULE(_dgcpu, m) {
           return result;
         },
         py::arg("jobs"), py::arg("threads") = 8, py::arg("skip_done") = true,
+        py::arg("mark_ko") = false,
         "parallel SGF->t7 transcription; per job: #positions, 0 dropped (no dan ranks), "
         "-1 illegal move, -2 skipped (done), -3 I/O error");
 
@@ -442,10 +459,11 @@ PYBIND11_MODULE(_dgcpu, m) {
     std::fclose(f);
   });
   m.def("expand",
-        [](u8arr planes, u8arr player, u8arr rank) {
+        [](u8arr planes, u8arr player, u8arr rank, bool ko) {
           const py::ssize_t B = player.size();
           if (planes.size() != B * 9 * NN) throw std::runtime_error("planes must be [B,9,19,19]");
-          py::array_t<float> out({B, (py::ssize_t)kNetPlanes, (py::ssize_t)19, (py::ssize_t)19});
+          const int NPL = ko ? kNetPlanesKo : kNetPlanes;
+          py::array_t<float> out({B, (py::ssize_t)NPL, (py::ssize_t)19, (py::ssize_t)19});
           float* o = out.mutable_data();
           const uint8_t* pl = planes.data();
           const uint8_t* py_ = player.data();
@@ -453,11 +471,12 @@ PYBIND11_MODULE(_dgcpu, m) {
           {
             py::gil_scoped_release nogil;
             for (py::ssize_t b = 0; b < B; ++b)
-              expand_position(pl + b * 9 * NN, py_[b], rk[b], o + b * kNetPlanes * NN);
+              expand_position(pl + b * 9 * NN, py_[b], rk[b], o + b * NPL * NN, NPL);
           }
           return out;
         },
-        "9 stored planes -> 37 network planes (float32 0/1)");
+        py::arg("planes"), py::arg("player"), py::arg("rank"), py::arg("ko") = false,
+        "9 stored planes -> 37 network planes (float32 0/1); ko: + plane 37, the simple-ko point");
   m.def("random_positions", [](int n, uint64_t seed, int max_moves) {
     std::vector<uint8_t> planes, player, rank;
     std::vector<int32_t> label;

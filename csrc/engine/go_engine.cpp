@@ -38,9 +38,13 @@ void Board::clear() {
   mark_.fill(0);
   lmark_.fill(0);
   stamp_ = 0;
+  ko_ = -1;
 }
 
-void Board::set_stones(const uint8_t* stones) { std::memcpy(s_.data(), stones, NN); }
+void Board::set_stones(const uint8_t* stones) {
+  std::memcpy(s_.data(), stones, NN);
+  ko_ = -1;
+}
 
 int Board::liberties(int idx, std::vector<int>* group, std::vector<int>* libs) {
   const uint8_t p = s_[idx];
@@ -120,9 +124,17 @@ void Board::play(const Move& m) {
   for (int i = 0; i < NN; ++i)
     if (age_[i] > 0 && age_[i] < 255) ++age_[i];
   std::vector<int> cleared;
-  place_and_resolve(idx, m.player, nullptr, nullptr, &cleared);
+  int captured = 0;
+  place_and_resolve(idx, m.player, nullptr, &captured, &cleared);
   age_[idx] = 1;
   for (int c : cleared) age_[c] = 1;
+  // simple ko: one stone captured by a lone stone now in atari (its one liberty is the
+  // captured point, which the opponent may not retake at once)
+  ko_ = -1;
+  if (captured == 1 && s_[idx] == m.player) {
+    std::vector<int> grp, lbs;
+    if (liberties(idx, &grp, &lbs) == 1 && grp.size() == 1) ko_ = lbs[0];
+  }
 }
 
 void Board::kills_and_liberties(int idx, int player, int* kills, int* libs_after) {
@@ -164,7 +176,7 @@ bool Board::ladder_moves(int gx, const int libs2[2], std::vector<int>* result, i
   return true;
 }
 
-void Board::summarize(uint8_t* out) {
+void Board::summarize(uint8_t* out, bool mark_ko) {
   uint8_t* st = out + P_STONES * NN;
   uint8_t* lib = out + P_LIBS * NN;
   uint8_t* age = out + P_AGE * NN;
@@ -203,15 +215,16 @@ void Board::summarize(uint8_t* out) {
       for (int mv : moves) lad[mv] = (uint8_t)members.size();
     }
   }
+  if (mark_ko && ko_ >= 0) lib[ko_] = KO_MARK;
 }
 
 int game_positions(const std::vector<Move>& handicap, const std::vector<Move>& moves,
-                   uint8_t* out) {
+                   uint8_t* out, bool mark_ko) {
   Board b;
   for (const Move& h : handicap) b.play(h);
   int k = 0;
   for (const Move& m : moves) {
-    b.summarize(out + (size_t)k * NUM_STORED * NN);
+    b.summarize(out + (size_t)k * NUM_STORED * NN, mark_ko);
     b.play(m);
     ++k;
   }

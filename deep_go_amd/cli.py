@@ -5,7 +5,7 @@
   resume    CKPT --iters N [--reset-optimizer] [--id NAME] [key=value ...]
             (experiments/repeated.lua: -gpu/-num/-iters -> --device/--id/--iters)
   eval      CKPT [--split test] [--n N]          (top-1 / NLL on a split; never done in the ref)
-  makedata  scatter SRC DST train=N validation=N test=N | transcribe SRC DST [--threads T]
+  makedata  scatter SRC DST train=N validation=N test=N | transcribe SRC DST [--threads T] [--ko]
             | count ROOT SPLIT | pack ROOT SPLIT
   export    CKPT OUT.t7        (reference Torch7 experiment table)
   import    IN.t7 OUT.model
@@ -110,7 +110,7 @@ def cmd_makedata(args):
         print(json.dumps(md.scatter(a[1], a[2], {k: int(v) for k, v in cats.items()},
                                     seed=args.seed)))
     elif op == "transcribe":
-        print(json.dumps(md.transcribe(a[1], a[2], threads=args.threads)))
+        print(json.dumps(md.transcribe(a[1], a[2], threads=args.threads, mark_ko=args.ko)))
     elif op == "count":
         print(md.count(a[1], a[2]))
     elif op == "pack":
@@ -180,6 +180,8 @@ def main(argv=None):
     e.set_defaults(fn=cmd_eval)
     m = sub.add_parser("makedata")
     m.add_argument("--threads", type=int, default=32)
+    m.add_argument("--ko", action="store_true",
+                   help="mark the simple-ko point in the stored liberty plane (for ko_plane=1)")
     m.add_argument("--seed", type=int, default=0)
     m.add_argument("rest", nargs="*")
     m.set_defaults(fn=cmd_makedata)

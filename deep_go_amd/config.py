@@ -24,6 +24,8 @@ NUM_POINTS = BOARD * BOARD  # 361
 # Network input planes (dataloader.lua:6-14): STONE=1, LIBERTIES=4, LIBERTIES_AFTER=8,
 # KILL=15, AGE=22, LADDER=27, RANK=28, TOTAL=37 (plane 28 is always zero).
 NUM_INPUT_PLANES = 37
+# + the optional simple-ko plane (ExperimentConfig.ko_plane; data/features.py)
+NUM_INPUT_PLANES_KO = 38
 # Stored uint8 planes per position (dataloader.lua:20-27).
 NUM_STORED_PLANES = 9
 
@@ -76,6 +78,9 @@ class ExperimentConfig:
     nan_policy: str = "guard"
     nan_max_skips: int = 10
     log_interval: int = 10         # train.lua:119
+    # optional 38th input plane: the simple-ko point (needs data made with makedata --ko;
+    # off = the reference's 37-plane layout)
+    ko_plane: bool = False
     id: Optional[str] = None
 
     # ---- derived layer schedule ----
@@ -85,13 +90,17 @@ class ExperimentConfig:
             [self.head_kernel] if self.numLayers >= 2 else [])
 
     @property
+    def input_planes(self) -> int:
+        return NUM_INPUT_PLANES_KO if self.ko_plane else NUM_INPUT_PLANES
+
+    @property
     def channels(self) -> List[int]:
-        return [NUM_INPUT_PLANES] + [self.channelSize] * (self.numLayers - 1) + [1]
+        return [self.input_planes] + [self.channelSize] * (self.numLayers - 1) + [1]
 
     def layer_specs(self) -> List[Tuple[int, int, int]]:
-        """(c_in, c_out, kernel) per layer; layer 1 sees the 37 input planes."""
+        """(c_in, c_out, kernel) per layer; layer 1 sees the 37 (38) input planes."""
         if self.numLayers == 1:
-            return [(NUM_INPUT_PLANES, 1, self.first_kernel)]
+            return [(self.input_planes, 1, self.first_kernel)]
         ch, ks = self.channels, self.kernels
         return [(ch[i], ch[i + 1], ks[i]) for i in range(self.numLayers)]
 

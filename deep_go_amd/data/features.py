@@ -1,4 +1,5 @@
-"""Feature-plane specification: 9 stored uint8 planes -> 37 network input planes.
+"""Feature-plane specification: 9 stored uint8 planes -> 37 network input planes (38 with
+the optional simple-ko plane).
 
 Stored planes (``dataloader.lua:20-27``, written by ``flatten_data`` ``:30-39``), index
 ``[plane][x][y]`` with x = first SGF coordinate:
@@ -10,6 +11,10 @@ Network planes (``preprocess``, ``dataloader.lua:50-92``), relative to the playe
   7 empty & liberties_after[p] == 0, 8-12 liberties_after[p] == 1..5, 13 >= 6,
   14-19 kills[p] == 1..6, 20 kills[p] >= 7, 21-25 age == 1..5, 26 ladder[p] >= 1,
   27 always zero (the reference's off-by-one rank offset), 28-36 rank of p == 1..9 dan.
+  37 (optional, ``ExperimentConfig.ko_plane``): the simple-ko point — an addition, the
+  reference tracks no ko.  It rides in stored plane 1 as ``KO_MARK`` at an EMPTY point (plane 1
+  is 0 at empty points otherwise; ``makedata --ko`` writes it), so the liberty planes 3-6 are
+  gated on a stone (identical on files without the mark).
 Label = 19*x0 + y0 (``dataloader.lua:89``).
 
 This numpy version is the CPU oracle; the GPU path is ``expand_features_kernel``
@@ -21,19 +26,23 @@ from __future__ import annotations
 import numpy as np
 
 NUM_PLANES = 37
+NUM_PLANES_KO = 38
+KO_MARK = 255     # csrc/engine/go_engine.h
 BOARD = 19
 
 
-def expand(planes: np.ndarray, player: int, rank: int, out: np.ndarray | None = None) -> np.ndarray:
-    """planes uint8 [9,19,19] -> float32 [37,19,19]."""
+def expand(planes: np.ndarray, player: int, rank: int, out: np.ndarray | None = None,
+           ko: bool = False) -> np.ndarray:
+    """planes uint8 [9,19,19] -> float32 [37,19,19] ([38,19,19] with ko)."""
     p = int(player)
     st = planes[0]
-    lib = planes[1]
+    lib = np.where(planes[0] != 0, planes[1], 0)
     la = planes[2 + (p - 1)]
     kill = planes[4 + (p - 1)]
     age = planes[6]
     lad = planes[7 + (p - 1)]
-    x = out if out is not None else np.zeros((NUM_PLANES, BOARD, BOARD), np.float32)
+    n = NUM_PLANES_KO if ko else NUM_PLANES
+    x = out if out is not None else np.zeros((n, BOARD, BOARD), np.float32)
     x[:] = 0
     x[0] = st == 0
     x[1] = st == p
@@ -53,14 +62,17 @@ def expand(planes: np.ndarray, player: int, rank: int, out: np.ndarray | None = 
     x[26] = lad >= 1
     if 1 <= rank <= 9:
         x[27 + rank] = 1.0
+    if ko:
+        x[37] = (st == 0) & (planes[1] == KO_MARK)
     return x
 
 
-def expand_batch(planes: np.ndarray, player: np.ndarray, rank: np.ndarray) -> np.ndarray:
+def expand_batch(planes: np.ndarray, player: np.ndarray, rank: np.ndarray,
+                 ko: bool = False) -> np.ndarray:
     B = planes.shape[0]
-    out = np.zeros((B, NUM_PLANES, BOARD, BOARD), np.float32)
+    out = np.zeros((B, NUM_PLANES_KO if ko else NUM_PLANES, BOARD, BOARD), np.float32)
     for b in range(B):
-        expand(planes[b], int(player[b]), int(rank[b]), out[b])
+        expand(planes[b], int(player[b]), int(rank[b]), out[b], ko)
     return out
 
 

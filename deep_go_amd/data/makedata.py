@@ -6,7 +6,9 @@
 * ``transcribe(src_split_dir, dst_split_dir, threads)`` — parallel SGF -> per-position t7
   files ``<dst>/<subdir>/<game>.sgf/<k>`` (``transcribe_in_parallel``, :506-533) on the C++
   thread pool; games whose ranks are not both dan are dropped; finished games are skipped on
-  re-runs (done marker, the reference's "file 100 exists").
+  re-runs (done marker, the reference's "file 100 exists").  ``mark_ko`` (an addition, off by
+  default) marks each position's simple-ko point in the stored liberty plane for models built
+  with ``ko_plane=1`` (data/features.py).
 * ``count(root, split)`` — the ``count_game_moves.sh`` index.
 * ``pack(root, split)`` — packed ``<root>/<split>.dgpack.npz`` for fast training.
 """
@@ -47,12 +49,13 @@ def scatter(src: str, dst: str, categories: Dict[str, int], seed: int = 0) -> Di
     return out
 
 
-def transcribe(src: str, dst: str, threads: int = 32, skip_done: bool = True) -> Dict[str, int]:
+def transcribe(src: str, dst: str, threads: int = 32, skip_done: bool = True,
+               mark_ko: bool = False) -> Dict[str, int]:
     jobs = []
     for f in all_files(src):
         rel = os.path.relpath(f, src)
         jobs.append((f, os.path.join(dst, rel)))
-    res = cpu().transcribe_files(jobs, threads, skip_done)
+    res = cpu().transcribe_files(jobs, threads, skip_done, mark_ko)
     stats = {"games": len(jobs), "written": sum(1 for r in res if r > 0),
              "positions": sum(r for r in res if r > 0), "dropped_no_dan": res.count(0),
              "illegal": res.count(-1), "skipped_done": res.count(-2), "io_errors": res.count(-3)}

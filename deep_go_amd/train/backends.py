@@ -73,7 +73,8 @@ class CPUBackend:
 
     def set_batch(self, planes, player, rank, labels):
         pl = _np(planes, np.uint8).reshape(-1, 9, 19, 19)
-        self._x = torch.from_numpy(cpu().expand(pl, _np(player, np.uint8), _np(rank, np.uint8)))
+        self._x = torch.from_numpy(cpu().expand(pl, _np(player, np.uint8), _np(rank, np.uint8),
+                                                 self.cfg.ko_plane))
         self._y = torch.from_numpy(_np(labels, np.int64))
 
     def _forward(self, x):

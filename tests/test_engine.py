@@ -151,3 +151,93 @@ def test_transcribe_files(eng, tmp_path):
     p = eng.read_position(str(out / "g" / "3"))
     assert (p["player"], p["x"], p["y"], p["ranks"]) == (1, 4, 16, (2, 3))
     assert eng.transcribe_files([(str(sgf), str(out / "g"))], 1) == [-2]  # done marker
+
+
+# A ko fight (an addition: the reference tracks no ko, makedata.lua:329-354).  Black
+# (3,4) (4,3) (5,4), White (3,5) (4,6) (5,5) around the empty (4,5); White's lone stone at
+# (4,4) is captured by Black (4,5) -> ko at (4,4) (80); White retakes at once (the engine,
+# like the reference, does not enforce ko) -> ko at (4,5) (81); Black connects elsewhere.
+KO_SGF = ("BR[2d]\r\nWR[4d]\r\n;B[de];W[df];B[ed];W[eg];B[fe];W[ff];B[pp];W[ee]\r\n"
+          ";B[ef];W[ee];B[pd];W[dd]\r\n")
+KO_BEFORE = [-1] * 9 + [80, 81, -1]
+
+
+@pytest.mark.parametrize("eol", ["\r\n", "\n"])
+def test_simple_ko_golden(eng, eol):
+    text = KO_SGF.replace("\r\n", eol)
+    g = eng.parse_sgf(text)
+    assert len(g["moves"]) == 12
+    assert eng.game_ko_points(g["handicap"], g["moves"]) == KO_BEFORE
+    plain = eng.transcribe_sgf(text)["planes"]
+    marked = eng.transcribe_sgf(text, mark_ko=True)["planes"]
+    K = eng.KO_MARK
+    for k, ko in enumerate(KO_BEFORE):
+        if ko < 0:
+            assert np.array_equal(plain[k], marked[k]), k
+            continue
+        x, y = divmod(ko, 19)
+        assert plain[k, 0, x, y] == 0 and plain[k, 1, x, y] == 0
+        assert marked[k, 1, x, y] == K
+        diff = plain[k] != marked[k]
+        assert diff.sum() == 1, k  # only the mark differs
+    # the captured-and-retaken stones really left the board
+    assert plain[9, 0, 4, 4] == 0 and plain[9, 0, 4, 5] == 1
+    assert plain[10, 0, 4, 5] == 0 and plain[10, 0, 4, 4] == 2
+
+
+def test_capture_without_ko(eng):
+    """Capturing one stone with a capturer that keeps 2+ liberties, or capturing two stones,
+    leaves no ko point."""
+    # black captures the white stone at (4,4) from (4,5), which keeps liberties (3,5),(5,5)
+    mv = [(1, 3, 4), (2, 4, 4), (1, 4, 3), (2, 15, 15), (1, 5, 4), (2, 15, 3), (1, 4, 5),
+          (2, 3, 15)]
+    assert eng.game_ko_points([], mv) == [-1] * 8
+    # two white stones (4,4)-(4,5) captured at once
+    mv2 = [(1, 3, 4), (2, 4, 4), (1, 3, 5), (2, 4, 5), (1, 4, 3), (2, 15, 15), (1, 5, 4),
+           (2, 15, 3), (1, 5, 5), (2, 3, 15), (1, 4, 6), (2, 3, 3)]
+    assert eng.game_ko_points([], mv2) == [-1] * 12
+
+
+def test_ko_plane_expansion(eng):
+    from deep_go_amd.data.features import expand_batch
+    g = eng.parse_sgf(KO_SGF)
+    marked = eng.transcribe_sgf(KO_SGF, mark_ko=True)["planes"]
+    plain = eng.transcribe_sgf(KO_SGF)["planes"]
+    n = len(KO_BEFORE)
+    player = np.array([m[0] for m in g["moves"]], np.uint8)
+    rank = np.where(player == 1, 2, 4).astype(np.uint8)
+    x38 = eng.expand(marked, player, rank, ko=True)
+    assert x38.shape == (n, 38, 19, 19)
+    assert np.array_equal(x38, expand_batch(marked, player, rank, ko=True))
+    for k, ko in enumerate(KO_BEFORE):
+        hot = np.flatnonzero(x38[k, 37].reshape(-1))
+        assert list(hot) == ([] if ko < 0 else [ko]), k
+    # the 37 parity planes ignore the mark: identical to the unmarked files
+    assert np.array_equal(eng.expand(marked, player, rank), eng.expand(plain, player, rank))
+    assert np.array_equal(x38[:, :37], eng.expand(plain, player, rank))
+
+
+def test_transcribe_files_mark_ko(eng, tmp_path):
+    sgf = tmp_path / "ko.sgf"
+    sgf.write_bytes(KO_SGF.encode())
+    out = tmp_path / "out"
+    assert eng.transcribe_files([(str(sgf), str(out / "a"))], 1, True, True) == [12]
+    assert eng.transcribe_files([(str(sgf), str(out / "b"))], 1) == [12]
+    a = eng.read_position(str(out / "a" / "10"))["planes"]
+    b = eng.read_position(str(out / "b" / "10"))["planes"]
+    assert a[1, 4, 4] == eng.KO_MARK and b[1, 4, 4] == 0
+
+
+def test_ko_plane_config_and_cpu_training():
+    """ko_plane=1 builds a 38-plane first layer; the CPU trainer sees the mark."""
+    from deep_go_amd.config import ExperimentConfig
+    from deep_go_amd.train.backends import CPUBackend
+    cfg = ExperimentConfig(numLayers=3, channelSize=8, batchSize=4, ko_plane=True)
+    assert cfg.layer_specs()[0] == (38, 8, 5)
+    be = CPUBackend(cfg, 4)
+    marked = cpu().transcribe_sgf(KO_SGF, mark_ko=True)["planes"][8:12]
+    player = np.array([1, 2, 1, 2], np.uint8)
+    be.set_batch(marked, player, np.full(4, 3, np.uint8), np.array([5, 6, 7, 8], np.int32))
+    assert be._x.shape == (4, 38, 19, 19)
+    assert be._x[1, 37, 4, 4] == 1 and be._x[2, 37, 4, 5] == 1 and be._x[:, 37].sum() == 2
+    be.train_step()
