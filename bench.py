@@ -28,8 +28,9 @@ random labels is meaningless and is not reported here; held-out top-1 on the rea
 comes from ``tools/real_data_run.py`` (profiles/).
 
 After the headline timing (never inside it) the same process measures:
-  * ``secondary``: the d=256 configs (BASELINE configs 3-5 per GPU: 12x256 bf16 and fp8) with
-    the same K/W and the same communicator (under N > 1 that is config 3/5's DP=N step);
+  * ``secondary``: the headline network in fp8 (12x128 fp8) and the d=256 configs (BASELINE
+    configs 3-5 per GPU: 12x256 bf16 and fp8) with the same K/W and the same communicator
+    (under N > 1 that is config 3/5's DP=N step);
   * ``dp`` (N > 1 or --force-dp): communicator kind and RCCL version, per-rank devices, bytes
     all-reduced per step, the step's bucket collectives timed alone (us/step, bus GB/s), the
     same network's step without collectives, and from those the exposed communication time
@@ -113,7 +114,7 @@ def parse(argv=None):
                          "overhead")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
-    ap.add_argument("--secondary", default="256:bf16,256:fp8",
+    ap.add_argument("--secondary", default="128:fp8,256:bf16,256:fp8",
                     help="after the headline: other configs as CHANNELS:DTYPE,... ('' = none)")
     ap.add_argument("--no-report", action="store_true",
                     help="skip the post-timing DP report (isolated collectives, no-comm step)")

@@ -33,7 +33,7 @@ void dg_conv_stack2_set_mode(int on);
 void dg_conv_stack_f8_set_mode(int m);
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
                             const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
-                            hipStream_t stream);
+                            const long long* sr_step, hipStream_t stream);
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, hipStream_t stream);
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
@@ -134,6 +134,7 @@ hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t n
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s);
+int dg_grad_update_tickets();
 int dg_grad_update_cols();
 hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
@@ -237,7 +238,7 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_stack_f8", [](int C, int epi, uintptr_t table, int nl, uintptr_t X0,
                             uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t stream) {
     check(dg_conv_stack_f8(C, epi, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
-                           P<unsigned>(amax_x0), B, nullptr, S(stream)),
+                           P<unsigned>(amax_x0), B, nullptr, nullptr, S(stream)),
           "conv_stack_f8");
   }, "fp8 layer stack (C = 128 | 256; epi 1 forward e4m3, 2 backward-data e5m2): table rows "
      "{A8_frag, pbias_frag, Y, mask, s_in, s_w, s_out, amax_out}; X0 quantized with *s_x0");
@@ -245,10 +246,20 @@ PYBIND11_MODULE(_dghip, m) {
                                uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t y8,
                                uintptr_t stream) {
     check(dg_conv_stack_f8(C, epi, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
-                           P<unsigned>(amax_x0), B, P<long long>(y8), S(stream)),
+                           P<unsigned>(amax_x0), B, P<long long>(y8), nullptr, S(stream)),
           "conv_stack_f8_y8");
   }, "conv_stack_f8 + fp8 copy-out: y8 = nl + 1 int64 {X8_0, Y8 of each layer} (448-row "
      "frames; the last layer's 0)");
+  m.def("conv_stack_f8_dgrad", [](int C, uintptr_t table, int nl, uintptr_t X0,
+                                  uintptr_t s_x0, uintptr_t amax_x0, int B, uintptr_t y8,
+                                  uintptr_t sr_step, uintptr_t stream) {
+    check(dg_conv_stack_f8(C, 2, P<long long>(table), nl, P<void>(X0), P<float>(s_x0),
+                           P<unsigned>(amax_x0), B, P<long long>(y8), P<long long>(sr_step),
+                           S(stream)),
+          "conv_stack_f8_dgrad");
+  }, "the e5m2 backward-data stack (conv_stack_f8 epi 2) with optional fp8 copies (y8, 0: "
+     "none) and stochastic rounding seeded by the int64 device step counter sr_step (0: "
+     "round to nearest even)");
   m.def("conv_wgrad_win8", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
                               int splits, uintptr_t stream) {
     check(dg_conv_wgrad_win8(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
@@ -464,6 +475,8 @@ PYBIND11_MODULE(_dghip, m) {
           "grad_update");
   }, "fused gradient pass 2 (slabs / bias partials, or the flat gradient) + SGD / RMSProp + "
      "operand refresh + LR decay (elementwise.hip grad_update_kernel)");
+  m.def("grad_update_tickets", []() { return dg_grad_update_tickets(); },
+        "uint32 ticket counters grad_update needs (zeroed once; the kernel leaves them zeroed)");
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });

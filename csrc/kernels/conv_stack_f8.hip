@@ -113,6 +113,9 @@ struct F8Args {
   uint8_t* X8_0;        // optional fp8 copy of the quantized input [B][448][C]
   int nl;
   int fuse_head;        // C = 128, EPI_FWD only
+  // EPI_DGRAD: stochastic rounding of the e5m2 gradient quantization (MODE bit 32), random
+  // bits from a hash of (step counter, layer, element); null: round to nearest even
+  const long long* sr_step;
   F8Layer L[MAXL];
   dghead::HeadMArgs head;
 };
@@ -169,6 +172,34 @@ DG_DEV uint32_t pack8x4(float a, float b, float c, float d) {
   v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
   return (uint32_t)v;
 }
+// e5m2 packing with stochastic rounding: the 4 conversions take 4 rotations of one 32-bit
+// hash (each conversion's rounding decision rests on different hash bits).  Unbiased: a
+// value between two e5m2 neighbours rounds up with probability equal to its fractional
+// position, so the dgrad chain and the weight-gradient sums over ~92k pixels keep the small
+// consistent components that round-to-nearest erases (the memorisation stall of
+// tools/fp8_memo.py: tests/test_train_gpu.py test_fp8_stress_vs_bf16_memorisation).
+DG_DEV uint32_t sr_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+DG_DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+DG_DEV uint32_t pack_bf8x4_sr(float a, float b, float c, float d, uint32_t h) {
+  int v = __builtin_amdgcn_cvt_sr_bf8_f32(a, (int)h, 0, 0);
+  v = __builtin_amdgcn_cvt_sr_bf8_f32(b, (int)rotl32(h, 8), v, 1);
+  v = __builtin_amdgcn_cvt_sr_bf8_f32(c, (int)rotl32(h, 16), v, 2);
+  v = __builtin_amdgcn_cvt_sr_bf8_f32(d, (int)rotl32(h, 24), v, 3);
+  return (uint32_t)v;
+}
+template <int EPI, int MODE>
+DG_DEV uint32_t pack8x4q(float a, float b, float c, float d, uint32_t key) {
+  if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0) return pack_bf8x4_sr(a, b, c, d, sr_hash(key));
+  return pack8x4<EPI>(a, b, c, d);
+}
+
 // 2 e4m3 / e5m2 -> 2 bf16 scaled by the power of two s (one v_cvt_scalef32_pk_bf16_*)
 template <int EPI, bool HI>
 DG_DEV uint32_t deq2(uint32_t w, float s) {
@@ -195,7 +226,8 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // spilled VGPRs.  MODE bit 16 (with 8): no dequantized bf16 copy-out of the non-last layers —
 // every consumer reads the fp8 copies instead (forward: the MX-fp8 weight gradient, the
 // backward-data chain reads ReLU bits; backward-data: the weight gradient and the bias-gradient
-// partials read the e5m2 copies); the table's Y is null there
+// partials read the e5m2 copies); the table's Y is null there.  MODE bit 32 (EPI_DGRAD):
+// stochastic rounding of the e5m2 quantization (pack_bf8x4_sr)
 template <int C, int EPI, int MODE>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   using G = Geo<C>;
@@ -213,6 +245,10 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   char* sI = smem + SCRATCH;                       // e4m3 image (C = 128 last layer: bf16)
   float* s_amax = (float*)(smem + G::AMAX_OFF);    // 2 x 8 floats (alternating per layer)
 
+  // stochastic-rounding key base of this step (EPI_DGRAD, MODE bit 32)
+  uint32_t sr_seed = 0;
+  if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0)
+    sr_seed = (uint32_t)*a.sr_step * 0x9E3779B9u;
   // ---- prologue: quantize the bf16 input frame into the image ----
   {
     const float inv = 1.f / *a.s_x0;
@@ -231,8 +267,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         x[e] = fmaxf(fminf(x[e] * inv, QMAX), -QMAX);
       }
       uint2 o;
-      o.x = pack8x4<EPI>(x[0], x[1], x[2], x[3]);
-      o.y = pack8x4<EPI>(x[4], x[5], x[6], x[7]);
+      const uint32_t key = sr_seed + (uint32_t)((b * FF + f) * C + q * 8);
+      o.x = pack8x4q<EPI, MODE>(x[0], x[1], x[2], x[3], key);
+      o.y = pack8x4q<EPI, MODE>(x[4], x[5], x[6], x[7], key + 4);
       *(uint2*)(sI + f * ROWB + (((q >> 1) ^ fsig<C>(f)) * 16) + (q & 1) * 8) = o;
       // the fp8 copy of the quantized input (the fp8 weight gradient's operand)
       if constexpr ((MODE & 8) != 0) *(uint2*)(a.X8_0 + ((size_t)(b * FP8P + f) * C + q * 8)) = o;
@@ -431,6 +468,11 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
           *(uint4*)(sIe + img * H_BYTES + row * 128 + q * 16) = uint4{0, 0, 0, 0};
         }
       }
+      // stochastic-rounding key of this lane's first element (fragment (0, 0)) in this pass
+      uint32_t sr_lane = 0;
+      if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0)
+        sr_lane = sr_seed + (uint32_t)(l + 1) * 0x85EBCA6Bu +
+                  (uint32_t)((b * NPTS + wn * NF * 16 + lr) * C + 128 * hp + wm * 64 + lq * 4);
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int p = wn * NF * 16 + j * 16 + lr;
@@ -461,7 +503,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
           if (!last) {
             vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             auto qz = [&](float x) { return fmaxf(fminf(x * inv_y, QMAX), -QMAX); };
-            const uint32_t q8 = pack8x4<EPI>(qz(v[0]), qz(v[1]), qz(v[2]), qz(v[3]));
+            // (key: layer l + 1's seed + the element index (b, p, co); the prologue is layer 0)
+            const uint32_t key = sr_lane + (uint32_t)(j * 16 * C + i * 16);
+            const uint32_t q8 = pack8x4q<EPI, MODE>(qz(v[0]), qz(v[1]), qz(v[2]), qz(v[3]), key);
             if (to_image) {
               // channel co = 128 hp + cl: slot co / 16 (XOR sig), byte co % 16
               const int co = 128 * hp + cl;
@@ -574,6 +618,11 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
   bool any_y = false;
   for (int i = 0; i + 1 < a.nl; ++i) any_y |= a.L[i].Y != nullptr;
   if (epi == EPI_DGRAD) {
+    if (a.sr_step) {
+      if (!y8) return launch_f8<C, EPI_DGRAD, 32>(a, B, stream);
+      return any_y ? launch_f8<C, EPI_DGRAD, 40>(a, B, stream)
+                   : launch_f8<C, EPI_DGRAD, 56>(a, B, stream);
+    }
     if (!y8) return launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
     return any_y ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream)
                  : launch_f8<C, EPI_DGRAD, 24>(a, B, stream);
@@ -592,11 +641,13 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
 
 hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void* X0,
                      const float* s_x0, unsigned* amax_x0, int B, const dghead::HeadMArgs* head,
-                     const long long* y8, hipStream_t stream) {
+                     const long long* y8, const long long* sr_step, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || B <= 0 || !s_x0 || !amax_x0) return hipErrorInvalidValue;
   if ((C != 128 && C != 256) || (epi != EPI_FWD && epi != EPI_DGRAD)) return hipErrorInvalidValue;
   if (head && epi != EPI_FWD) return hipErrorInvalidValue;
+  if (sr_step && epi != EPI_DGRAD) return hipErrorInvalidValue;
   F8Args a;
+  a.sr_step = sr_step;
   a.X0 = (const char*)X0;
   a.s_x0 = s_x0;
   a.amax_x0 = amax_x0;
@@ -637,11 +688,12 @@ extern "C" {
 void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 
 // table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask, s_in, s_w,
-// s_out, amax_out} (int64); epi 1 forward, 2 backward-data
+// s_out, amax_out} (int64); epi 1 forward, 2 backward-data; sr_step (backward-data): the
+// device step counter seeding stochastic rounding of the e5m2 gradients (null: nearest even)
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
                             const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
-                            hipStream_t stream) {
-  return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, y8, stream);
+                            const long long* sr_step, hipStream_t stream) {
+  return f8_launch(C, epi, table, nl, X0, s_x0, amax_x0, B, nullptr, y8, sr_step, stream);
 }
 
 // C = 128: the head on the last layer's LDS image; 256: on its bf16 frame, read back
@@ -653,7 +705,7 @@ hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, cons
                                      const long long* y8, hipStream_t stream) {
   const dghead::HeadMArgs h{nullptr, w, bias, posb, labels, loss, pred, nullptr, (char*)dZ,
                             gw_part, dzb, head_relu, grad_scale};
-  return f8_launch(C, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, y8, stream);
+  return f8_launch(C, EPI_FWD, table, nl, X0, s_x0, amax_x0, B, &h, y8, nullptr, stream);
 }
 
 }  // extern "C"

@@ -328,11 +328,8 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   const dim3 grid(nl * (M / 64) * (Cx / 64) * splits);
   // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
   // the same — profiles/r3_fp8_wgrad_ab.txt)
-  static const int ra = getenv("DG_WIN8_RA") ? atoi(getenv("DG_WIN8_RA")) : 1;   // (A/B)
-  if (ra == 2)
-    hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 2>), grid, dim3(512), 0, stream, a, Ls);
-  else
-    hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1>), grid, dim3(512), 0, stream, a, Ls);
+  // (B reads 2 taps ahead measured the same as 1: profiles/r4_s1_fused_update_and_fp8_bisection.txt)
+  hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1>), grid, dim3(512), 0, stream, a, Ls);
   return hipGetLastError();
 }
 

@@ -508,13 +508,18 @@ weight_refresh_kernel(WRefreshArgs a, double* lr, double decay, long long* step)
 // (64 co x 64 ci at one tap per tile): sum the slabs (the same fixed order as
 // wgrad_reduce_kernel: bit-identical gradients), write the fp32 gradient, update the fp32
 // master weight, and write the tile's operand copies from the updated values.  The bias
-// part: every block recomputes the layer's new per-channel bias (C sums of R row partials)
-// and updates its share of the per-position biases, then writes the forward epilogue's bias
-// tables from the new values.  Readers of an old value and the writer of its new value must
-// not race: the per-channel biases and the learning rate are written by the LAST block to
-// finish (an atomic ticket per layer / for the grid, taken after the block's reads; the
-// counters are reset by that block, so the launch is graph-replayable).  grid.y = n: the
-// plain range (the head's parameters, whose gradient head_reduce already wrote).
+// part runs in its OWN blocks (blockIdx.x >= tblocks, beside the tile blocks rather than after
+// their tiles — each block's chain of dependent memory round trips is the launch's limiter):
+// a bias block recomputes the new per-channel bias of its 64-channel block (64 sums of R row
+// partials), updates its share of the per-position biases, then writes the forward
+// epilogue's bias tables from the new values.  Readers of an old value and the writer of its
+// new value must not race: the per-channel biases and the learning rate are written by the
+// LAST block to finish (atomic tickets taken after the block's reads; the counters are reset
+// by that block, so the launch is graph-replayable).  The grid's ticket is a 3-level tree
+// (16-block groups -> rows -> grid): device-scope atomics on ONE address serialize, and a
+// flat grid ticket (1872 increments at 12x256) cost more than the rest of the launch.
+// grid.y = n: the plain range (the head's parameters, whose gradient head_reduce already
+// wrote).
 //
 // Non-finite gradient entries are not applied (the parameter keeps its value) and flag the
 // step (bad_steps += 1 once); gate (device, optional) = 0 skips every update (a non-finite
@@ -531,8 +536,17 @@ constexpr int MAX_GU = 20;
 // blocks per layer, one ticket each
 constexpr int GU_BCH = 64;
 DG_DEV int gu_bch(int C) { return C < GU_BCH ? C : GU_BCH; }
+constexpr int GU_NB = 16;        // bias blocks per 64-channel block (of the widest layer)
+constexpr int GU_TG = 16;        // blocks per first-level ticket group
+constexpr int GU_MAXG = 64;      // groups per row (grid.x <= 1024)
+// ticket layout (uint32): per (layer, channel block) | per row | per (row, group) | grid
+constexpr int GU_T_ROW = 4 * MAX_GU;
+constexpr int GU_T_GRP = GU_T_ROW + MAX_GU + 1;
+constexpr int GU_T_GRID = GU_T_GRP + (MAX_GU + 1) * GU_MAXG;
+constexpr int GU_TICKETS = GU_T_GRID + 1;
 struct GUArgs {
   int n;
+  int tblocks;         // blocks [0, tblocks) of a row: weight tiles; the rest: biases
   WRefreshLayer L[MAX_GU];
   GUSrc S[MAX_GU];
   long long plain_off, plain_n;
@@ -545,8 +559,8 @@ struct GUArgs {
   const double* lr;
   double decay;
   long long* step;
-  unsigned* tickets;   // [4n + 1]: per (layer, channel block), then the grid's (+ the
-                       // non-finite flag << 16)
+  unsigned* tickets;   // [GU_TICKETS] zeroed (the tree counters carry the non-finite flag
+                       // << 16)
   int write_grads;     // slab mode: also write the reduced fp32 gradient (tests / tools)
   int* bad_steps;
 };
@@ -611,7 +625,8 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
     const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
     const size_t zstride = (size_t)S.Mpad * S.KP;
     const bool vec = S.slab && (L.cin & 3) == 0 && (L.cinp & 3) == 0 && (S.KP & 3) == 0;
-    for (int tix = blockIdx.x; tix < tiles; tix += gridDim.x) {
+    const bool tile_block = (int)blockIdx.x < a.tblocks;
+    for (int tix = blockIdx.x; tile_block && tix < tiles; tix += a.tblocks) {
       const int t = tix / (nct * nit);
       const int r = tix - t * nct * nit;
       const int cot = r / nit, cit = r - cot * nit;
@@ -620,6 +635,7 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
         // (16 16-B slab loads in flight per thread; slab_sums4 = slab_sum4's order per element)
         const float* src[4];
         bool ok[4];
+        f32x4 pp[4];   // the weights, loaded beside the slabs
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + 256 * u;
@@ -627,6 +643,8 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
           const int co = cot * 64 + rr, ci = cit * 64 + cc;
           ok[u] = co < L.cout && ci < L.cin;
           src[u] = S.slab + (ok[u] ? (size_t)co * S.KP + t * L.cinp + ci : 0);
+          const size_t o = ok[u] ? ((size_t)co * L.taps + t) * L.cin + ci : 0;
+          pp[u] = *(const f32x4*)(Pw + o);
         }
         f32x4 gs[4];
         slab_sums4<4>(src, S.splits, zstride, gs);
@@ -640,7 +658,7 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
             const f32x4 g4 = gs[u];
             const size_t o = ((size_t)co * L.taps + t) * L.cin + ci;
             if (a.write_grads) *(f32x4*)(Gw + o) = g4;
-            const f32x4 p4 = *(const f32x4*)(Pw + o);
+            const f32x4 p4 = pp[u];
             f32x4 m4 = {0.f, 0.f, 0.f, 0.f};
             if (MSw) m4 = *(const f32x4*)(MSw + o);
 #pragma unroll
@@ -681,17 +699,19 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
       __syncthreads();    // tileS complete (also orders the next tile's writes after reads)
       if (refresh_needs_tile(L)) refresh_tile_copies(L, t, cot, cit, tileS, inv8);
     }
-    refresh_amax(L, wmax, s_amax);
-    // ---- biases, in channel blocks of 64: bias block (cb, pb) = channels 64 cb .. +63 over
-    // position range pb.  Each recomputes the NEW per-channel bias of its 64 channels only (64
-    // sums of R row partials), updates its positions' per-position biases and writes those
-    // entries of the bias tables.
+    if (tile_block) refresh_amax(L, wmax, s_amax);   // (slot blockIdx.x < tblocks <= 512)
+    // ---- biases (blocks tblocks..), in channel blocks of 64: bias block (cb, pb) = channels
+    // 64 cb .. +63 over position range pb.  Each recomputes the NEW per-channel bias of its 64
+    // channels only (64 sums of R row partials), updates its positions' per-position biases
+    // and writes those entries of the bias tables.
     const int C = L.cout;
     const int bch = gu_bch(C);
     const int ncb = C / bch;
-    const int npb = gridDim.x / ncb > 0 ? (int)gridDim.x / ncb : 1;
-    const int cb = blockIdx.x % ncb, pb = blockIdx.x / ncb;
-    if (pb < npb) {
+    const int nbb = (int)gridDim.x - a.tblocks;
+    const int npb = nbb / ncb;
+    const int bidx = (int)blockIdx.x - a.tblocks;
+    const int cb = bidx % ncb, pb = bidx / ncb;
+    if (!tile_block && pb < npb) {
       const int c0 = cb * bch;
       const int R = S.bchunks * BOARD;
       const float* rowpart = S.bpart ? S.bpart + (size_t)S.bchunks * NPTS * C : nullptr;
@@ -756,10 +776,11 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
   if (bad) s_flag[0] = 1u;     // (benign same-value race)
   __syncthreads();
   int cbw = -1;   // the channel block this block closes (last of its position blocks)
-  if (ly < a.n) {
+  if (ly < a.n && (int)blockIdx.x >= a.tblocks) {
     const int ncb = a.L[ly].cout / gu_bch(a.L[ly].cout);
-    const int npb = gridDim.x / ncb > 0 ? (int)gridDim.x / ncb : 1;
-    const int cb = blockIdx.x % ncb, pb = blockIdx.x / ncb;
+    const int npb = ((int)gridDim.x - a.tblocks) / ncb;
+    const int bidx = (int)blockIdx.x - a.tblocks;
+    const int cb = bidx % ncb, pb = bidx / ncb;
     if (pb < npb) {
       if (tid == 0)
         s_flag[1] = atomicAdd(&a.tickets[4 * ly + cb], 1u) == (unsigned)npb - 1 ? 1u : 0u;
@@ -779,15 +800,32 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
     if (tid == 0) a.tickets[4 * ly + cbw] = 0u;
   }
   if (tid == 0) {
-    const unsigned total = gridDim.x * gridDim.y;   // < 2^16 (host check)
-    const unsigned old = atomicAdd(&a.tickets[4 * a.n], 1u + (s_flag[0] ? 0x10000u : 0u));
-    if ((old & 0xFFFFu) == total - 1) {
-      double* lrw = const_cast<double*>(a.lr);
-      *lrw = *lrw * (1.0 - a.decay);
-      if (a.step) *a.step += 1;
-      const bool flagged = (old >> 16) != 0u || s_flag[0];
-      if (flagged && a.bad_steps && apply) *a.bad_steps += 1;
-      a.tickets[4 * a.n] = 0u;
+    // 3-level ticket tree: group of GU_TG blocks -> row -> grid; the last arrival at each
+    // level resets its counter and moves up, carrying the non-finite flag in the high half
+    unsigned* T = a.tickets;
+    const unsigned g = blockIdx.x / GU_TG;
+    const unsigned ng = (gridDim.x + GU_TG - 1) / GU_TG;
+    const unsigned gsize = min((unsigned)GU_TG, gridDim.x - g * GU_TG);
+    unsigned flag = s_flag[0] ? 0x10000u : 0u;
+    unsigned* tg = T + GU_T_GRP + ly * GU_MAXG + g;
+    unsigned old = atomicAdd(tg, 1u + flag);
+    if ((old & 0xFFFFu) == gsize - 1) {
+      *tg = 0u;
+      flag = ((old >> 16) != 0u || flag) ? 0x10000u : 0u;
+      old = atomicAdd(T + GU_T_ROW + ly, 1u + flag);
+      if ((old & 0xFFFFu) == ng - 1) {
+        T[GU_T_ROW + ly] = 0u;
+        flag = ((old >> 16) != 0u || flag) ? 0x10000u : 0u;
+        old = atomicAdd(T + GU_T_GRID, 1u + flag);
+        if ((old & 0xFFFFu) == gridDim.y - 1) {
+          double* lrw = const_cast<double*>(a.lr);
+          *lrw = *lrw * (1.0 - a.decay);
+          if (a.step) *a.step += 1;
+          const bool flagged = (old >> 16) != 0u || flag;
+          if (flagged && a.bad_steps && apply) *a.bad_steps += 1;
+          T[GU_T_GRID] = 0u;
+        }
+      }
     }
   }
 }
@@ -999,11 +1037,13 @@ hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double d
 // The fused gradient pass 2 + optimizer + refresh (grad_update_kernel).  table: n rows of
 // GU_COLS int64 = the 20 weight_refresh columns, then {slab, bpart, splits, Mpad, KP,
 // bchunks, w_off, b_off, pos_off} (slab / bpart 0: the layer's gradient is read from G / G16).
-// plain_off / plain_n: a flat range updated from G only (the head).  tickets: 4n + 1 zeroed
-// uint32 (left zeroed).  write_grads: with slabs, also store the reduced gradient in G.  Same block count per layer as dg_weight_refresh (the fp8 |w| max
-// slots).
+// plain_off / plain_n: a flat range updated from G only (the head).  tickets:
+// dg_grad_update_tickets() zeroed uint32 (left zeroed).  write_grads: with slabs, also store
+// the reduced gradient in G.  Tile blocks per row = dg_weight_refresh's block count (the fp8
+// |w| max slots), plus GU_NB bias blocks per 64-channel block of the widest layer.
 constexpr int GU_COLS = 29;
 int dg_grad_update_cols() { return GU_COLS; }
+int dg_grad_update_tickets() { return GU_TICKETS; }
 hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
@@ -1013,7 +1053,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
     return hipErrorInvalidValue;
   GUArgs a;
   a.n = n;
-  int maxtotal = 1;
+  int maxtotal = 1, maxncb = 1;
   for (int i = 0; i < n; ++i) {
     const long long* t = table + GU_COLS * i;
     WRefreshLayer& L = a.L[i];
@@ -1038,6 +1078,8 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
       return hipErrorInvalidValue;   // the refresh row must describe the same parameters
     const int tiles = refresh_tiles(L);
     if (tiles > maxtotal) maxtotal = tiles;
+    const int ncb = L.cout > GU_BCH ? L.cout / GU_BCH : 1;
+    if (ncb > maxncb) maxncb = ncb;
   }
   a.plain_off = plain_off;
   a.plain_n = plain_n;
@@ -1054,8 +1096,9 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
   a.tickets = tickets;
   a.bad_steps = bad_steps;
   a.write_grads = write_grads;
-  const int blocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
-  if (blocks * (n + 1) >= 0x10000) return hipErrorInvalidValue;   // the packed grid ticket
+  a.tblocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
+  const int blocks = a.tblocks + GU_NB * maxncb;
+  if (blocks > GU_TG * GU_MAXG) return hipErrorInvalidValue;   // the ticket tree's groups
   hipLaunchKernelGGL(grad_update_kernel, dim3(blocks, n + 1), dim3(256), 0, s, a);
   return hipGetLastError();
 }

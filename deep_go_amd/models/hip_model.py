@@ -124,7 +124,7 @@ class HipGoNet:
         self.gate = torch.ones(1, dtype=torch.float32, device=dev)
         self.bad_steps = torch.zeros(1, dtype=torch.int32, device=dev)
         # fused end of step (grad_update): per-layer + grid tickets, zero between launches
-        self.gu_tickets = torch.zeros(4 * cfg.numLayers + 1, dtype=torch.int32, device=dev)
+        self.gu_tickets = torch.zeros(self.h.grad_update_tickets(), dtype=torch.int32, device=dev)
         # the fused update with the pass 2 deferred writes the reduced gradient to self.grads
         # only when asked (tests, tools): nothing in the step reads it
         self.keep_grads = False
@@ -249,6 +249,9 @@ class HipGoNet:
         # bf16 frames (448 rows per board); allocated by _fuse_forward_stack /
         # _fuse_dgrad_stack for the layers they cover
         self.fp8_wgrad = self.fp8 and os.environ.get("DG_FP8_WGRAD", "1") != "0"
+        # stochastic rounding of the fp8 backward-data stack's e5m2 gradients, seeded by the
+        # device step counter (conv_stack_f8.hip pack_bf8x4_sr; DG_FP8_SR=0: nearest even)
+        self.fp8_sr = self.fp8 and os.environ.get("DG_FP8_SR", "1") != "0"
         self.x8q: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.dz8q: List[Optional[torch.Tensor]] = [None] * len(self.plans)
         self.fp8_scales = torch.ones(2 * len(self.plans), dtype=torch.float32, device=dev)
@@ -780,9 +783,10 @@ class HipGoNet:
                      self.relu_mask[i - 1].data_ptr(), GS + 4 * i, S + 4 * 2 * i,
                      GS + 4 * (i - 1), GA + 4 * (i - 1)] for i in run]
             self._dstack_table = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-            args = (self.plans[run[0]].cout, self.h.EPI_DGRAD, self._dstack_table.ctypes.data,
+            args = (self.plans[run[0]].cout, self._dstack_table.ctypes.data,
                     len(run), self.dz[run[0]].data_ptr(), GS + 4 * run[0], GA + 4 * run[0],
                     self.B)
+            sr = self.step_count.data_ptr() if self.fp8_sr else 0
             if self.fp8_wgrad:
                 # the raw e5m2 gradient of every run layer for the fp8 weight gradients:
                 # dz8q[top] = the quantized input, dz8q[i - 1] = each non-last output
@@ -794,10 +798,10 @@ class HipGoNet:
                 # dz8q[j] that are exactly the bf16 frame dz[j] (the copy-out bytes)
                 self._dz8_exact = {i - 1 for i in run if i != run[-1]}
                 self._dstack_y8 = np.ascontiguousarray(np.array(y8, dtype=np.int64))
-                self._bwd_pre.append((self.h.conv_stack_f8_y8,
-                                      args + (self._dstack_y8.ctypes.data,)))
+                self._bwd_pre.append((self.h.conv_stack_f8_dgrad,
+                                      args + (self._dstack_y8.ctypes.data, sr)))
             else:
-                self._bwd_pre.append((self.h.conv_stack_f8, args))
+                self._bwd_pre.append((self.h.conv_stack_f8_dgrad, args + (0, sr)))
         else:
             rows = [[self.wdfrag[i].data_ptr(), 0, self.dz[i - 1].data_ptr(),
                      self.relu_mask[i - 1].data_ptr()] for i in run]

@@ -316,13 +316,18 @@ def test_expand_features():
     planes[:, 0] = rng.integers(0, 3, (B, 19, 19))
     for c in range(1, 9):
         planes[:, c] = rng.integers(0, 12, (B, 19, 19))
+    # simple-ko marks at a few empty points (liberty plane = KO_MARK; data/features.py)
+    for b in range(B):
+        e = np.flatnonzero(planes[b, 0].reshape(-1) == 0)[b % 3]
+        planes[b, 1].reshape(-1)[e] = 255
     player = rng.integers(1, 3, B).astype(np.uint8)
     rank = rng.integers(1, 10, B).astype(np.uint8)
     got = Fn.expand_features(torch.from_numpy(planes), torch.from_numpy(player),
                              torch.from_numpy(rank))
-    ref = expand_batch(planes, player, rank)
-    assert torch.equal(got[:, :37].cpu(), torch.from_numpy(ref))
-    assert got[:, 37:].abs().sum().item() == 0
+    ref = expand_batch(planes, player, rank, ko=True)
+    assert torch.equal(got[:, :38].cpu(), torch.from_numpy(ref))
+    assert got[:, 37].sum().item() == B
+    assert got[:, 38:].abs().sum().item() == 0
 
 
 def test_bias_grad():
@@ -396,7 +401,8 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     assert scales[1].item() == s0[1].item()          # layer 0 s_y: amax_y NaN -> unchanged
     assert gscales[0].item() == g0[0].item() and gscales[2].item() == g0[2].item()
     assert abs(scales[0].item() - 100.0 * 1.05 / 448.0) < 1e-6      # finite ones update
-    assert gscales[1].item() == 2.0 ** np.ceil(np.log2(H * 1000.0 / 57344.0))
+    HG = 8.0                                         # FP8_GRAD_HEADROOM
+    assert gscales[1].item() == 2.0 ** np.ceil(np.log2(HG * 1000.0 / 57344.0))
     s = sat.tolist()
     assert s[2 * 1] == 1 and s[2 * 0 + 1] == 1        # weights l1, activations l0
     assert s[2 * n + 0] == 1 and s[2 * n + 2] == 1    # gradients l0 (inf), l2 (NaN)

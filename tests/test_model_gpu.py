@@ -24,7 +24,7 @@ def _oracle(net, data):
     from deep_go_amd.data.features import expand_batch
     from deep_go_amd.models.gocnn import reference_forward
     planes, player, rank, labels = data
-    x = torch.from_numpy(expand_batch(planes, player, rank))
+    x = torch.from_numpy(expand_batch(planes, player, rank, ko=net.cfg.ko_plane))
     # oracle sees the bf16-rounded weights the kernels use
     flat = net.params.detach().cpu().clone()
     for spec in net.layout.layers[:-1]:
@@ -179,6 +179,61 @@ def test_model_matches_oracle(layers, ch, B):
         a, b = g[off:off + n], g_ref[off:off + n]
         err = (a - b).norm() / (b.norm() + 1e-12)
         assert err < 0.08, (name, err.item())
+
+
+def _mark_ko(data):
+    """A simple-ko mark (liberty plane = KO_MARK) at one empty point per board."""
+    planes = data[0].copy()
+    for b in range(planes.shape[0]):
+        e = np.flatnonzero(planes[b, 0].reshape(-1) == 0)[3 * b + 1]
+        planes[b, 1].reshape(-1)[e] = 255
+    return (planes,) + tuple(data[1:])
+
+
+def _set(net, data):
+    net.set_batch(*(torch.from_numpy(a).cuda() for a in data))
+
+
+@pytest.mark.parametrize("layers,ch,B", [(3, 64, 5), (4, 128, 3)])
+def test_ko_plane_model_matches_oracle(layers, ch, B):
+    """ko_plane=1: a 38-plane first layer whose plane 37 is the ko mark, through the same
+    kernels (the mark is expanded into padded input channel 37)."""
+    cfg, net, data = _setup(layers, ch, B, ko_plane=True)
+    assert net.layout.layers[0].cin == 38
+    data = _mark_ko(data)
+    _set(net, data)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, _, g_ref = _oracle(net, data)
+    assert abs(net.mean_loss().item() - loss_ref) < 2e-2 * max(1.0, abs(loss_ref))
+    g = net.grads.cpu()
+    for name, off, n in net.layout.tensor_ranges():
+        a, b = g[off:off + n], g_ref[off:off + n]
+        err = (a - b).norm() / (b.norm() + 1e-12)
+        assert err < 0.08, (name, err.item())
+    # the ko-plane weights get a real gradient
+    L0 = net.layout.layers[0]
+    w0 = g[L0.w_off:L0.w_off + L0.w_numel].view(L0.cout, -1, 38)  # [cout][k*k][cin]
+    assert w0[:, :, 37].abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("ch", [64, 128])
+def test_37_plane_model_ignores_ko_mark(ch):
+    """Without ko_plane the mark changes nothing: bit-identical loss and gradients (d = 64:
+    the VALU head's LDS float atomics sum in a varying order — within 1e-5 then)."""
+    cfg, net, data = _setup(4, ch, 4)
+    net.forward_backward()
+    torch.cuda.synchronize()
+    loss0, g0 = net.mean_loss().item(), net.grads.clone()
+    _set(net, _mark_ko(data))
+    net.forward_backward()
+    torch.cuda.synchronize()
+    if ch >= 128:
+        assert net.mean_loss().item() == loss0
+        assert torch.equal(net.grads, g0)
+    else:
+        assert abs(net.mean_loss().item() - loss0) < 1e-6
+        assert torch.allclose(net.grads, g0, rtol=1e-5, atol=1e-7)
 
 
 def test_every_gradient_is_written_each_step():

@@ -161,3 +161,70 @@ def test_fp8_stack_matches_emulated_oracle(C, nl, epi):
             assert torch.equal((nz << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8), ms[l])
         assert ys[l][:, 0].abs().sum().item() == 0 and ys[l][:, :, 0].abs().sum().item() == 0
         xin = ys[l]
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_fp8_dgrad_stochastic_rounding_is_unbiased(C):
+    """The e5m2 backward-data stack with stochastic rounding (conv_stack_f8_dgrad, sr_step =
+    the device step counter): deterministic for one step, different across steps, and
+    unbiased — the mean over 32 steps of the last layer's output approaches the unquantized
+    fp32 chain far closer than round-to-nearest-even does (whose error is systematic)."""
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    torch.manual_seed(5)
+    B, nl = 4, 2
+    x = LY.alloc_frame(B, C, 1, DEV)
+    LY.frame_interior(x, 1).copy_(1e-3 * torch.randn(B, 19, 19, C, device=DEV))
+    s = torch.empty(nl + 1, device=DEV)
+    s[0] = 2.0 ** math.ceil(math.log2(x.float().abs().max().item() / 57344.0))
+    ws = torch.empty(nl, device=DEV)
+    amax = torch.zeros(nl + 1, dtype=torch.int32, device=DEV)
+    W8, ys, ms = [], [], []
+    for l in range(nl):
+        w = torch.randn(C, 9, C, device=DEV) / (3 * C ** 0.5)
+        ws[l] = w.abs().max() / 448.0
+        s[1 + l] = 2.0 ** (-20 - l)
+        W8.append((w / ws[l]).clamp(-448, 448).to(torch.float8_e4m3fn))
+        ys.append(LY.alloc_frame(B, C, 1, DEV))
+        ms.append(torch.randint(0, 256, (B, 361, C // 8), dtype=torch.uint8, device=DEV))
+    frags = [LY.stack_frag_f8(w8.view(torch.uint8)) for w8 in W8]
+    f4 = 4
+    tab = np.array([[frags[i].data_ptr(), 0, ys[i].data_ptr(), ms[i].data_ptr(),
+                     s.data_ptr() + f4 * i, ws.data_ptr() + f4 * i, s.data_ptr() + f4 * (i + 1),
+                     amax.data_ptr() + f4 * (i + 1)] for i in range(nl)], dtype=np.int64)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+
+    def run(sr):
+        h.conv_stack_f8_dgrad(C, tab.ctypes.data, nl, x.data_ptr(), s.data_ptr(),
+                              amax.data_ptr(), B, 0, step.data_ptr() if sr else 0,
+                              stream_handle())
+        torch.cuda.synchronize()
+        return LY.frame_interior(ys[-1], 1).float().clone()
+
+    # unquantized fp32 chain with the same e4m3 weights and masks
+    v = LY.frame_interior(x, 1).float()
+    for l in range(nl):
+        wq = W8[l].float().reshape(C, 3, 3, C).permute(0, 3, 1, 2) * ws[l].item()
+        v = F.conv2d(v.permute(0, 3, 1, 2).cpu(), wq.cpu(), padding=1).to(DEV).permute(0, 2, 3, 1)
+        bits = (ms[l].long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1
+        v = v * bits.reshape(B, 19, 19, C).float()
+    ref = v
+    rel = lambda a: ((a - ref).norm() / ref.norm()).item()  # noqa: E731
+    rne = run(False)
+    step.fill_(7)
+    a, b = run(True), run(True)
+    assert torch.equal(a, b)                    # one step: deterministic
+    step.fill_(8)
+    assert not torch.equal(run(True), a)        # another step: other rounding
+    acc = torch.zeros_like(ref)
+    errs = []
+    for k in range(32):
+        step.fill_(100 + k)
+        y = run(True)
+        errs.append(rel(y))
+        acc += y
+    e_rne, e_mean = rel(rne), rel(acc / 32)
+    print(f"C={C}: rne {e_rne:.4f} single-SR {np.mean(errs):.4f} mean-of-32 {e_mean:.4f}")
+    assert max(errs) < 3 * e_rne               # one SR draw: same order as nearest-even
+    assert e_mean < 0.4 * e_rne                 # the mean converges: unbiased

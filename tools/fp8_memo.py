@@ -2,7 +2,10 @@
 test_fp8_stress_vs_bf16_memorisation): the same init and batch stream (a 256-position subset
 of the real fixture, cycled) through bf16 and through the fp8 path with each fp8 stage
 switched back to bf16 in turn — forward stack (always fp8 with dtype=fp8), e5m2 backward-data
-stack (DG_FP8_DGRAD), MX-fp8 weight gradients (DG_FP8_WGRAD).  Prints the 100-step window
+stack (DG_FP8_DGRAD), MX-fp8 weight gradients (DG_FP8_WGRAD) — and the e5m2 gradients rounded
+to nearest even instead of stochastically (DG_FP8_SR=0).  Round 4 result (12x128, 800
+steps, rate 0.1): nearest-even e5m2 gradients stall near 5.3 nats while bf16 reaches 2.7;
+bf16 backward-data recovers it (so the forward is fine): the fix is stochastic rounding.  Prints the 100-step window
 mean losses per variant as one JSON line (and writes gpurun_out/fp8_memo_12x<ch>.json).
 Usage: python tools/fp8_memo.py [CH] [STEPS] [RATE]"""
 import json
@@ -32,12 +35,16 @@ def main():
     ld.close()
     variants = [("bf16", "bf16", {}),
                 ("fp8", "fp8", {}),
+                ("fp8 rne", "fp8", {"DG_FP8_SR": "0"}),
                 ("fp8 bf16-wgrad", "fp8", {"DG_FP8_WGRAD": "0"}),
                 ("fp8 bf16-dgrad", "fp8", {"DG_FP8_DGRAD": "0", "DG_FP8_WGRAD": "0"}),
                 ]
+    only = os.environ.get("FP8_MEMO_VARIANTS")
+    if only:
+        variants = [v for v in variants if v[0] in only.split(",")]
     out, flat0 = {}, None
     for name, dt, env in variants:
-        for k in ("DG_FP8_WGRAD", "DG_FP8_DGRAD"):
+        for k in ("DG_FP8_WGRAD", "DG_FP8_DGRAD", "DG_FP8_SR"):
             os.environ.pop(k, None)
         os.environ.update(env)
         cfg = ExperimentConfig(numLayers=12, channelSize=ch, batchSize=B, rate=rate,
