@@ -94,7 +94,8 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
                              const float* s_w, const float* s_y, unsigned* amax_y, void* mask,
                              hipStream_t stream);
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w, unsigned* amax_y, float w_margin,
-                               int* sat, float* gscales, unsigned* gamax, hipStream_t s);
+                               float g_headroom, int* sat, float* gscales, unsigned* gamax,
+                               hipStream_t s);
 hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
                          const float* s_w, hipStream_t s);
 hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
@@ -322,12 +323,12 @@ PYBIND11_MODULE(_dghip, m) {
           "conv_board_fp8");
   });
   m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, int nparts_w,
-                                uintptr_t amax_y, float w_margin, uintptr_t sat,
-                                uintptr_t gscales, uintptr_t gamax, uintptr_t stream) {
+                                uintptr_t amax_y, float w_margin, float g_headroom,
+                                uintptr_t sat, uintptr_t gscales, uintptr_t gamax,
+                                uintptr_t stream) {
     check(dg_fp8_update_scales(n, P<float>(scales), P<unsigned>(amax_w), nparts_w,
-                               P<unsigned>(amax_y),
-                               w_margin, P<int>(sat), P<float>(gscales), P<unsigned>(gamax),
-                               S(stream)),
+                               P<unsigned>(amax_y), w_margin, g_headroom, P<int>(sat),
+                               P<float>(gscales), P<unsigned>(gamax), S(stream)),
           "fp8_update_scales");
   });
   m.def("weight_fp8", [](uintptr_t w, uintptr_t wf8, int cout, int cin, int taps, int cinp,

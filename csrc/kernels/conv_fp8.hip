@@ -242,18 +242,16 @@ conv_board_fp8_kernel(Fp8Args a) {
 // max.  1.25 left 0.8% of layer-steps saturated in the slow 1000-step stress run but 2-9%
 // per layer in a memorisation run (rate 0.1, loss falling > 1 nat: amax grows faster than
 // 25% per step); 2.0 (one more power of two, one less e4m3 binade at the bottom) keeps
-// that regime under 1%.  Weights use their own margin (w_margin, host).  The e5m2 gradients
-// take 8 (FP8_GRAD_HEADROOM): with stochastic rounding (conv_stack_f8.hip) the memorisation
-// run trains through to ~0 loss, where gradient amax jumps more than 2x between steps (2% of
-// gradient layer-steps saturated at 12x256 with 2.0); e5m2's 30 binades leave room for 2 more
-// at the top.
+// that regime under 1%.  Weights use their own margin (w_margin, host), the e5m2 gradients
+// their own headroom (g_headroom, host: hip_model.FP8_G_HEADROOM — with stochastic rounding,
+// conv_stack_f8.hip, the memorisation run trains through to ~0 loss, where gradient amax
+// jumps more than 2x between steps: 2% of gradient layer-steps saturated at 12x256 with 2).
 constexpr float FP8_HEADROOM = 2.0f;
-constexpr float FP8_GRAD_HEADROOM = 8.0f;
 __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* scales,
                                                                unsigned* amax_w, int nparts_w,
                                                                unsigned* amax_y, float w_margin,
-                                                               int* sat, float* gscales,
-                                                               unsigned* gamax) {
+                                                               float g_headroom, int* sat,
+                                                               float* gscales, unsigned* gamax) {
   const int l = blockIdx.x, lane = threadIdx.x;
   unsigned mwb = 0u;   // unsigned max of non-negative float bits: inf / NaN bits win
   for (int j = lane; j < nparts_w; j += 64) {
@@ -275,7 +273,7 @@ __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* sca
     const float mg = __uint_as_float(gamax[l]);
     const bool ok = __builtin_isfinite(mg);
     if (sat && (!ok || mg > 57344.f * gscales[l])) sat[2 * n + l] += 1;
-    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(FP8_GRAD_HEADROOM * mg / 57344.f)));
+    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(g_headroom * mg / 57344.f)));
     gamax[l] = 0u;
   }
   const float mw = __uint_as_float(mwb);
@@ -390,11 +388,11 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
 }
 
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w,
-                               unsigned* amax_y, float w_margin, int* sat, float* gscales,
-                               unsigned* gamax, hipStream_t s) {
-  if (n <= 0 || n > 1024 || nparts_w <= 0) return hipErrorInvalidValue;
+                               unsigned* amax_y, float w_margin, float g_headroom, int* sat,
+                               float* gscales, unsigned* gamax, hipStream_t s) {
+  if (n <= 0 || n > 1024 || nparts_w <= 0 || !(g_headroom >= 1.f)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(n), dim3(64), 0, s, n, scales, amax_w,
-                     nparts_w, amax_y, w_margin, sat, gscales, gamax);
+                     nparts_w, amax_y, w_margin, g_headroom, sat, gscales, gamax);
   return hipGetLastError();
 }
 

@@ -44,6 +44,9 @@ FP8_PITCH = 448   # rows per board of the fp8 copy-out frames (441 + 7 zero rows
 # the weights between two refreshes; 1.05 saturated up to 3% of layer-steps in the
 # memorisation stress run (tests/test_train_gpu.py), 1.25 covers a 25% step-to-step growth
 FP8_W_MARGIN = 1.25
+# headroom of the delayed power-of-two e5m2 gradient scales over the last observed amax
+# (conv_fp8.hip fp8_update_scales; tests/test_train_gpu.py test_fp8_stress_vs_bf16_memorisation)
+FP8_G_HEADROOM = 8.0
 REFRESH_PARTS = 512   # weight_refresh workgroups per layer (elementwise.hip)
 
 
@@ -1406,7 +1409,7 @@ class HipGoNet:
         if self.fp8:
             self.h.fp8_update_scales(len(self.plans), self.fp8_scales.data_ptr(),
                                      self.fp8_amax_w.data_ptr(), REFRESH_PARTS,
-                                     self.fp8_amax.data_ptr(), FP8_W_MARGIN,
+                                     self.fp8_amax.data_ptr(), FP8_W_MARGIN, FP8_G_HEADROOM,
                                      self.fp8_sat.data_ptr(), self.fp8_gscales.data_ptr(),
                                      self.fp8_gamax.data_ptr(), s)
 

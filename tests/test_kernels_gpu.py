@@ -392,7 +392,8 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     sat = torch.zeros(3 * n, dtype=torch.int32, device=DEV)
     s0, g0 = scales.clone(), gscales.clone()
     h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), 1, amax_y.data_ptr(), 1.05,
-                        sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(), stream_handle())
+                        8.0, sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(),
+                        stream_handle())
     torch.cuda.synchronize()
     assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
     assert scales[2].item() == s0[2].item()          # layer 1 s_w: amax_w inf -> unchanged
@@ -401,7 +402,7 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     assert scales[1].item() == s0[1].item()          # layer 0 s_y: amax_y NaN -> unchanged
     assert gscales[0].item() == g0[0].item() and gscales[2].item() == g0[2].item()
     assert abs(scales[0].item() - 100.0 * 1.05 / 448.0) < 1e-6      # finite ones update
-    HG = 8.0                                         # FP8_GRAD_HEADROOM
+    HG = 8.0                                         # g_headroom passed above
     assert gscales[1].item() == 2.0 ** np.ceil(np.log2(HG * 1000.0 / 57344.0))
     s = sat.tolist()
     assert s[2 * 1] == 1 and s[2 * 0 + 1] == 1        # weights l1, activations l0

@@ -5,9 +5,10 @@ switched back to bf16 in turn — forward stack (always fp8 with dtype=fp8), e5m
 stack (DG_FP8_DGRAD), MX-fp8 weight gradients (DG_FP8_WGRAD) — and the e5m2 gradients rounded
 to nearest even instead of stochastically (DG_FP8_SR=0).  Round 4 result (12x128, 800
 steps, rate 0.1): nearest-even e5m2 gradients stall near 5.3 nats while bf16 reaches 2.7;
-bf16 backward-data recovers it (so the forward is fine): the fix is stochastic rounding.  Prints the 100-step window
-mean losses per variant as one JSON line (and writes gpurun_out/fp8_memo_12x<ch>.json).
-Usage: python tools/fp8_memo.py [CH] [STEPS] [RATE]"""
+bf16 backward-data recovers it (so the forward is fine): the fix is stochastic rounding.
+"ghead" variants: other e5m2 gradient-scale headrooms (hip_model.FP8_G_HEADROOM).  Prints the
+100-step window mean losses per variant (and writes gpurun_out/fp8_memo_12x<ch>.json).
+Usage: [FP8_MEMO_VARIANTS=name,...] python tools/fp8_memo.py [CH] [STEPS] [RATE]"""
 import json
 import os
 import sys
@@ -20,6 +21,9 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    from deep_go_amd.models import hip_model
+    global G_HEAD0
+    G_HEAD0 = hip_model.FP8_G_HEADROOM
     from deep_go_amd.config import ExperimentConfig
     from deep_go_amd.data.dataset import PackedDataset
     from deep_go_amd.data.loader import BatchLoader
@@ -38,14 +42,19 @@ def main():
                 ("fp8 rne", "fp8", {"DG_FP8_SR": "0"}),
                 ("fp8 bf16-wgrad", "fp8", {"DG_FP8_WGRAD": "0"}),
                 ("fp8 bf16-dgrad", "fp8", {"DG_FP8_DGRAD": "0", "DG_FP8_WGRAD": "0"}),
+                ("fp8 ghead2", "fp8", {"ghead": 2.0}),
+                ("fp8 ghead8", "fp8", {"ghead": 8.0}),
                 ]
     only = os.environ.get("FP8_MEMO_VARIANTS")
     if only:
         variants = [v for v in variants if v[0] in only.split(",")]
     out, flat0 = {}, None
     for name, dt, env in variants:
+        from deep_go_amd.models import hip_model
         for k in ("DG_FP8_WGRAD", "DG_FP8_DGRAD", "DG_FP8_SR"):
             os.environ.pop(k, None)
+        env = dict(env)
+        hip_model.FP8_G_HEADROOM = env.pop("ghead", G_HEAD0)
         os.environ.update(env)
         cfg = ExperimentConfig(numLayers=12, channelSize=ch, batchSize=B, rate=rate,
                                rateDecay=1e-5, head_relu=False, useCuda=True, seed=13,
@@ -61,6 +70,7 @@ def main():
         ls = np.array(ls)
         rec = {"windows": [round(float(ls[w:w + 100].mean()), 4) for w in range(0, N, 100)]}
         if dt == "fp8":
+            rec["ghead"] = hip_model.FP8_G_HEADROOM
             rec["sat"] = be.net.fp8_sat.cpu().tolist()
             rec["scales"] = be.net.fp8_scales.cpu().tolist()
             rec["gscales"] = be.net.fp8_gscales.cpu().tolist()
