@@ -20,10 +20,31 @@
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 
+#include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
+
+// oneshot.hip
+namespace dgipc {
+constexpr int MAXW = 8;
+struct OneShotArgs {
+  const void* src;
+  void* dst;
+  long long nvec;
+  int dtype;
+  int rank, world;
+  char* bufs[MAXW];
+  unsigned* flags[MAXW];
+  long long half_bytes;
+  unsigned* state;
+  long long timeout_ticks;
+};
+}  // namespace dgipc
+extern "C" hipError_t dg_oneshot_allreduce(const dgipc::OneShotArgs* a, int blocks,
+                                           hipStream_t stream);
 
 namespace {
 
@@ -154,6 +175,120 @@ class Comm {
   int world_, rank_;
 };
 
+void hcheck(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("dgcomm ") + what + ": " + hipGetErrorString(e));
+}
+
+// The one-shot IPC all-reduce of small buckets (oneshot.hip): this rank's uncached staging
+// buffer (2 halves of `capacity` bytes) and flag array, exported as IPC handles; open_peers
+// maps every other rank's pair (handles exchanged by the caller, e.g. through the c10d store).
+class IpcOneShot {
+ public:
+  IpcOneShot(int world, int rank, int device, long long capacity, double timeout_s)
+      : world_(world), rank_(rank), cap_((capacity + 15) / 16 * 16) {
+    if (world < 1 || world > dgipc::MAXW || rank < 0 || rank >= world || capacity <= 0)
+      throw std::invalid_argument("dgcomm ipc: world 1..8, 0 <= rank < world, capacity > 0");
+    hcheck(hipSetDevice(device), "hipSetDevice");
+    hcheck(hipExtMallocWithFlags((void**)&buf_, 2 * cap_, hipDeviceMallocUncached),
+           "staging alloc");
+    hcheck(hipExtMallocWithFlags((void**)&flags_, dgipc::MAXW * sizeof(unsigned),
+                                 hipDeviceMallocUncached),
+           "flag alloc");
+    hcheck(hipMemset(flags_, 0, dgipc::MAXW * sizeof(unsigned)), "flag init");
+    hcheck(hipMalloc((void**)&state_, 4 * sizeof(unsigned)), "state alloc");
+    hcheck(hipMemset(state_, 0, 4 * sizeof(unsigned)), "state init");
+    hcheck(hipDeviceSynchronize(), "init sync");
+    a_ = dgipc::OneShotArgs{};
+    a_.rank = rank;
+    a_.world = world;
+    a_.half_bytes = cap_;
+    a_.state = state_;
+    a_.timeout_ticks = (long long)(timeout_s * 1e8);
+    a_.bufs[rank] = buf_;
+    a_.flags[rank] = flags_;
+  }
+  ~IpcOneShot() { close(); }
+
+  py::bytes handle_buf() const { return handle(buf_); }
+  py::bytes handle_flags() const { return handle(flags_); }
+
+  // handles[j] = (staging handle, flag handle) of rank j (this rank's own entry is ignored)
+  void open_peers(const std::vector<std::pair<py::bytes, py::bytes>>& handles) {
+    if ((int)handles.size() != world_) throw std::invalid_argument("dgcomm ipc: one pair per rank");
+    for (int j = 0; j < world_; ++j) {
+      if (j == rank_) continue;
+      a_.bufs[j] = (char*)open(handles[j].first);
+      a_.flags[j] = (unsigned*)open(handles[j].second);
+      opened_.push_back(a_.bufs[j]);
+      opened_.push_back(a_.flags[j]);
+    }
+  }
+  // count elements of dtype ("fp32" | "bf16"), a multiple of 16 bytes (the kernel moves
+  // 16-byte vectors; the flat gradient's layer ranges are aligned)
+  void all_reduce(uintptr_t src, uintptr_t dst, size_t count, const std::string& dt,
+                  int blocks, uintptr_t stream) {
+    const int es = dt == "fp32" ? 4 : dt == "bf16" ? 2 : 0;
+    if (!es) throw std::invalid_argument("dgcomm ipc: fp32 | bf16");
+    const long long nbytes = (long long)count * es;
+    if (nbytes > cap_) throw std::invalid_argument("dgcomm ipc: bucket larger than capacity");
+    if (nbytes % 16 != 0) throw std::invalid_argument("dgcomm ipc: bucket not a multiple of 16 B");
+    for (int j = 0; j < world_; ++j)
+      if (!a_.bufs[j]) throw std::runtime_error("dgcomm ipc: peers not opened");
+    dgipc::OneShotArgs a = a_;
+    a.src = (const void*)src;
+    a.dst = (void*)dst;
+    a.nvec = nbytes / 16;
+    a.dtype = es == 4 ? 0 : 1;
+    hcheck(dg_oneshot_allreduce(&a, blocks, (hipStream_t)stream), "oneshot all-reduce");
+  }
+  // non-zero once a call timed out waiting for a peer (its result is garbage)
+  unsigned error() const {
+    unsigned v[4];
+    hcheck(hipMemcpy(v, state_, sizeof(v), hipMemcpyDeviceToHost), "state read");
+    return v[3];
+  }
+  unsigned calls() const {
+    unsigned v[4];
+    hcheck(hipMemcpy(v, state_, sizeof(v), hipMemcpyDeviceToHost), "state read");
+    return v[0];
+  }
+  long long capacity() const { return cap_; }
+  void close() {
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    opened_.clear();
+    if (buf_) (void)hipFree(buf_);
+    if (flags_) (void)hipFree(flags_);
+    if (state_) (void)hipFree(state_);
+    buf_ = nullptr;
+    flags_ = nullptr;
+    state_ = nullptr;
+  }
+
+ private:
+  static py::bytes handle(void* p) {
+    hipIpcMemHandle_t h;
+    hcheck(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+    return py::bytes((const char*)&h, sizeof(h));
+  }
+  static void* open(const py::bytes& b) {
+    const std::string s = b;
+    hipIpcMemHandle_t h;
+    if (s.size() != sizeof(h)) throw std::invalid_argument("dgcomm ipc: bad handle");
+    std::memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    hcheck(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return p;
+  }
+  int world_, rank_;
+  long long cap_;
+  char* buf_ = nullptr;
+  unsigned* flags_ = nullptr;
+  unsigned* state_ = nullptr;
+  dgipc::OneShotArgs a_;
+  std::vector<void*> opened_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_dgcomm, m) {
@@ -168,6 +303,18 @@ PYBIND11_MODULE(_dgcomm, m) {
     ncclGetVersion(&v);
     return v;
   });
+  py::class_<IpcOneShot>(m, "IpcOneShot")
+      .def(py::init<int, int, int, long long, double>(), py::arg("world"), py::arg("rank"),
+           py::arg("device"), py::arg("capacity"), py::arg("timeout_s") = 10.0)
+      .def("handle_buf", &IpcOneShot::handle_buf)
+      .def("handle_flags", &IpcOneShot::handle_flags)
+      .def("open_peers", &IpcOneShot::open_peers)
+      .def("all_reduce", &IpcOneShot::all_reduce, py::arg("src"), py::arg("dst"),
+           py::arg("count"), py::arg("dtype"), py::arg("blocks"), py::arg("stream"))
+      .def("error", &IpcOneShot::error)
+      .def("calls", &IpcOneShot::calls)
+      .def("capacity", &IpcOneShot::capacity)
+      .def("close", &IpcOneShot::close);
   py::class_<Comm>(m, "Comm")
       .def(py::init<py::bytes, int, int, int>(), py::arg("uid"), py::arg("world"),
            py::arg("rank"), py::arg("device"))

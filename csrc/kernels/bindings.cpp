@@ -95,7 +95,7 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
                              hipStream_t stream);
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w, unsigned* amax_y, float w_margin,
                                float g_headroom, int* sat, float* gscales, unsigned* gamax,
-                               hipStream_t s);
+                               float* ghist, hipStream_t s);
 hipError_t dg_weight_fp8(const float* w, void* wf8, int cout, int cin, int taps, int cinp, int kp,
                          const float* s_w, hipStream_t s);
 hipError_t dg_frame_to_fp8(const void* src, void* dst, size_t n, const float* scale,
@@ -325,10 +325,11 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("fp8_update_scales", [](int n, uintptr_t scales, uintptr_t amax_w, int nparts_w,
                                 uintptr_t amax_y, float w_margin, float g_headroom,
                                 uintptr_t sat, uintptr_t gscales, uintptr_t gamax,
-                                uintptr_t stream) {
+                                uintptr_t ghist, uintptr_t stream) {
     check(dg_fp8_update_scales(n, P<float>(scales), P<unsigned>(amax_w), nparts_w,
                                P<unsigned>(amax_y), w_margin, g_headroom, P<int>(sat),
-                               P<float>(gscales), P<unsigned>(gamax), S(stream)),
+                               P<float>(gscales), P<unsigned>(gamax), P<float>(ghist),
+                               S(stream)),
           "fp8_update_scales");
   });
   m.def("weight_fp8", [](uintptr_t w, uintptr_t wf8, int cout, int cin, int taps, int cinp,

@@ -242,16 +242,21 @@ conv_board_fp8_kernel(Fp8Args a) {
 // max.  1.25 left 0.8% of layer-steps saturated in the slow 1000-step stress run but 2-9%
 // per layer in a memorisation run (rate 0.1, loss falling > 1 nat: amax grows faster than
 // 25% per step); 2.0 (one more power of two, one less e4m3 binade at the bottom) keeps
-// that regime under 1%.  Weights use their own margin (w_margin, host), the e5m2 gradients
-// their own headroom (g_headroom, host: hip_model.FP8_G_HEADROOM — with stochastic rounding,
-// conv_stack_f8.hip, the memorisation run trains through to ~0 loss, where gradient amax
-// jumps more than 2x between steps: 2% of gradient layer-steps saturated at 12x256 with 2).
+// that regime under 1%.  Weights use their own margin (w_margin, host).  The e5m2 gradient
+// scales come from the MAX over the last FP8_GHIST observed gradient amaxes (ghist, a per-
+// layer history) times their own headroom (g_headroom, host: hip_model.FP8_G_HEADROOM): with
+// stochastic rounding (conv_stack_f8.hip) the memorisation run trains through to ~0 loss,
+// where the gradient amax of successive batches differs by 10x and more — one-step delayed
+// scaling then saturated 2-3% of gradient layer-steps at 12x256 even with 8x headroom; a
+// history spanning the batch-to-batch spread is the usual delayed-scaling recipe.
 constexpr float FP8_HEADROOM = 2.0f;
+constexpr int FP8_GHIST = 16;
 __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* scales,
                                                                unsigned* amax_w, int nparts_w,
                                                                unsigned* amax_y, float w_margin,
                                                                float g_headroom, int* sat,
-                                                               float* gscales, unsigned* gamax) {
+                                                               float* gscales, unsigned* gamax,
+                                                               float* ghist) {
   const int l = blockIdx.x, lane = threadIdx.x;
   unsigned mwb = 0u;   // unsigned max of non-negative float bits: inf / NaN bits win
   for (int j = lane; j < nparts_w; j += 64) {
@@ -264,6 +269,21 @@ __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* sca
     const unsigned v = (unsigned)__shfl_xor((int)mwb, o, 64);
     mwb = v > mwb ? v : mwb;
   }
+  // gradient amax history (lanes 0..FP8_GHIST-1 hold one entry each): shift in this step's
+  // finite amax, take the max (the whole wave, before lane 0 goes on alone)
+  float ghmax = 0.f;
+  if (gscales && ghist && l < n) {
+    const float mg = __uint_as_float(gamax[l]);
+    float* hl = ghist + (size_t)l * FP8_GHIST;
+    const float old = lane < FP8_GHIST ? hl[lane] : 0.f;
+    const float prev = __shfl_up(old, 1, 64);
+    float v = old;
+    if (__builtin_isfinite(mg) && lane < FP8_GHIST) v = lane == 0 ? mg : prev;
+    if (lane < FP8_GHIST) hl[lane] = v;
+    ghmax = v;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ghmax = fmaxf(ghmax, __shfl_xor(ghmax, o, 64));
+  }
   if (l >= n || lane != 0) return;
   // a non-finite amax (an inf / NaN reached a quantized tensor: amax is an atomicMax over
   // float bits, so NaN bits win too) never becomes a scale — exp2f(inf) = inf would zero
@@ -273,7 +293,8 @@ __global__ void __launch_bounds__(64) fp8_update_scales_kernel(int n, float* sca
     const float mg = __uint_as_float(gamax[l]);
     const bool ok = __builtin_isfinite(mg);
     if (sat && (!ok || mg > 57344.f * gscales[l])) sat[2 * n + l] += 1;
-    if (ok && mg > 0.f) gscales[l] = exp2f(ceilf(log2f(g_headroom * mg / 57344.f)));
+    const float mh = ghist ? ghmax : mg;   // (the history holds this step's finite amax)
+    if (ok && mh > 0.f) gscales[l] = exp2f(ceilf(log2f(g_headroom * mh / 57344.f)));
     gamax[l] = 0u;
   }
   const float mw = __uint_as_float(mwb);
@@ -389,10 +410,10 @@ hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int 
 
 hipError_t dg_fp8_update_scales(int n, float* scales, unsigned* amax_w, int nparts_w,
                                unsigned* amax_y, float w_margin, float g_headroom, int* sat,
-                               float* gscales, unsigned* gamax, hipStream_t s) {
+                               float* gscales, unsigned* gamax, float* ghist, hipStream_t s) {
   if (n <= 0 || n > 1024 || nparts_w <= 0 || !(g_headroom >= 1.f)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fp8_update_scales_kernel, dim3(n), dim3(64), 0, s, n, scales, amax_w,
-                     nparts_w, amax_y, w_margin, g_headroom, sat, gscales, gamax);
+                     nparts_w, amax_y, w_margin, g_headroom, sat, gscales, gamax, ghist);
   return hipGetLastError();
 }
 

@@ -113,10 +113,18 @@ def build_comm(force: bool = False) -> Path:
     OUT.mkdir(exist_ok=True)
     target = OUT / f"_dgcomm{EXT}"
     src = CDIR / "comm.cpp"
-    if force or _newer(src, target):
-        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", *(_pybind_includes()),
-              "-I/opt/rocm/include", str(src), "-o", str(target), "-L/opt/rocm/lib", "-lrccl",
-              "-lamdhip64"])
+    kern = CDIR / "oneshot.hip"       # the one-shot IPC all-reduce kernel (small buckets)
+    obj = BUILD / "comm_oneshot.hip.o"
+    if force or _newer(kern, obj):
+        _run([HIPCC, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-c", str(kern),
+              "-o", str(obj)])
+    hobj = BUILD / "comm_host.cpp.o"
+    if force or _newer(src, hobj):
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-c",
+              *(_pybind_includes()), "-I/opt/rocm/include", str(src), "-o", str(hobj)])
+    if force or _newer(hobj, target) or _newer(obj, target):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", str(hobj), str(obj), "-o",
+              str(target), "-L/opt/rocm/lib", "-lrccl", "-lamdhip64"])
     return target
 
 

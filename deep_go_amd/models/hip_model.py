@@ -44,9 +44,11 @@ FP8_PITCH = 448   # rows per board of the fp8 copy-out frames (441 + 7 zero rows
 # the weights between two refreshes; 1.05 saturated up to 3% of layer-steps in the
 # memorisation stress run (tests/test_train_gpu.py), 1.25 covers a 25% step-to-step growth
 FP8_W_MARGIN = 1.25
-# headroom of the delayed power-of-two e5m2 gradient scales over the last observed amax
+# headroom of the delayed power-of-two e5m2 gradient scales over the max of the last
+# FP8_GHIST observed amaxes
 # (conv_fp8.hip fp8_update_scales; tests/test_train_gpu.py test_fp8_stress_vs_bf16_memorisation)
-FP8_G_HEADROOM = 8.0
+FP8_G_HEADROOM = 4.0
+FP8_GHIST = 16        # gradient amax history length (conv_fp8.hip FP8_GHIST)
 REFRESH_PARTS = 512   # weight_refresh workgroups per layer (elementwise.hip)
 
 
@@ -271,6 +273,10 @@ class HipGoNet:
         # their observed |dz| max (delayed scaling, powers of two)
         self.fp8_gscales = torch.ones(len(self.plans), dtype=torch.float32, device=dev)
         self.fp8_gamax = torch.zeros(len(self.plans), dtype=torch.int32, device=dev)
+        # the last FP8_GHIST gradient amaxes per layer (conv_fp8.hip: the gradient scale
+        # comes from their max)
+        self.fp8_ghist = torch.zeros((len(self.plans), FP8_GHIST), dtype=torch.float32,
+                                     device=dev)
         self._fp8_calibrated = not self.fp8
         # backward side stream ("bias", the default): the HBM-bound bias-grad partials run on
         # it beside the MFMA-bound weight-gradient launch of the same layers, and the first
@@ -749,6 +755,7 @@ class HipGoNet:
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
         self._dz8_exact = set()    # layers whose e5m2 gradient copy equals their bf16 dZ
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
+        self._l0_bias_main = os.environ.get("DG_L0_BIAS_MAIN", "1") != "0"
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
         if os.environ.get("DG_DSTACK", "1") == "0":
@@ -1195,8 +1202,15 @@ class HipGoNet:
         elif self.side_mode == "bias":
             side = self.side
             l0_side = self._l0_side_at == i
+            # the first layer's bias partial (HBM-bound, 24-48 MB) on the main stream right
+            # after the grouped launch instead of squeezed beside it on the side stream
+            # (12x128: 48 us beside the window kernel, a few us alone), its slab reduce then
+            # on the main stream too, after the side stream's 5x5 weight gradient
+            l0_bias_main = self._l0_bias_main
             if i == 0 and self._l0_side_at is not None:
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
+                if l0_bias_main:
+                    self._run(ops[2:3], main.cuda_stream)
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
                 self._flush_head_reduce(side.cuda_stream)
@@ -1207,9 +1221,13 @@ class HipGoNet:
                 # (profiles/r3_l0_chain_stream_ab.txt): the chain before the partials, or on a
                 # third stream beside the grouped launch, is 5-6% slower at 12x128 and
                 # 0.3-1.6% at 12x256 — compute beside the window kernel slows it
+                l0ops = self._layer_ops(0)
                 if l0_side:
-                    self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
+                    self._run(self._l0_dgrad + (l0ops[1:2] if l0_bias_main else l0ops[:3]),
+                              side.cuda_stream)
                 self._run(ops[1:2], main.cuda_stream)
+                if l0_side and l0_bias_main:
+                    self._run(l0ops[:1], main.cuda_stream)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
@@ -1411,7 +1429,7 @@ class HipGoNet:
                                      self.fp8_amax_w.data_ptr(), REFRESH_PARTS,
                                      self.fp8_amax.data_ptr(), FP8_W_MARGIN, FP8_G_HEADROOM,
                                      self.fp8_sat.data_ptr(), self.fp8_gscales.data_ptr(),
-                                     self.fp8_gamax.data_ptr(), s)
+                                     self.fp8_gamax.data_ptr(), self.fp8_ghist.data_ptr(), s)
 
     def calibrate_fp8(self):
         """Forward(+backward) passes on the current inputs to observe activation (and, with

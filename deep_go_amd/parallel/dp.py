@@ -137,6 +137,75 @@ class TorchComm:
         pass
 
 
+class IpcOneShot:
+    """One-shot IPC all-reduce of SMALL buckets on one node (csrc/comm/oneshot.hip; SURVEY
+    §5.8's optional small-bucket path): each rank stages its bucket in an uncached,
+    IPC-exported buffer, signals every peer, and one kernel sums all `world` buffers over
+    xGMI in rank order — one kernel instead of a ring's 2(n-1) latency-bound steps.
+    Stream-ordered and graph-capturable like the RCCL calls.  Handles travel through a c10d
+    store (the default process group's, or ``store``).  A peer that never arrives does not
+    hang the kernel: it gives up after ``timeout_s`` and ``error()`` turns non-zero.
+
+    Validated with two processes sharing one GPU (tests/test_ipc_gpu.py); the cross-GPU
+    path over xGMI has not been measured by the builder (no multi-GPU box), so NativeComm
+    routes small buckets here only when asked (``ipc_small_bytes`` / DG_IPC_SMALL)."""
+    kind = "ipc"
+    in_graph = True
+    _seq = 0
+
+    def __init__(self, device, capacity_bytes: int, world: Optional[int] = None,
+                 rank: Optional[int] = None, store=None, mod=None, timeout_s: float = 10.0,
+                 blocks: int = 16):
+        if mod is None:
+            from ..ops.native import comm as _comm_mod
+            mod = _comm_mod()
+        self.device = torch.device(device)
+        if world is None:
+            world = dist.get_world_size() if dist.is_initialized() else 1
+            rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world, self.rank, self.blocks = world, rank, blocks
+        self.c = mod.IpcOneShot(world, rank, self.device.index or 0, int(capacity_bytes),
+                                float(timeout_s))
+        self.capacity = int(self.c.capacity())
+        key = f"dg_ipc_{IpcOneShot._seq}"
+        IpcOneShot._seq += 1
+        if world > 1:
+            if store is None:
+                store = dist.distributed_c10d._get_default_store()
+            hb, hf = bytes(self.c.handle_buf()), bytes(self.c.handle_flags())
+            store.set(f"{key}_{rank}", (hb + hf).hex())
+            pairs = []
+            for j in range(world):
+                v = bytes.fromhex(store.get(f"{key}_{j}").decode())
+                pairs.append((v[:len(hb)], v[len(hb):]))
+        else:
+            pairs = [(b"", b"")]
+        self.c.open_peers(pairs)
+        self.stream = torch.cuda.Stream(device=self.device)
+
+    def fits(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return (t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+                and nb <= self.capacity and nb % 16 == 0)
+
+    def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
+        if op != "sum" or not self.fits(t):
+            raise ValueError("ipc one-shot: contiguous fp32/bf16 sum, a multiple of 16 B "
+                             "within capacity")
+        s = stream if stream is not None else self.stream
+        self.c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(),
+                          "fp32" if t.dtype == torch.float32 else "bf16", self.blocks,
+                          int(s.cuda_stream))
+        return t
+
+    def error(self) -> int:
+        return int(self.c.error())
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        self.c.close()
+
+
 class NativeComm:
     """The native RCCL communicator (csrc/comm/comm.cpp, ``_dgcomm``) on its own HIP stream.
 
@@ -149,7 +218,7 @@ class NativeComm:
     in_graph = True
     _seq = 0
 
-    def __init__(self, device, mod=None, stream=None):
+    def __init__(self, device, mod=None, stream=None, ipc_small_bytes: Optional[int] = None):
         if mod is None:
             from ..ops.native import comm as _comm_mod
             mod = _comm_mod()
@@ -174,6 +243,13 @@ class NativeComm:
         self.uid = uid
         self.c = mod.Comm(uid, self.world, self.rank, device.index or 0)
         self.stream = stream if stream is not None else torch.cuda.Stream(device=device)
+        # buckets up to ipc_small_bytes take the one-shot IPC all-reduce (one node only;
+        # off unless asked: DG_IPC_SMALL=<bytes>)
+        if ipc_small_bytes is None:
+            ipc_small_bytes = int(os.environ.get("DG_IPC_SMALL", "0"))
+        one_node = int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world
+        self.ipc = (IpcOneShot(device, ipc_small_bytes, self.world, self.rank, mod=mod)
+                    if ipc_small_bytes > 0 and self.world > 1 and one_node else None)
 
     def version(self) -> int:
         return int(self.mod.version())
@@ -186,6 +262,8 @@ class NativeComm:
     def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
         """In-place all-reduce of a contiguous tensor on ``stream`` (default: comm stream)."""
         s = stream if stream is not None else self.stream
+        if self.ipc is not None and op == "sum" and self.ipc.fits(t):
+            return self.ipc.all_reduce_(t, stream=s)
         self.c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), op,
                           int(s.cuda_stream))
         return t
@@ -210,6 +288,8 @@ class NativeComm:
             return {"error": str(e)}
 
     def async_error(self) -> str:
+        if self.ipc is not None and self.ipc.error():
+            return "ipc one-shot all-reduce: a peer never arrived (timed out)"
         return self.c.async_error()
 
     def abort(self):
@@ -217,6 +297,8 @@ class NativeComm:
 
     def close(self):
         torch.cuda.synchronize(self.device)
+        if self.ipc is not None:
+            self.ipc.close()
         self.c.destroy()
 
 

@@ -1,0 +1,114 @@
+"""The one-shot IPC all-reduce of small buckets (csrc/comm/oneshot.hip, dp.IpcOneShot) with
+two processes sharing ONE GPU: IPC handles through a TCPStore, both ranks' staging buffers
+mapped into each other, rank-order fp32 sums compared bit-exactly with the same sums on the
+host (fp32 and bf16 buckets, several sizes, eager and captured in a hipGraph), and a peer
+that never arrives: the kernel gives up after its time limit and flags the error instead of
+hanging.  (The cross-GPU xGMI path is the same code; the builder has no multi-GPU box.)"""
+import multiprocessing as mp
+import socket
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(1024, "fp32"), (4096, "bf16"), (65536, "fp32"), (8, "bf16"), (262144, "fp32")]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(k, r, n, dt):
+    import torch
+    g = torch.Generator().manual_seed(1000 * k + r)
+    x = torch.randn(n, generator=g)
+    return x.to(torch.bfloat16) if dt == "bf16" else x
+
+
+def _worker(rank, world, port, mode, q):
+    import datetime
+    try:
+        import torch
+        from torch.distributed import TCPStore
+        from deep_go_amd.parallel.dp import IpcOneShot
+        store = TCPStore("127.0.0.1", port, world, rank == 0,
+                         timeout=datetime.timedelta(seconds=60))
+        c = IpcOneShot("cuda:0", 1 << 20, world, rank, store=store,
+                       timeout_s=1.0 if mode == "absent" else 20.0)
+        out = {"rank": rank}
+        if mode == "absent":
+            if rank == 0:
+                x = torch.ones(1024, device="cuda:0")
+                c.all_reduce_(x, stream=torch.cuda.current_stream())
+                torch.cuda.synchronize()
+                out["error"] = c.error()
+                store.set("done", "1")
+            else:
+                store.wait(["done"])
+            q.put(out)
+            return
+        ok = []
+        for k, (n, dt) in enumerate(SIZES):
+            x = _data(k, rank, n, dt).cuda()
+            c.all_reduce_(x, stream=torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            want = torch.zeros(n)
+            for r in range(world):
+                want = want + _data(k, r, n, dt).float()
+            want = want.to(x.dtype)
+            ok.append(bool(torch.equal(x.cpu(), want)))
+        # captured: two buckets per replay, three replays
+        a = torch.empty(2048, device="cuda:0")
+        b = torch.empty(4096, dtype=torch.bfloat16, device="cuda:0")
+        g = torch.cuda.CUDAGraph()
+        cur = torch.cuda.current_stream()
+        with torch.cuda.graph(g):
+            s = torch.cuda.current_stream()
+            a.fill_(float(rank + 1))
+            b.fill_(float(2 * rank + 1))
+            c.stream.wait_stream(s)
+            c.all_reduce_(a)
+            c.all_reduce_(b)
+            s.wait_stream(c.stream)
+        for _ in range(3):
+            g.replay()
+        cur.synchronize()
+        ok.append(bool((a == float(world * (world + 1) // 2)).all()))
+        ok.append(bool((b.float() == float(world * world)).all()))
+        out["ok"] = ok
+        out["error"] = c.error()
+        out["calls"] = int(c.c.calls())
+        c.close()
+        q.put(out)
+    except Exception as e:  # noqa: BLE001
+        q.put({"rank": rank, "exc": repr(e)})
+
+
+def _run(mode, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    return sorted(res, key=lambda d: d["rank"])
+
+
+def test_ipc_oneshot_two_processes_exact_sums():
+    res = _run("sum")
+    for r in res:
+        assert "exc" not in r, r
+        assert all(r["ok"]), r
+        assert r["error"] == 0
+        assert r["calls"] == len(SIZES) + 2 * 3
+
+
+def test_ipc_oneshot_missing_peer_times_out_instead_of_hanging():
+    res = _run("absent")
+    assert "exc" not in res[0] and "exc" not in res[1], res
+    assert res[0]["error"] == 1

@@ -392,7 +392,7 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     sat = torch.zeros(3 * n, dtype=torch.int32, device=DEV)
     s0, g0 = scales.clone(), gscales.clone()
     h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), 1, amax_y.data_ptr(), 1.05,
-                        8.0, sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(),
+                        8.0, sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(), 0,
                         stream_handle())
     torch.cuda.synchronize()
     assert torch.isfinite(scales).all() and torch.isfinite(gscales).all()
@@ -408,3 +408,38 @@ def test_fp8_scale_update_ignores_non_finite_amax():
     assert s[2 * 1] == 1 and s[2 * 0 + 1] == 1        # weights l1, activations l0
     assert s[2 * n + 0] == 1 and s[2 * n + 2] == 1    # gradients l0 (inf), l2 (NaN)
     assert (amax_w == 0).all() and (amax_y == 0).all() and (gamax == 0).all()
+
+
+def test_fp8_gradient_scale_uses_amax_history():
+    """The e5m2 gradient scale comes from the max of the last 16 observed gradient amaxes
+    (conv_fp8.hip FP8_GHIST): a step with a small amax after a large one keeps the large
+    one's range; non-finite amaxes never enter the history; after 16 small steps the scale
+    follows the small amax."""
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    n = 2
+    f = lambda vals: torch.tensor(vals, dtype=torch.float32, device=DEV)  # noqa: E731
+    scales = f([1.0] * (2 * n))
+    gscales = f([1.0] * n)
+    ghist = torch.zeros((n, 16), dtype=torch.float32, device=DEV)
+    sat = torch.zeros(3 * n, dtype=torch.int32, device=DEV)
+    amax_w = torch.zeros(n, dtype=torch.int32, device=DEV)
+    amax_y = torch.zeros(n, dtype=torch.int32, device=DEV)
+    HG = 4.0
+    want = lambda a: 2.0 ** np.ceil(np.log2(HG * a / 57344.0))   # noqa: E731
+
+    def step(g0, g1):
+        gamax = f([g0, g1]).view(torch.int32).clone()
+        h.fp8_update_scales(n, scales.data_ptr(), amax_w.data_ptr(), 1, amax_y.data_ptr(), 1.25,
+                            HG, sat.data_ptr(), gscales.data_ptr(), gamax.data_ptr(),
+                            ghist.data_ptr(), stream_handle())
+        torch.cuda.synchronize()
+        return gscales.tolist()
+
+    assert step(1000.0, 5.0) == [want(1000.0), want(5.0)]
+    assert step(10.0, float("nan")) == [want(1000.0), want(5.0)]   # history max; NaN skipped
+    for _ in range(14):
+        g = step(10.0, 7.0)
+    assert g == [want(1000.0), want(7.0)]          # 1000 is 15 entries old: still inside
+    assert step(10.0, 7.0) == [want(10.0), want(7.0)]   # 16 newer entries: 1000 left
+    assert ghist[0].tolist() == [10.0] * 16
