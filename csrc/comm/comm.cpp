@@ -18,6 +18,7 @@
 // makeDataParallel (/root/reference/experiments.lua:155-168).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
 #include <cstring>

@@ -755,7 +755,6 @@ class HipGoNet:
         self._dgrad_first = False  # every dZ (down to dZ_0) produced in _bwd_pre
         self._dz8_exact = set()    # layers whose e5m2 gradient copy equals their bf16 dZ
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
-        self._l0_bias_main = os.environ.get("DG_L0_BIAS_MAIN", "1") != "0"
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
         if os.environ.get("DG_DSTACK", "1") == "0":
@@ -1202,15 +1201,8 @@ class HipGoNet:
         elif self.side_mode == "bias":
             side = self.side
             l0_side = self._l0_side_at == i
-            # the first layer's bias partial (HBM-bound, 24-48 MB) on the main stream right
-            # after the grouped launch instead of squeezed beside it on the side stream
-            # (12x128: 48 us beside the window kernel, a few us alone), its slab reduce then
-            # on the main stream too, after the side stream's 5x5 weight gradient
-            l0_bias_main = self._l0_bias_main
             if i == 0 and self._l0_side_at is not None:
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
-                if l0_bias_main:
-                    self._run(ops[2:3], main.cuda_stream)
             else:
                 side.wait_stream(main)           # dZ of the layer (group) final
                 self._flush_head_reduce(side.cuda_stream)
@@ -1220,14 +1212,14 @@ class HipGoNet:
                 # then dZ_0 and the first layer's whole chain, joined at layer 0.  Measured
                 # (profiles/r3_l0_chain_stream_ab.txt): the chain before the partials, or on a
                 # third stream beside the grouped launch, is 5-6% slower at 12x128 and
-                # 0.3-1.6% at 12x256 — compute beside the window kernel slows it
-                l0ops = self._layer_ops(0)
+                # 0.3-1.6% at 12x256 — compute beside the window kernel slows it; and its
+                # bias partial on the main stream after the window kernel (its 5x5 weight
+                # gradient then starts ~50 us earlier beside it) stretched the fp8 window
+                # kernel by 100 us: -6% at 12x256 fp8, 0 elsewhere
+                # (profiles/r4_s1_l0_bias_main_ab.txt)
                 if l0_side:
-                    self._run(self._l0_dgrad + (l0ops[1:2] if l0_bias_main else l0ops[:3]),
-                              side.cuda_stream)
+                    self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
                 self._run(ops[1:2], main.cuda_stream)
-                if l0_side and l0_bias_main:
-                    self._run(l0ops[:1], main.cuda_stream)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
             for fn in hooks:
