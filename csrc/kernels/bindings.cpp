@@ -77,9 +77,6 @@ hipError_t dg_conv_l1(int kw, const void* A, int KP, int M, int Mpad, const void
                       void* mask, const void* pbias, hipStream_t stream);
 void dg_conv_wgrad_win_set_ablate(int mode);
 int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus);
-int dg_conv_wgrad_l0_splits(int M, int B, int num_cus);
-hipError_t dg_conv_wgrad_l0(const void* dZ, const void* X, const void* zero, float* slab,
-                            int M, int Mpad, int KP, int B, int splits, hipStream_t stream);
 hipError_t dg_conv_layer2(int epi, const void* A, const void* pbias, const void* X, void* Y,
                           void* mask, int C, int B, hipStream_t stream);
 hipError_t dg_conv_layer2_multi_head(const long long* table, int nl, int B, const float* w,
@@ -544,16 +541,6 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
           "conv_wgrad_win");
   }, "sliding-window 3x3 weight gradients (frame-linear K, 9 taps per staged X window)");
-  m.def("conv_wgrad_l0", [](uintptr_t dz, uintptr_t x, uintptr_t zero, uintptr_t slab, int M,
-                            int Mpad, int KP, int B, int splits, uintptr_t stream) {
-    check(dg_conv_wgrad_l0(P<void>(dz), P<void>(x), P<void>(zero), P<float>(slab), M, Mpad, KP,
-                           B, splits, S(stream)),
-          "conv_wgrad_l0");
-  }, "first-layer (5x5, 40-channel) sliding-window weight gradient: dZ frames pad 1, X frames "
-     "pad 2, fp32 slabs [splits][Mpad][KP] with k = t * 40 + ci (conv_wgrad_l0.hip)");
-  m.def("conv_wgrad_l0_splits", [](int M, int B, int num_cus) {
-    return dg_conv_wgrad_l0_splits(M, B, num_cus);
-  });
   m.def("conv_wgrad_win_splits", [](int nl, int M, int Cx, int B, int num_cus) {
     return dg_conv_wgrad_win_splits(nl, M, Cx, B, num_cus);
   });

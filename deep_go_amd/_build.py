@@ -28,7 +28,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
-HIP_SOURCES = ["conv_mfma.hip", "conv_board.hip", "conv_stack2.hip", "conv_layer2.hip", "conv_stack_f8.hip", "conv_wgrad_win.hip", "conv_wgrad_win8.hip", "conv_wgrad_l0.hip", "conv_l1.hip", "conv_fp8.hip", "head.hip", "head_mfma.hip", "elementwise.hip", "bindings.cpp"]
+HIP_SOURCES = ["conv_mfma.hip", "conv_board.hip", "conv_stack2.hip", "conv_layer2.hip", "conv_stack_f8.hip", "conv_wgrad_win.hip", "conv_wgrad_win8.hip", "conv_l1.hip", "conv_fp8.hip", "head.hip", "head_mfma.hip", "elementwise.hip", "bindings.cpp"]
 CPU_SOURCES = ["go_engine.cpp", "sgf.cpp", "t7.cpp", "features.cpp", "loader.cpp",
                "bindings.cpp"]
 

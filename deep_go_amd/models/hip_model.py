@@ -74,7 +74,6 @@ class ConvPlan:
     board: bool = False    # fwd uses the board-tiled kernel
     board_d: bool = False  # dgrad uses the board-tiled kernel
     fp8: bool = False      # forward on the e4m3 MX-MFMA kernel (conv_fp8.hip)
-    l0win: bool = False    # first-layer weight gradient on conv_wgrad_l0.hip
 
 
 class HipGoNet:
@@ -159,11 +158,8 @@ class HipGoNet:
             splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
                                            self.h.conv_wgrad_wgs_per_cu_for(KPw),
                                            self.h.conv_wgrad_ktile(KPw))
-            l0win = self._l0_win_ok(spec, cinp, KPw)
-            if l0win:
-                splits = self.h.conv_wgrad_l0_splits(spec.cout, batch, num_cus)
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
-                         Mpad, KPw, Mpad_w, splits, board=board, l0win=l0win)
+                         Mpad, KPw, Mpad_w, splits, board=board)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
             if spec.index > 0:
                 bm_d, bn_d = LY.pick_tiles(npix, spec.cin, num_cus)
@@ -300,7 +296,6 @@ class HipGoNet:
         bpart = torch.empty(self.bchunks * (NUM_POINTS + 19) * cmax, dtype=torch.float32,
                             device=dev)
         self.slabs = [slab] * len(self.plans)
-        self.zero_rows = torch.zeros(64, dtype=torch.int32, device=dev)   # 256 zero bytes
         self.bparts = [bpart] * len(self.plans)
         self.slab = slab
 
@@ -546,17 +541,11 @@ class HipGoNet:
             slab, bpart = self.slabs[i].data_ptr(), self.bparts[i].data_ptr()
             ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
                                               bpart)))
-            if p.l0win:
-                # the first layer's 5x5 weight gradient as a sliding window over the 23 x 23
-                # input frames (conv_wgrad_l0.hip) instead of the im2col three-slice kernel
-                assert dzp == 1 and spec.pad == 2
-                ops.append((h.conv_wgrad_l0, (self.dz[i].data_ptr(), xin.data_ptr(),
-                                              self.zero_rows.data_ptr(), slab, p.cout,
-                                              p.Mpad_w, p.KPw, self.B, p.splits)))
-            else:
-                ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                           xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                           p.splits, slab)))
+            # (the first layer's 5x5 as a sliding window over its 23 x 23 input frames was
+            # measured slower: profiles/r4_s1_wgrad_l0_window_ab.txt)
+            ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                       xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
+                                       p.splits, slab)))
             red = (slab, G + spec.w_off * f4, p.splits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
                    p.cin, p.cinp, bpart, self.bchunks, G + spec.pos_off * f4,
                    G + spec.b_off * f4)
@@ -867,15 +856,6 @@ class HipGoNet:
         if moved:
             self._dgrad_first = True
             self._group_wgrads(set(range(len(self.plans))))
-
-    def _l0_win_ok(self, spec, cinp: int, KPw: int) -> bool:
-        """The first layer's weight gradient on the sliding-window kernel (conv_wgrad_l0.hip:
-        5x5 taps over the 23 x 23 expanded-input frames, dZ gathered from the 21 x 21 frames
-        of a 3x3 second layer).  DG_WGRAD_L0=0: the im2col three-slice kernel."""
-        lay = self.layout.layers
-        return (spec.index == 0 and spec.k == 5 and spec.pad == 2 and cinp == INPUT_CP == 40
-                and spec.cout % 64 == 0 and KPw >= 1000 and len(lay) > 1 and lay[1].pad == 1
-                and os.environ.get("DG_WGRAD_L0", "1") != "0")
 
     def _layer2_ok(self, p: ConvPlan) -> bool:
         """A hidden 3x3 256 -> 256 bf16 layer runs forward and backward-data on conv_layer2.hip

@@ -443,34 +443,3 @@ def test_fp8_gradient_scale_uses_amax_history():
     assert g == [want(1000.0), want(7.0)]          # 1000 is 15 entries old: still inside
     assert step(10.0, 7.0) == [want(10.0), want(7.0)]   # 16 newer entries: 1000 left
     assert ghist[0].tolist() == [10.0] * 16
-
-
-@pytest.mark.parametrize("B,cout,splits,cin", [(3, 128, 5, 37), (5, 256, 7, 37), (2, 128, 1, 38),
-                                               (4, 64, 13, 40)])
-def test_conv_wgrad_l0(B, cout, splits, cin):
-    """First-layer 5x5 sliding-window weight gradient (conv_wgrad_l0.hip: 23 x 23 input
-    frames, dZ rows gathered from the 21 x 21 frames, flat (tap, channel) columns, split
-    ranges that start / end inside a board) vs the fp32 reference, summed over its slabs."""
-    torch.manual_seed(8)
-    from deep_go_amd.ops import layouts as LY
-    from deep_go_amd.ops.native import hip, stream_handle
-    h = hip()
-    x = torch.zeros(B, 40, 19, 19, device=DEV)
-    x[:, :cin] = (torch.rand(B, cin, 19, 19, device=DEV) < 0.3).float()   # 0/1 feature planes
-    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
-    xf = LY.alloc_frame(B, 40, 2, DEV)
-    LY.frame_interior(xf, 2).copy_(x.permute(0, 2, 3, 1))
-    dzf = LY.alloc_frame(B, cout, 1, DEV)
-    LY.frame_interior(dzf, 1).copy_(dz.permute(0, 2, 3, 1))
-    Mpad, KP = LY.round_up(cout, 128), 1024
-    slab = torch.full((splits, Mpad, KP), float("nan"), device=DEV)
-    zero = torch.zeros(64, dtype=torch.int32, device=DEV)
-    h.conv_wgrad_l0(dzf.data_ptr(), xf.data_ptr(), zero.data_ptr(), slab.data_ptr(), cout, Mpad,
-                    KP, B, splits, stream_handle())
-    torch.cuda.synchronize()
-    got = slab[:, :cout, :1000].sum(0).reshape(cout, 25, 40)
-    w0 = torch.zeros(cout, 5, 5, 40, device=DEV, requires_grad=True)
-    (gw,) = torch.autograd.grad(conv_ref(x, w0, 5), w0, dz)
-    assert torch.isfinite(got).all()
-    assert rel_err(got, gw.reshape(cout, 25, 40)) < 1e-3
-    assert h.conv_wgrad_l0_splits(128, 256, 256) >= 1
