@@ -140,7 +140,7 @@ int dg_grad_update_cols();
 hipError_t dg_grad_update(const long long* table, int n, long long plain_off, long long plain_n,
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
-                          long long* step, unsigned* tickets, int* bad_steps, int write_grads,
+                          long long* step, unsigned* tickets, int* bad_steps, int write_grads, int final,
                           hipStream_t s);
 }
 
@@ -469,11 +469,11 @@ PYBIND11_MODULE(_dghip, m) {
                           uintptr_t p, uintptr_t g, uintptr_t g16, uintptr_t ms, float rms_decay,
                           float gscale, uintptr_t gate, uintptr_t lr, double decay,
                           uintptr_t step, uintptr_t tickets, uintptr_t bad, int write_grads,
-                          uintptr_t stream) {
+                          int final, uintptr_t stream) {
     check(dg_grad_update(P<long long>(table), n, plain_off, plain_n, P<float>(p), P<float>(g),
                          P<void>(g16), P<float>(ms), rms_decay, gscale, P<float>(gate),
                          P<double>(lr), decay, P<long long>(step), P<unsigned>(tickets),
-                         P<int>(bad), write_grads, S(stream)),
+                         P<int>(bad), write_grads, final, S(stream)),
           "grad_update");
   }, "fused gradient pass 2 (slabs / bias partials, or the flat gradient) + SGD / RMSProp + "
      "operand refresh + LR decay (elementwise.hip grad_update_kernel)");

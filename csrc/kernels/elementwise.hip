@@ -543,7 +543,8 @@ constexpr int GU_MAXG = 64;      // groups per row (grid.x <= 1024)
 constexpr int GU_T_ROW = 4 * MAX_GU;
 constexpr int GU_T_GRP = GU_T_ROW + MAX_GU + 1;
 constexpr int GU_T_GRID = GU_T_GRP + (MAX_GU + 1) * GU_MAXG;
-constexpr int GU_TICKETS = GU_T_GRID + 1;
+constexpr int GU_T_PEND = GU_T_GRID + 1;   // a non-final launch's non-finite flag
+constexpr int GU_TICKETS = GU_T_PEND + 1;
 struct GUArgs {
   int n;
   int tblocks;         // blocks [0, tblocks) of a row: weight tiles; the rest: biases
@@ -563,6 +564,10 @@ struct GUArgs {
                        // << 16)
   int write_grads;     // slab mode: also write the reduced fp32 gradient (tests / tools)
   int* bad_steps;
+  // 1: the step's last (or only) update launch — decays the LR, counts the step, consumes a
+  // pending non-finite flag; 0: an earlier part (e.g. the hidden layers, issued as soon as
+  // their gradients exist) — leaves the LR alone and parks its non-finite flag
+  int final;
 };
 
 // one parameter's update; ms (RMSProp only) is updated in place
@@ -818,11 +823,17 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
         flag = ((old >> 16) != 0u || flag) ? 0x10000u : 0u;
         old = atomicAdd(T + GU_T_GRID, 1u + flag);
         if ((old & 0xFFFFu) == gridDim.y - 1) {
-          double* lrw = const_cast<double*>(a.lr);
-          *lrw = *lrw * (1.0 - a.decay);
-          if (a.step) *a.step += 1;
           const bool flagged = (old >> 16) != 0u || flag;
-          if (flagged && a.bad_steps && apply) *a.bad_steps += 1;
+          if (a.final) {
+            double* lrw = const_cast<double*>(a.lr);
+            *lrw = *lrw * (1.0 - a.decay);
+            if (a.step) *a.step += 1;
+            const bool any = flagged || T[GU_T_PEND] != 0u;
+            if (any && a.bad_steps && apply) *a.bad_steps += 1;
+            T[GU_T_PEND] = 0u;
+          } else if (flagged) {
+            T[GU_T_PEND] = 1u;
+          }
           T[GU_T_GRID] = 0u;
         }
       }
@@ -1048,7 +1059,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
                           long long* step, unsigned* tickets, int* bad_steps, int write_grads,
-                          hipStream_t s) {
+                          int final, hipStream_t s) {
   if (n <= 0 || n > MAX_GU || !P || !G || !lr || !tickets || plain_n < 0)
     return hipErrorInvalidValue;
   GUArgs a;
@@ -1096,6 +1107,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
   a.tickets = tickets;
   a.bad_steps = bad_steps;
   a.write_grads = write_grads;
+  a.final = final;
   a.tblocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
   const int blocks = a.tblocks + GU_NB * maxncb;
   if (blocks > GU_TG * GU_MAXG) return hipErrorInvalidValue;   // the ticket tree's groups

@@ -137,6 +137,8 @@ class HipGoNet:
         # (train_step / SegmentedStep's whole-step graph; see can_defer)
         self._defer = False
         self._gate_issued = False   # this step's loss gate already issued (side stream)
+        self._early_issued = False  # this step's early update launch issued (main stream)
+        self._early_ok = os.environ.get("DG_EARLY_UPDATE", "1") != "0"
         self._red_src = {}    # layer -> (slab, bpart, splits, Mpad, KP, bchunks) of its pass 2
 
         # ---- per-layer plans + bf16 operand weights ----
@@ -1224,6 +1226,8 @@ class HipGoNet:
                 self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
                 self._run(ops[2:3], main.cuda_stream)
+                if l0_side:
+                    self._issue_early_update(main.cuda_stream)
             for fn in hooks:
                 fn()
         self._run(ops[3:], main.cuda_stream)
@@ -1315,7 +1319,8 @@ class HipGoNet:
         if self.cfg.nan_policy != "raise":
             gate = self.gate.data_ptr()
         self._gate_issued = False
-        self._fp8_update(s)
+        if not (slabs and self._early_issued):
+            self._fp8_update(s)
         if os.environ.get("DG_FUSED_UPDATE", "1") == "0":
             if self.ms is not None:
                 (self.h.rmsprop_bf16 if w16 else self.h.rmsprop)(
@@ -1331,14 +1336,54 @@ class HipGoNet:
             return
         t = self._gu_table(slabs)
         hd = self.head
-        self.h.grad_update(t.ctypes.data, len(t), hd.w_off, n - hd.w_off,
+        plain = (hd.w_off, n - hd.w_off)
+        if slabs and self._early_issued:
+            # the hidden layers and the head were updated by the early launch (beside the
+            # first layer's gradient chain): the rest, then the LR decay
+            t = self._gu_split(t)[1]
+            plain = (0, 0)
+        self._early_issued = False
+        self._gu_launch(t, plain, grad_scale, gate, 1, s)
+
+    def _gu_launch(self, t, plain, grad_scale, gate, final, s):
+        w16 = self.grads16 is not None
+        self.h.grad_update(t.ctypes.data, len(t), plain[0], plain[1],
                            self.params.data_ptr(), self.grads.data_ptr(),
                            self.grads16.data_ptr() if w16 else 0,
                            self.ms.data_ptr() if self.ms is not None else 0,
                            float(self.cfg.rmsprop_decay), grad_scale, gate, self.lr.data_ptr(),
                            float(self.cfg.rateDecay), self.step_count.data_ptr(),
                            self.gu_tickets.data_ptr(), self.bad_steps.data_ptr(),
-                           int(self.keep_grads), s)
+                           int(self.keep_grads), final, s)
+
+    def _gu_split(self, t):
+        """(early rows, late rows) of a deferred step's grad_update table: the grouped
+        launch's layers (their slabs and bias partials exist once it ends) | the rest (the
+        first layer: its side-stream chain ends later)."""
+        sp = getattr(self, "_gu_split_tabs", None)
+        if sp is None:
+            early = self._defer_layers()
+            idx_e = [k for k, p in enumerate(self.plans) if p.index in early]
+            idx_l = [k for k, p in enumerate(self.plans) if p.index not in early]
+            sp = (np.ascontiguousarray(t[idx_e]), np.ascontiguousarray(t[idx_l]))
+            self._gu_split_tabs = sp
+        return sp
+
+    def _issue_early_update(self, stream):
+        """Deferred single-GPU step: update the grouped launch's layers and the head as soon
+        as their gradients exist (right after the grouped weight-gradient launch, on the main
+        stream beside the first layer's side-stream chain) instead of after it; the fused
+        update's final launch then covers only the first layer and decays the LR.
+        DG_EARLY_UPDATE=0: one update launch at the end."""
+        if not (self._defer and self._early_ok and self.cfg.nan_policy != "raise"
+                and len(self._gu_split(self._gu_table(True))[1]) > 0):
+            return
+        self._fp8_update(stream)
+        hd = self.head
+        t = self._gu_split(self._gu_table(True))[0]
+        self._gu_launch(t, (hd.w_off, self.layout.numel - hd.w_off), 1.0,
+                        self.gate.data_ptr(), 0, stream)
+        self._early_issued = True
 
     def _gu_table(self, slabs: bool) -> np.ndarray:
         """grad_update's table: the per-step refresh row of every conv layer + where its
