@@ -640,27 +640,38 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
     check()
 
 
-def test_fused_update_skips_non_finite_gradient_entries():
+@pytest.mark.parametrize("early", [True, False])
+def test_fused_update_skips_non_finite_gradient_entries(early):
     """With the pass 2 deferred the gradient does not exist before the update: a non-finite
     gradient entry is left unapplied (that parameter keeps its value), the step is counted
-    in bad_steps, every other parameter still updates."""
+    in bad_steps, every other parameter still updates.  early: the grouped layers' update
+    runs right after their weight-gradient launch (its flag parked for the final launch);
+    else one launch at the end."""
     cfg, net, _ = _setup(4, 128, 4, seed=1)
     net.keep_grads = True
+    net._early_ok = early
     net.forward_backward()
     torch.cuda.synchronize()
     g_ref = net.grads.clone()
     p0 = net.params.clone()
-    # poison one slab entry of a hidden layer's pass 2 (the group's slab region)
+    # poison one slab entry of a hidden layer's pass 2 (the group's slab region) on the
+    # stream, just before the update that reads it
     i = net.wgroups[0][0]
     slab, _, S, Mpad, KP, _ = net._red_src[i]
     spec = net.layout.layers[i]
+    view = torch.as_strided(net.gslab, (1,), (1,), (slab - net.gslab.data_ptr()) // 4)
+    orig = net._issue_early_update
+
+    def poisoned(stream):
+        view.fill_(float("nan"))        # co 0, tap 0, ci 0 of the first split
+        orig(stream)
+    net._issue_early_update = poisoned
     net.set_defer(True)
     try:
         net.forward_backward()
-        torch.cuda.synchronize()
-        view = torch.as_strided(net.gslab, (1,), (1,),
-                                (slab - net.gslab.data_ptr()) // 4)
-        view.fill_(float("nan"))        # co 0, tap 0, ci 0 of the first split
+        if not early:
+            view.fill_(float("nan"))
+        assert net._early_issued == early
         net.optimizer_step()
     finally:
         net._defer = False
