@@ -116,7 +116,6 @@ struct F8Args {
   // EPI_DGRAD: stochastic rounding of the e5m2 gradient quantization (MODE bit 32), random
   // bits from a hash of (step counter, layer, element); null: round to nearest even
   const long long* sr_step;
-  int park_swz;         // (A/B: 7 = swizzled park rows, 0 = plain)
   F8Layer L[MAXL];
   dghead::HeadMArgs head;
 };
@@ -515,12 +514,13 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
               // C = 256 pass 0: park (pixel-major 128-B rows) in the LDS around the image.
               // 16-B piece cl / 16 of pixel p sits at piece (cl / 16) ^ (p & 7): unswizzled,
               // the 16 pixels of a store (rows 128 B apart) hit one bank — a 16-way conflict
-              // on every parked store (~15M conflict cycles per 12x256 launch, PMC r4_s1);
-              // now 2-way (32 lanes over 8 pieces x 2 words).  (p & 7 == lane & 7: a fragment's
+              // on every parked store (~15M conflict cycles per 12x256 launch); now 2-way (32
+              // lanes over 8 pieces x 2 words): 18.0M / 16.4M -> 6.4M / 4.8M conflict cycles
+              // per launch (profiles/r4_s1_early_update_park_ab.txt).  (p & 7 == lane & 7: a fragment's
               // 16 pixels start at a multiple of 16)
               char* pr = p < G::PARK1 ? smem + p * 128
                                       : smem + SCRATCH + G::IMG + (p - G::PARK1) * 128;
-              *(uint32_t*)(pr + z0 + (cl ^ ((lane & a.park_swz) << 4))) = q8;
+              *(uint32_t*)(pr + z0 + (cl ^ ((lane & 7) << 4))) = q8;
             }
           } else if constexpr (BF16_LAST_IMAGE) {
             // bf16 two-image layout (conv_stack2 / head_body.h) for the fused head
@@ -556,7 +556,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
           const int p = u >> 3, q = u & 7;
           const char* pr = p < G::PARK1 ? smem + p * 128
                                         : smem + SCRATCH + G::IMG + (p - G::PARK1) * 128;
-          const uint4 v = *(const uint4*)(pr + z0 + ((q ^ (p & a.park_swz)) * 16));
+          const uint4 v = *(const uint4*)(pr + z0 + ((q ^ (p & 7)) * 16));
           const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
           const int f = (h + 1) * F + (w + 1);
           *(uint4*)(sIe + f * ROWB + ((q ^ fsig<C>(f)) * 16)) = v;
@@ -654,8 +654,6 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
   if (sr_step && epi != EPI_DGRAD) return hipErrorInvalidValue;
   F8Args a;
   a.sr_step = sr_step;
-  static const int park = getenv("DG_F8_PARK_SWZ") && atoi(getenv("DG_F8_PARK_SWZ")) == 0 ? 0 : 7;
-  a.park_swz = park;
   a.X0 = (const char*)X0;
   a.s_x0 = s_x0;
   a.amax_x0 = amax_x0;

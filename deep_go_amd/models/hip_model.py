@@ -138,7 +138,8 @@ class HipGoNet:
         self._defer = False
         self._gate_issued = False   # this step's loss gate already issued (side stream)
         self._early_issued = False  # this step's early update launch issued (main stream)
-        self._early_ok = os.environ.get("DG_EARLY_UPDATE", "1") != "0"
+        self._early_env = os.environ.get("DG_EARLY_UPDATE")   # None: auto (fp8 window)
+        self._early_ok = self._early_env != "0"
         self._red_src = {}    # layer -> (slab, bpart, splits, Mpad, KP, bchunks) of its pass 2
 
         # ---- per-layer plans + bf16 operand weights ----
@@ -1373,10 +1374,15 @@ class HipGoNet:
         """Deferred single-GPU step: update the grouped launch's layers and the head as soon
         as their gradients exist (right after the grouped weight-gradient launch, on the main
         stream beside the first layer's side-stream chain) instead of after it; the fused
-        update's final launch then covers only the first layer and decays the LR.
-        DG_EARLY_UPDATE=0: one update launch at the end."""
+        update's final launch then covers only the first layer and decays the LR.  Taken with
+        the MX-fp8 weight gradients (the early launch fills the CUs the fp8 window kernel
+        leaves while the first layer's 5x5 gradient finishes: +1.1% at 12x256 fp8); the bf16
+        window kernel's step measured 0.6% slower with it at 12x128 and equal at 12x256
+        (profiles/r4_s1_early_update_park_ab.txt).  DG_EARLY_UPDATE=0 / 1: never / always."""
         if not (self._defer and self._early_ok and self.cfg.nan_policy != "raise"
                 and len(self._gu_split(self._gu_table(True))[1]) > 0):
+            return
+        if self._early_env is None and not self.win8_groups:
             return
         self._fp8_update(stream)
         hd = self.head

@@ -649,7 +649,7 @@ def test_fused_update_skips_non_finite_gradient_entries(early):
     else one launch at the end."""
     cfg, net, _ = _setup(4, 128, 4, seed=1)
     net.keep_grads = True
-    net._early_ok = early
+    net._early_ok, net._early_env = early, ("1" if early else "0")
     net.forward_backward()
     torch.cuda.synchronize()
     g_ref = net.grads.clone()
