@@ -941,16 +941,17 @@ def test_fp8_weight_gradient_teacher_forced(ch, layers):
         xb = net.act[i - 1].view(B, 441, ch).float()
         gb = net.dz[i].view(B, 441, ch).float()
         # a stack's own input (act[0] from conv_l1, dz[top] from the head) stays unquantized
-        # bf16: its fp8 copy is its rounding (e4m3: 2^-4, e5m2: 2^-3 relative); every other
-        # bf16 frame IS the dequantized fp8 image, bit for bit
-        # (bounds: half an ulp relative, plus the subnormal step: e4m3 2^-9, e5m2 2^-16)
+        # bf16: its fp8 copy is its rounding (e4m3 to nearest: half an ulp, 2^-4 relative;
+        # e5m2 rounded stochastically: under one ulp, 2^-2 relative); every other bf16 frame
+        # IS the dequantized fp8 image, bit for bit (plus the subnormal step: e4m3 2^-9,
+        # e5m2 2^-16)
         if i == 1:
             bad = int(((x8 - xb).abs() > xb.abs() * 2 ** -4 + 2 ** -9 * s_x).sum())
             assert bad == 0, f"layer 1: {bad} fp8 activations off their rounding"
         else:
             assert torch.equal(x8, xb), f"layer {i}: fp8 activation copy != bf16 frame"
         if i == layers - 2:
-            bad = int(((g8 - gb).abs() > gb.abs() * 2 ** -3 + 2 ** -16 * s_g).sum())
+            bad = int(((g8 - gb).abs() > gb.abs() * 2 ** -2 + 2 ** -16 * s_g).sum())
             assert bad == 0, f"layer {i}: {bad} fp8 gradients off their rounding"
         else:
             assert torch.equal(g8, gb), f"layer {i}: fp8 gradient copy != bf16 frame"
