@@ -542,17 +542,29 @@ class HipGoNet:
             # bias grads: pass 1 (per board-chunk partials); pass 2 runs inside the slab
             # reduce launch, which also finalises the weight grad
             slab, bpart = self.slabs[i].data_ptr(), self.bparts[i].data_ptr()
-            ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
-                                              bpart)))
+            bch = self.bchunks
+            if i == 0 and os.environ.get("DG_L0_BIAS_SMALL", "1") != "0":
+                # the first layer's partials on the multi-layer kernel's 256-thread,
+                # 48-VGPR workgroups (64-board chunks): they fit beside the window kernel's
+                # workgroups, where the single-layer launch's 600-thread ones wait for free
+                # CUs (12x256 bf16: 552 us on the side stream's critical chain)
+                self._l0_btab = np.ascontiguousarray(
+                    np.array([[self.dz[i].data_ptr(), bpart, 0]], dtype=np.int64))
+                bch = self.bchunks_g
+                ops.append((h.bias_grad_partial_multi, (self._l0_btab.ctypes.data, 1, self.B,
+                                                        p.cout, dzp)))
+            else:
+                ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
+                                                  bpart)))
             # (the first layer's 5x5 as a sliding window over its 23 x 23 input frames was
             # measured slower: profiles/r4_s1_wgrad_l0_window_ab.txt)
             ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
                                        xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
                                        p.splits, slab)))
             red = (slab, G + spec.w_off * f4, p.splits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
-                   p.cin, p.cinp, bpart, self.bchunks, G + spec.pos_off * f4,
+                   p.cin, p.cinp, bpart, bch, G + spec.pos_off * f4,
                    G + spec.b_off * f4)
-            self._red_src[i] = (slab, bpart, p.splits, p.Mpad_w, p.KPw, self.bchunks)
+            self._red_src[i] = (slab, bpart, p.splits, p.Mpad_w, p.KPw, bch)
             if self.grads16 is not None:
                 ops.append((h.wgrad_reduce_w, red + (self._g16(spec.w_off),
                                                      self._g16(spec.pos_off),
