@@ -178,13 +178,13 @@ DG_DEV uint32_t pack8x4(float a, float b, float c, float d) {
 // position, so the dgrad chain and the weight-gradient sums over ~92k pixels keep the small
 // consistent components that round-to-nearest erases (the memorisation stall of
 // tools/fp8_memo.py: tests/test_train_gpu.py test_fp8_stress_vs_bf16_memorisation).
+// (one multiply-xorshift round: the keys are distinct per element and step, and the SR
+// decision needs well-spread bits per element, not a full avalanche mix; the two-round
+// finalizer it replaces cost 8 VALU per fragment — test_fp8_dgrad_stochastic_rounding_is_
+// unbiased checks the statistics)
 DG_DEV uint32_t sr_hash(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
+  x *= 0x9E3779B1u;
+  return x ^ (x >> 16);
 }
 DG_DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 DG_DEV uint32_t pack_bf8x4_sr(float a, float b, float c, float d, uint32_t h) {
