@@ -36,9 +36,10 @@
 // 8 dZ + 16 X blocks per workgroup, and a super-step needs at most 11 new X blocks: 128 rows,
 // +32 across a board edge, +16 alignment — a wave without a block re-loads the first one,
 // same bytes), so "super-step S+1 landed" with S+2 .. S+PD-1 still in flight =
-// vmcnt(PER * (PD - 1)).  Prefetch distance PD = 3: the ring holds super-steps S .. S+3,
-// whose rows span at most 4 x (128 + 32) + 76 + 30 = 746 < 1024 rows (static_assert below),
-// so a DMA never overwrites rows a wave may still read.
+// vmcnt(PER * (PD - 1)).  Prefetch distance PD = 3 (a template parameter, 2..4; 4 measured
+// equal): the ring holds super-steps S .. S+PD, whose rows span at most (PD + 1) x (128 + 32)
+// + 76 + 30 rows = 746 at PD 3, 906 at PD 4, < 1024 (static_assert below), so a DMA never
+// overwrites rows a wave may still read.
 // Output: fp32 split slabs slab[z][co][t*Cx + ci], the layout wgrad_reduce_multi sums (the
 // bf16 kernel's), so the reduce, the bias gradients and the DP buckets are unchanged.
 //
@@ -61,11 +62,11 @@ constexpr int SPB = 13;           // 32-row sub-steps per board (rows 21 .. 436)
 constexpr int XR = 1024;          // X ring rows (64 B each)
 constexpr int XRING = XR * 64;    // 64 KB
 constexpr int DZB = 128 * 64;     // one super-step of dZ rows: 8 KB
-constexpr int PD = 3;             // DMA distance (super-steps): 2 in flight beyond the next
+constexpr int PD_MAX = 4;         // DMA distance (super-steps): PD - 1 in flight beyond the next
 constexpr int MAXL = 16;
 // ring capacity at prefetch distance PD (see the header): PD + 1 super-steps of at most
 // 128 + 32 rows each, plus the 76-row tap window and 30 rows of block alignment
-static_assert((PD + 1) * (128 + 32) + 76 + 30 <= XR, "X ring capacity");
+static_assert((PD_MAX + 1) * (128 + 32) + 76 + 30 <= XR, "X ring capacity");
 
 struct Win8Layers {
   const uint8_t* dZ[MAXL];   // e5m2 [B][448][M]
@@ -95,8 +96,9 @@ DG_DEV i32x2 tr8(const LDS_AS char* p) {
 // the DMA schedule (20 1-KB blocks per super-step: 8 dZ + 12 X) are the same.
 // RA: B (X) fragments read RA taps ahead of their MFMAs (each tap's 4 tr8 reads then have
 // RA x MI MFMAs to land)
-template <int NW, int RA>
+template <int NW, int RA, int PD>
 __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Args a, Win8Layers Ls) {
+  static_assert(PD >= 2 && PD <= PD_MAX, "prefetch distance");
   constexpr int MI = 16 / NW;            // 16-co accumulator fragments per wave (4 | 2)
   constexpr int XPW = NW == 4 ? 3 : 2;   // X blocks per wave per super-step (12 | 16 >= 11)
   constexpr int DPW = 8 / NW;            // dZ blocks per wave per super-step (2 | 1)
@@ -254,12 +256,18 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
     }
     // this wave's DMAs of super-step S + 1 landed (those of S + 2 .. S + PD may remain),
     // then every wave's (barrier): the next super-step's rows are visible and S's free
-    if (S + PD < s1)
-      dma_wait<PER * (PD - 1)>();
-    else if (S + 2 < s1)
-      dma_wait<PER>();
-    else
-      dma_wait<0>();
+    {
+      // in flight beyond S + 1: super-steps S + 2 .. min(S + PD, s1 - 1)
+      const int ahead = min(PD - 1, s1 - S - 2);
+      if (ahead >= PD - 1)
+        dma_wait<PER * (PD - 1)>();
+      else if (ahead == 2)
+        dma_wait<2 * PER>();
+      else if (ahead == 1)
+        dma_wait<PER>();
+      else
+        dma_wait<0>();
+    }
     __syncthreads();
   }
 
@@ -329,7 +337,9 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
   // the same — profiles/r3_fp8_wgrad_ab.txt)
   // (B reads 2 taps ahead measured the same as 1: profiles/r4_s1_fused_update_and_fp8_bisection.txt)
-  hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1>), grid, dim3(512), 0, stream, a, Ls);
+  // prefetch distance 3: 4 measured equal (12x256 fp8 133.7k vs 133.9k,
+  // profiles/r4_s2_sr_hash_win8_pd_ab.txt)
+  hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3>), grid, dim3(512), 0, stream, a, Ls);
   return hipGetLastError();
 }
 
