@@ -1040,6 +1040,18 @@ class HipGoNet:
                 # ops = [bias partial, wgrad, reduce, (dgrad)]: the group's first layer
                 # launches all three passes for the whole group
                 self._bwd[i][0:3] = [(self._noop, ())] * 3
+            # layer 0's bias partials as one more row of the last group's launch (its chain
+            # runs on the side stream right after it) at d = 128: 12x128 fp8 +1.1%, bf16
+            # equal; at d = 256 the 5x5 weight gradient then starts earlier beside the window
+            # kernel and stretches it (12x256 fp8 -6.6%, bf16 equal;
+            # profiles/r4_s2_l0_bias_merge_ab.txt)
+            p_l0 = self.plans[0]
+            if (g is groups[-1] and self._l0_side_at is not None and len(brows) < 16
+                    and p_l0.cout == p0.cout and p0.cout <= 128
+                    and self.dzp[0] == self.dzp[g[0]]
+                    and self._bwd[0][0][0] is h.bias_grad_partial_multi):
+                brows.append([self.dz[0].data_ptr(), self.bparts[0].data_ptr(), 0])
+                self._bwd[0][0] = (self._noop, ())
             tabs = [np.ascontiguousarray(np.array(r, dtype=np.int64))
                     for r in (wrows, brows, rrows)]
             self._wgroup_tables.extend(tabs)
