@@ -81,17 +81,22 @@ def _dp_worker(rank, world, port, B, out_path, grad_dtype):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
-def test_dp2_equals_dp1(tmp_path, grad_dtype):
+@pytest.mark.parametrize("world,grad_dtype", [(2, "fp32"), (2, "bf16"), (4, "fp32"),
+                                              (8, "fp32")])
+def test_dp_equals_dp1(tmp_path, world, grad_dtype):
+    """DP=k with per-rank batch B/k gives the update of DP=1 with batch B
+    (world 2, 4 and 8 gloo ranks on the CPU; 8 = one rank per MI355X of a node)."""
     B = 8
-    out2 = str(tmp_path / "dp2.pt")
-    mp.spawn(_dp_worker, args=(2, _free_port(), B, out2, grad_dtype), nprocs=2, join=True)
+    outk = str(tmp_path / f"dp{world}.pt")
+    mp.spawn(_dp_worker, args=(world, _free_port(), B, outk, grad_dtype), nprocs=world,
+             join=True)
     out1 = str(tmp_path / "dp1.pt")
     mp.spawn(_dp_worker, args=(1, _free_port(), B, out1, grad_dtype), nprocs=1, join=True)
-    a = torch.load(out2, weights_only=True)
+    a = torch.load(outk, weights_only=True)
     b = torch.load(out1, weights_only=True)
     assert torch.allclose(a["params"], b["params"], atol=1e-6, rtol=1e-5)
-    ref = torch.arange(1000, dtype=torch.float32) * 3  # sum over ranks of (rank+1)*i
+    # sum over ranks of (rank + 1) * i
+    ref = torch.arange(1000, dtype=torch.float32) * (world * (world + 1) // 2)
     if grad_dtype == "fp32":
         assert torch.equal(a["g"], ref)
     else:
