@@ -260,8 +260,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
       if constexpr (ABL & 1) {
         asm volatile("" ::"v"(bfr));
       } else {
+        if constexpr (ABL & 32) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[i], bfr, acc[i][t]);
+        if constexpr (ABL & 32) __builtin_amdgcn_s_setprio(0);
       }
     }
     wait_next(st);
@@ -328,6 +330,15 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
   }
   WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / coch) * (Cx / 64) * splits);
+  // d >= 256: s_setprio 1 around each tap's MFMAs (ABL bit 32).  This kernel is the step's
+  // critical path there and the side stream's bias partials / 5x5 weight gradient share its
+  // CUs: 12x256 bf16 +1.6%; at d = 128 the side chain is the critical one (-2.9%), and the
+  // same priority on the MX-fp8 window kernel, the side kernels or the stacks measured equal
+  // or slower (profiles/r4_s2_wave_priority_ab.txt)
+  if (M >= 256 && (g_win_ablate & 31) == 0) {
+    launch_win<32>(grid, a, Ls, stream);
+    return hipGetLastError();
+  }
   switch (g_win_ablate & 31) {
     case 0: launch_win<0>(grid, a, Ls, stream); break;
 #define WIN_CASE(n) \
