@@ -1400,13 +1400,16 @@ class HipGoNet:
         stream beside the first layer's side-stream chain) instead of after it; the fused
         update's final launch then covers only the first layer and decays the LR.  Taken with
         the MX-fp8 weight gradients (the early launch fills the CUs the fp8 window kernel
-        leaves while the first layer's 5x5 gradient finishes: +1.1% at 12x256 fp8); the bf16
-        window kernel's step measured 0.6% slower with it at 12x128 and equal at 12x256
-        (profiles/r4_s1_early_update_park_ab.txt).  DG_EARLY_UPDATE=0 / 1: never / always."""
+        leaves while the first layer's 5x5 gradient finishes: +1.1% at 12x256 fp8) and at
+        d >= 256 in bf16 (+0.4% at 12x256 once its window kernel runs at wave priority 1); the
+        bf16 step at 12x128 measured 0.6% slower / equal with it
+        (profiles/r4_s1_early_update_park_ab.txt, profiles/r4_s2_early_update_ab.txt).
+        DG_EARLY_UPDATE=0 / 1: never / always."""
         if not (self._defer and self._early_ok and self.cfg.nan_policy != "raise"
                 and len(self._gu_split(self._gu_table(True))[1]) > 0):
             return
-        if self._early_env is None and not self.win8_groups:
+        if (self._early_env is None and not self.win8_groups
+                and max(self.plans[i].cout for g in self.wgroups for i in g) < 256):
             return
         self._fp8_update(stream)
         hd = self.head
