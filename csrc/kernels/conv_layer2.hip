@@ -302,10 +302,15 @@ __global__ void __launch_bounds__(NT) conv_layer2_multi_kernel(MultiArgs m) {
     }
   };
   auto mma = [&](const bf16x8 (&af)[MF], const bf16x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+    // each k-half's MFMA cluster at wave priority 1: the SIMD's other wave then issues its
+    // LDS reads / loads around the cluster instead of between its MFMAs (12x256 bf16 +0.4%,
+    // profiles/r4_s2_wave_priority_ab.txt)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   bool staged = false;   // buffer 0 already holds this item's chunk 0

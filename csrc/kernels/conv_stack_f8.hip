@@ -319,12 +319,16 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     }
   };
   auto mma = [&](const i32x8 (&af)[MF], int i0, const i32x8 (&bfr)[NF], f32x4 (&acc)[MF][NF]) {
+    // each MFMA cluster at wave priority 1 (12x128 fp8 +0.5%, 12x256 fp8 +0.7%;
+    // profiles/r4_s2_wave_priority_ab.txt)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = i0; i < i0 + 2; ++i)
 #pragma unroll
       for (int j = 0; j < NF; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0,
                                                                       BFMT, 0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   // Copy-out of the previous layer's output (the e4m3 image) as bf16 (x s_prev) + ReLU bits:
