@@ -24,8 +24,7 @@ What one step is (nothing skipped inside the timed region):
 Weak scaling: 256 boards per GPU per step (BASELINE.json config "12-layer d=128 CNN bf16
 on one MI355X, batch=256"; global batch = 256*N).  Synthetic 19x19 positions, random-init
 weights (BASELINE.json: no datasets/checkpoints available).  Top-1 accuracy on synthetic
-random labels is meaningless and is not reported here; held-out top-1 on the real fixture
-comes from ``tools/real_data_run.py`` (profiles/).
+random labels is meaningless; the metric's accuracy half is measured separately (below).
 
 After the headline timing (never inside it) the same process measures:
   * ``secondary``: the headline network in fp8 (12x128 fp8) and the d=256 configs (BASELINE
@@ -34,7 +33,11 @@ After the headline timing (never inside it) the same process measures:
   * ``dp`` (N > 1 or --force-dp): communicator kind and RCCL version, per-rank devices, bytes
     all-reduced per step, the step's bucket collectives timed alone (us/step, bus GB/s), the
     same network's step without collectives, and from those the exposed communication time
-    and the fraction of it hidden behind compute.
+    and the fraction of it hidden behind compute;
+  * ``accuracy`` (rank 0, --accuracy-steps): the headline network trained on the reference's
+    bundled games, top-1 / NLL on every position of the held-out validation and test games
+    (``fixture_top1`` = validation top-1; one game per split: paper-level parity unpinned;
+    ``deep_go_amd/train/accuracy.py``).
 
 Multi-rank safety: every rank arms a phase guard (``utils/faults.PhaseGuard``) before the
 process-group rendezvous.  Each phase has its own deadline: ``init`` / ``comm`` / ``capture``
@@ -95,8 +98,9 @@ def parse(argv=None):
                     help="DP gradient wire format (the bucket all-reduces): bf16 halves the "
                          "bytes on xGMI; every gradient pass 2 writes the bf16 twin itself "
                          "and the fused update reads it (no conversion kernels).  Bounded "
-                         "against the fp32 wire by tests/test_train_gpu.py "
-                         "test_bf16_gradient_wire_200_step_curve")
+                         "against the fp32 wire at world 8 (per-hop ring rounding) by "
+                         "tests/test_wire_cpu.py and tests/test_train_gpu.py "
+                         "test_bf16_gradient_wire_world8_memorisation_curve")
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
                          "torch = torch.distributed between graph segments, proxy = world-1 "
@@ -137,6 +141,11 @@ def parse(argv=None):
                          "run may use the budget minus a 150-s reserve; if a rank's guard "
                          "reports a hang while it was on the native communicator, the "
                          "fallback run gets what is left.  Worst case: %(default)s s")
+    ap.add_argument("--accuracy-steps", type=int, default=1000,
+                    help="after the timed phases (untimed): train the bench's network this many "
+                         "SGD steps (batch 64) on the reference's bundled training games and "
+                         "report top-1 / NLL on the held-out validation and test games "
+                         "(\"accuracy\" in the JSON; rank 0 only; 0 = skip)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/timing/JSON path on CPU over gloo (BASELINE config 1 "
                          "model); no GPU")
@@ -617,10 +626,12 @@ def run_gpu(args) -> int:
              "step_mode": case.step.mode, "spinup_steps": args.spinup_steps,
              "input_prefetch": bool(case.prefetch)}
     step_ms = 1000.0 * max(elapsed_all) / args.steps
+    # gradient precision of the step: single-GPU gradients are reduced in fp32 (split-K slabs
+    # + fused update); under DP the bucket all-reduces run in --grad-dtype
+    extra["grad_dtype"] = args.grad_dtype if use_dp else "fp32"
     if use_dp:
         extra["comm"] = comm.kind
         extra["ranks_params_identical"] = consistent
-        extra["grad_dtype"] = args.grad_dtype
         extra.update(extra_comm)
         if not args.no_report:
             extra["dp"] = _dp_report(case, comm, world, dev, args, step_ms)
@@ -662,6 +673,19 @@ def run_gpu(args) -> int:
         torch.cuda.empty_cache()
     if sec:
         headline["secondary"] = sec
+    if args.accuracy_steps > 0:
+        # the metric's accuracy half (train.lua:14-45,122), untimed; rank 0 trains its own
+        # single-GPU copy while the other ranks wait at the barrier
+        guard.phase("accuracy", args.phase_timeout)
+        acc = None
+        if info.rank == 0:
+            from deep_go_amd.train.accuracy import fixture_accuracy
+            acc = fixture_accuracy(dev, layers=args.layers, channels=args.channels,
+                                   dtype=args.dtype, steps=args.accuracy_steps)
+        dp.barrier()
+        if acc is not None:
+            headline["fixture_top1"] = acc["validation_top1"]
+            headline["accuracy"] = acc
     guard.stop()
     if info.rank == 0:
         print(json.dumps(headline), flush=True)

@@ -531,6 +531,54 @@ class GradBucketer:
         torch.cuda.current_stream().wait_stream(self.comm.stream)
 
 
+BF16_UNIT_ROUNDOFF = 2.0 ** -8    # bf16: 8 significand bits, round to nearest even
+
+
+def ring_allreduce_emulate(parts: Sequence[torch.Tensor],
+                           buckets: Optional[Sequence[Tuple[int, int, int]]] = None,
+                           wire: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """What a ring all-reduce of ``len(parts)`` ranks' flat gradients (each already in the
+    wire dtype: the bf16 twin every gradient pass 2 writes) hands back, rounding like RCCL's
+    reduction kernels: every hop of the reduce-scatter loads the incoming partial sum and the
+    local value, adds them in fp32 and stores the result in the wire dtype.  Each bucket is
+    cut into ``n`` contiguous chunks; chunk c is accumulated in rank order c+1, c+2, ...,
+    c+n (mod n), so its n-1 additions are rounded n-1 times (the all-gather half copies).
+    That is the most roundings any of RCCL's algorithms applies to one element (a tree's
+    reduce rounds at most depth <= n-1 times), so bounds shown for this emulation hold for
+    the real collective.  Returns the reduced gradient in the wire dtype.
+    Reference: the DataParallelTable reduces fp32 gradients (experiments.lua:155-168)."""
+    n = len(parts)
+    if n == 0:
+        raise ValueError("no ranks")
+    numel = parts[0].numel()
+    if any(p.numel() != numel for p in parts):
+        raise ValueError("every rank's gradient must have the same size")
+    stack = torch.stack([p.reshape(-1).to(wire) for p in parts])     # [n, numel]
+    out = torch.empty(numel, dtype=wire, device=stack.device)
+    for s, e, _ in (buckets or [(0, numel, 0)]):
+        bounds = [s + (e - s) * c // n for c in range(n + 1)]
+        for c in range(n):
+            lo, hi = bounds[c], bounds[c + 1]
+            if hi <= lo:
+                continue
+            order = [(c + 1 + j) % n for j in range(n)]
+            acc = stack[order[0], lo:hi]
+            for r in order[1:]:
+                acc = (acc.float() + stack[r, lo:hi].float()).to(wire)
+            out[lo:hi] = acc
+    return out
+
+
+def recursive_sum_bound(parts: Sequence[torch.Tensor], u: float = BF16_UNIT_ROUNDOFF) -> torch.Tensor:
+    """Elementwise a-priori bound on |fl(ring sum) - exact sum| for n terms summed with n-1
+    roundings of unit roundoff u (Higham, recursive summation): gamma_{n-1} * sum |x_i|,
+    gamma_k = k u / (1 - k u).  The terms are the wire-dtype values themselves."""
+    n = len(parts)
+    k = n - 1
+    gamma = k * u / (1.0 - k * u)
+    return gamma * torch.stack([p.reshape(-1).double().abs() for p in parts]).sum(0)
+
+
 def all_reduce_scalars(vals: Sequence[float], device=None, op=None) -> List[float]:
     """Sum a few scalars across ranks (validation cost / errors / count)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:

@@ -137,45 +137,68 @@ def test_200_step_training_curve_matches_fp32_oracle(tmp_path):
     assert gpu_be.rate == pytest.approx(cpu_be.rate, rel=1e-9)
 
 
-def test_bf16_gradient_wire_200_step_curve(tmp_path):
-    """The data-parallel bf16 gradient wire (every gradient pass 2 writes a bf16 twin; the
-    buckets are all-reduced on it and the fused update reads it) against the fp32 wire: 200
-    SGD steps on the real fixture from the same init and batch stream at the headline shape
-    (12x128, batch 64, rate 0.05).  The twin is what a world-N all-reduce sums, so at world 1
-    this isolates its rounding.  Bounds: per-step loss within 0.02 nats, each 50-step window
-    mean within 0.5%, the parameter update (p_200 - p_0) within 5% relative norm."""
+def test_bf16_gradient_wire_world8_memorisation_curve(tmp_path):
+    """The data-parallel bf16 gradient wire at WORLD 8, emulated on one GPU, against the fp32
+    wire, in a regime with a real learning signal.  Every step's global
+    batch of 64 (cycling a 256-position subset of the real fixture: memorisation; 12x128, rate
+    0.07, no head ReLU) is split into 8 rank shards of 8 boards; each shard's backward runs on
+    the HIP executor with the global-batch gradient scale, exactly as a rank would.  The bf16
+    arm takes each shard's bf16 twin (what the gradient pass 2 writes) and sums them with a
+    ring all-reduce's per-hop bf16 rounding (parallel.dp.ring_allreduce_emulate: 7 roundings
+    per element — RCCL's worst case); the fp32 arm sums the fp32 shard gradients in fp32 (the
+    reference's DataParallelTable reduce).  Both optimizers then run from those reduced
+    gradients (the bf16 arm reads the twin, as under DP).  Bounds: every loss finite; both
+    arms fall by more than 1 nat; the first 100-step windows agree within 2%; afterwards the
+    bf16 arm lags by at most one window (the fp8 stress test's one-sided rule: SGD at this
+    rate is chaotic, so the trajectories separate and either may learn faster)."""
     from deep_go_amd.data.dataset import PackedDataset
     from deep_go_amd.data.loader import BatchLoader
     from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep
-    cfg = _cfg(tmp_path, numLayers=12, channelSize=128, batchSize=64, rate=0.05,
-               rateDecay=1e-4, head_relu=False, synthetic=False, data_root=FIXTURE)
+    from deep_go_amd.parallel import dp
+    B, R, N, W = 64, 8, 600, 100
     pk = PackedDataset.load(os.path.join(FIXTURE, "train.dgpack.npz"))
-    ld = BatchLoader(pk, 64, threads=2, prefetch=3, seed=6, pin=False)
-    batches = [ld.next_numpy() for _ in range(200)]
+    ld = BatchLoader(pk, B, threads=2, prefetch=4, seed=9, pin=False)
+    subset = [[np.asarray(x) for x in ld.next_numpy()] for _ in range(256 // B)]
     ld.close()
-    nets = [HipGoNet(cfg, 64, device="cuda", grad_wire=w) for w in ("fp32", "bf16")]
-    nets[1].load_params(nets[0].params.clone())
-    assert nets[1].grads16 is not None and not nets[1].can_defer()
-    p0 = nets[0].params.clone()
-    steps = [SegmentedStep(n, None, use_graphs=True) for n in nets]
-    curves = [[], []]
-    for bt in batches:
-        for k, n in enumerate(nets):
-            n.set_batch(*(torch.from_numpy(np.asarray(x)).cuda() for x in bt))
-            steps[k]()
-            curves[k].append(n.mean_loss().item())
-    l32, l16 = np.array(curves[0]), np.array(curves[1])
+    cfg = _cfg(tmp_path, numLayers=12, channelSize=128, batchSize=B, rate=0.07,
+               rateDecay=1e-5, head_relu=False, synthetic=False, data_root=FIXTURE, seed=13)
+    nets = {w: HipGoNet(cfg, B // R, device="cuda", global_batch=B, grad_wire=w)
+            for w in ("fp32", "bf16")}
+    nets["bf16"].load_params(nets["fp32"].params.clone())
+    steps = {w: SegmentedStep(n, None, use_graphs=True) for w, n in nets.items()}
+    lay = nets["fp32"].layout
+    buckets = dp.make_buckets([lay.layer_range(i) for i in range(len(lay.layers))],
+                              int(cfg.bucket_mb * 2 ** 20), groups=nets["bf16"].wgroups)
+    curves = {"fp32": [], "bf16": []}
+    for k in range(N):
+        bt = subset[k % len(subset)]
+        for w, net in nets.items():
+            parts, loss = [], 0.0
+            for r in range(R):
+                sl = slice(r * (B // R), (r + 1) * (B // R))
+                net.set_batch(*(torch.from_numpy(x[sl]).cuda() for x in bt))
+                steps[w].forward_backward()
+                parts.append((net.grads16 if w == "bf16" else net.grads).clone())
+                loss += net.loss.sum().item()
+            if w == "bf16":
+                net.grads16.copy_(dp.ring_allreduce_emulate(parts, buckets))
+            else:
+                net.grads.copy_(dp.ring_allreduce_emulate(parts, buckets, wire=torch.float32))
+            steps[w].optimizer()
+            curves[w].append(loss / B)
+    l32, l16 = np.array(curves["fp32"]), np.array(curves["bf16"])
     import json
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/curve_200_bf16_wire.json", "w") as f:
-        json.dump({"fp32_wire": l32.tolist(), "bf16_wire": l16.tolist()}, f)
-    assert np.isfinite(l16).all()
-    assert np.abs(l32 - l16).max() < 0.02, np.abs(l32 - l16).max()
-    for w in range(4):
-        a, b = l32[50 * w:50 * (w + 1)].mean(), l16[50 * w:50 * (w + 1)].mean()
-        assert abs(a - b) < 5e-3 * a, (w, a, b)
-    da, db = nets[0].params - p0, nets[1].params - p0
-    assert ((da - db).norm() / da.norm()).item() < 0.05
+    with open("gpurun_out/curve_world8_bf16_wire.json", "w") as f:
+        json.dump({"fp32_wire": l32.tolist(), "bf16_wire_world8": l16.tolist()}, f)
+    assert np.isfinite(l16).all() and np.isfinite(l32).all()
+    assert l32[-W:].mean() < l32[:W].mean() - 1.0, (l32[:W].mean(), l32[-W:].mean())
+    assert l16[-W:].mean() < l16[:W].mean() - 1.0, (l16[:W].mean(), l16[-W:].mean())
+    assert abs(l16[:W].mean() - l32[:W].mean()) < 0.02 * l32[:W].mean()
+    for w in range(W, N, W):
+        m32, m16 = l32[w:w + W].mean(), l16[w:w + W].mean()
+        ref = max(m32, l32[w - W:w].mean())
+        assert m16 < ref + max(0.15, 0.10 * ref), (w, m32, m16)
 
 
 @pytest.mark.parametrize("ch", [128, 256])

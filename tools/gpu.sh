@@ -94,7 +94,7 @@ for step in "$@"; do
         for cfg in "${cfgs[@]}"; do
           e="${cfg%%@*}"; [ "$e" = "-" ] && e=""
           xa=""; [ "$e" != "$cfg" ] || true; case "$cfg" in *@*) xa="${cfg#*@}" ;; esac
-          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 ${AB_ARGS:-} $xa 2>/dev/null \
+          out=$(env $e timeout -k 10 200 python bench.py --steps 60 --warmup 10 --accuracy-steps 0 ${AB_ARGS:-} $xa 2>/dev/null \
                 | grep metric) || { rc=1; break 2; }
           echo "$cfg $(echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], ' '.join(f'{k}={v[\"value\"]}' for k, v in d.get('secondary', {}).items()))")" \
             | tee -a gpurun_out/ab.txt
