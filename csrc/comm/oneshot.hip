@@ -17,11 +17,21 @@
 //   3. every block waits (one lane per peer, acquire loads, s_sleep) until all `world` slots
 //      of its own flag array reach seq — with a wall-clock limit (s_memrealtime, 100 MHz):
 //      a missing peer sets the error word and the kernel finishes instead of hanging;
-//   4. every block sums its share over the world staging halves in rank order into dst;
+//   4. every block sums its share over the world staging halves in rank order into dst — a
+//      block that timed out in 3 writes NaN over its share instead: a peer's staging half
+//      may be stale, and a NaN gradient is what the optimizer's device gate skips (under DP
+//      it checks the whole all-reduced gradient), so a timed-out call never applies a sum
+//      of stale buffers (the error word also makes the watchdog abort the run);
 //   5. the last block to finish resets the counters and stores seq (graph-replayable: no
 //      host-side arguments change between calls).
 // Staging buffers and flags are allocated uncached (hipDeviceMallocUncached): remote writes
 // and reads then see memory, not a stale L2 line.  dtype 0 = fp32, 1 = bf16 (summed in fp32).
+// Co-residency: a block past step 2 waits for the LAST block's arrival, so the call completes
+// only once every one of its `blocks` workgroups has been scheduled.  Launched beside the
+// step's compute kernels (which fill every CU) the late blocks start as those kernels' own
+// workgroups retire — a delay, never a deadlock (no compute kernel waits on this one) — so
+// keep `blocks` small (the default 16 fits in the CU slots the backward leaves free) and the
+// timeout far above a step.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -76,6 +86,9 @@ __global__ void __launch_bounds__(256) oneshot_allreduce_kernel(OneShotArgs a) {
   if (s_last && tid < a.world)
     __hip_atomic_store(a.flags[tid] + a.rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   // 3. wait for every peer's data (bounded)
+  __shared__ unsigned s_timeout;
+  if (tid == 0) s_timeout = 0u;
+  __syncthreads();
   if (tid < a.world) {
     const unsigned* f = a.flags[a.rank] + tid;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -83,13 +96,20 @@ __global__ void __launch_bounds__(256) oneshot_allreduce_kernel(OneShotArgs a) {
       __builtin_amdgcn_s_sleep(2);
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
         __hip_atomic_fetch_or(a.state + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_timeout = 1u;   // (benign same-value race between the waiting lanes)
         break;
       }
     }
   }
   __syncthreads();
-  // 4. sum in rank order
+  // 4. sum in rank order (a timed-out block: NaN over its share, never a stale sum)
+  const bool timed_out = s_timeout != 0u;
   for (long long i = gid; i < a.nvec; i += stride) {
+    if (timed_out) {
+      ((uint4*)a.dst)[i] = a.dtype == 0 ? uint4{0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u}
+                                        : uint4{0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u};
+      continue;
+    }
     if (a.dtype == 0) {
       float4 s = {0.f, 0.f, 0.f, 0.f};
       for (int j = 0; j < a.world; ++j) {

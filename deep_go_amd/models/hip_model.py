@@ -29,7 +29,7 @@ from ..config import NUM_POINTS, ExperimentConfig
 from ..data.batch import pack_batch, packed_batch_bytes, unpack_views  # noqa: F401
 from ..ops import layouts as LY
 from ..ops.native import hip, stream_handle
-from ..utils import trace
+from ..utils import streamcheck, trace
 from .gocnn import ParamLayout, init_params
 
 INPUT_CP = 40  # 37 planes padded to 5 x 8-channel groups
@@ -328,6 +328,9 @@ class HipGoNet:
         self.head_dzb = torch.zeros((B, NUM_POINTS), dtype=torch.float32, device=dev)
 
         self.side = torch.cuda.Stream(device=dev) if self.side_mode != "none" else None
+        # DG_CHECK_STREAMS=1: every cross-stream hand-off bracketed by timing events, verified
+        # after each eager step (utils/streamcheck.py; check_streams())
+        self.sc = streamcheck.StreamCheck() if streamcheck.enabled() else None
         self._head_red_defer = False
         self._head_red_pending = False
         self._refresh_table = self._build_refresh_table()
@@ -1140,7 +1143,11 @@ class HipGoNet:
                 fill(self._inbufs[t], self._in_views[t])
                 ready = torch.cuda.Event()
                 ready.record(self.load_stream)
+            if self.sc:
+                self.sc.produce("load->compute", self.load_stream)
             main.wait_event(ready)
+            if self.sc:
+                self.sc.consume("load->compute", main)
             self.select_inputs(t)
         if not self._fp8_calibrated:
             self.calibrate_fp8()
@@ -1230,14 +1237,25 @@ class HipGoNet:
         elif self.side_mode == "bias":
             side = self.side
             l0_side = self._l0_side_at == i
+            sc = self.sc
             if i == 0 and self._l0_side_at is not None:
+                if sc:
+                    sc.produce("l0-chain->main", side)
                 main.wait_stream(side)           # layer 0's chain ran on the side stream
+                if sc:
+                    sc.consume("l0-chain->main", main)
             else:
+                if sc:
+                    sc.produce("dz->side", main)
                 side.wait_stream(main)           # dZ of the layer (group) final
+                if sc:
+                    sc.consume("dz->side", side)
                 self._flush_head_reduce(side.cuda_stream)
                 self._issue_loss_gate(side.cuda_stream)
                 self._run(ops[:1], side.cuda_stream)
                 ev = side.record_event()         # partials ready for the reduce
+                if sc:
+                    sc.produce("partials->reduce", side)
                 # then dZ_0 and the first layer's whole chain, joined at layer 0.  Measured
                 # (profiles/r3_l0_chain_stream_ab.txt): the chain before the partials, or on a
                 # third stream beside the grouped launch, is 5-6% slower at 12x128 and
@@ -1250,6 +1268,8 @@ class HipGoNet:
                     self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
                 self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
+                if sc:
+                    sc.consume("partials->reduce", main)
                 self._run(ops[2:3], main.cuda_stream)
                 if l0_side:
                     self._issue_early_update(main.cuda_stream)
@@ -1310,7 +1330,18 @@ class HipGoNet:
     def join_side(self):
         self._flush_head_reduce(stream_handle())
         if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
+            cur = torch.cuda.current_stream()
+            if self.sc:
+                self.sc.produce("side->join", self.side)
+            cur.wait_stream(self.side)
+            if self.sc:
+                self.sc.consume("side->join", cur)
+
+    def check_streams(self) -> int:
+        """DG_CHECK_STREAMS=1: synchronize and verify every cross-stream hand-off recorded
+        since the last check (raises on a violation); returns how many were checked (0 when
+        the mode is off or the step ran inside a graph capture)."""
+        return self.sc.check() if self.sc else 0
 
     def evaluate(self):
         s = stream_handle()
@@ -1570,6 +1601,8 @@ class SegmentedStep:
     def __init__(self, net: HipGoNet, bucketer=None, use_graphs: bool = True, warmup: int = 1):
         self.net = net
         self.bucketer = bucketer
+        if bucketer is not None and hasattr(bucketer, "sc"):
+            bucketer.sc = net.sc         # DG_CHECK_STREAMS: comm fork / join checked too
         fire_after = {}
         if bucketer is not None:
             for bi, (_, _, first_layer) in enumerate(bucketer.buckets):
@@ -1719,6 +1752,8 @@ class SegmentedStep:
             return
         if self.in_graph_comm:          # eager with the native communicator
             self._fb_in_stream()
+            if not self.use_graphs:
+                self.net.check_streams()
             return
         for si, (fns, fire) in enumerate(self.segments):
             with trace.range(f"segment{si}"):
@@ -1757,6 +1792,9 @@ class SegmentedStep:
                 self.net.optimizer_step()
             finally:
                 self.net.set_defer(False)
+            self.net.check_streams()
             return
         self.forward_backward()
         self.optimizer()
+        if not self.use_graphs:
+            self.net.check_streams()

@@ -146,6 +146,13 @@ class IpcOneShot:
     store (the default process group's, or ``store``).  A peer that never arrives does not
     hang the kernel: it gives up after ``timeout_s`` and ``error()`` turns non-zero.
 
+    A timed-out call writes NaN (not a sum of possibly stale peer buffers) over the shares it
+    could not complete, so the optimizer's finite gate skips that step, and ``error()``
+    reports it (the watchdog aborts on it).  The kernel's sequence counters assume its calls
+    are serialized: NativeComm issues every IPC call on ``self.stream`` (ordered after the
+    caller's stream and joined back).  Its ``blocks`` workgroups must all get scheduled for a
+    call to complete (csrc/comm/oneshot.hip: co-residency), so keep ``blocks`` small.
+
     Validated with two processes sharing one GPU (tests/test_ipc_gpu.py); the cross-GPU
     path over xGMI has not been measured by the builder (no multi-GPU box), so NativeComm
     routes small buckets here only when asked (``ipc_small_bytes`` / DG_IPC_SMALL)."""
@@ -259,11 +266,20 @@ class NativeComm:
         return {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float64: "fp64",
                 torch.int32: "i32", torch.int64: "i64", torch.float16: "fp16"}[t.dtype]
 
-    def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum"):
-        """In-place all-reduce of a contiguous tensor on ``stream`` (default: comm stream)."""
+    def all_reduce_(self, t: torch.Tensor, stream=None, op: str = "sum", use_ipc: bool = True):
+        """In-place all-reduce of a contiguous tensor on ``stream`` (default: comm stream).
+        Buckets the IPC one-shot takes run on ITS stream (every IPC call serialized there:
+        the kernel's sequence counters assume one call at a time), ordered after ``stream``
+        and joined back into it; ``use_ipc=False`` forces RCCL."""
         s = stream if stream is not None else self.stream
-        if self.ipc is not None and op == "sum" and self.ipc.fits(t):
-            return self.ipc.all_reduce_(t, stream=s)
+        if use_ipc and self.ipc is not None and op == "sum" and self.ipc.fits(t):
+            ist = self.ipc.stream
+            if s != ist:
+                ist.wait_stream(s)
+            self.ipc.all_reduce_(t, stream=ist)
+            if s != ist:
+                s.wait_stream(ist)
+            return t
         self.c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), op,
                           int(s.cuda_stream))
         return t
@@ -422,9 +438,12 @@ def selftest_in_graph(c: NativeComm, n: int = 4096):
     capturing stream (the step graph's structure), replay it twice, check the sums.  Every
     collective runs before any check raises, so all ranks issue the same sequence."""
     dev = c.device
+    # RCCL itself (use_ipc=False: a small test buffer would otherwise take the one-shot IPC
+    # path when DG_IPC_SMALL covers it, and the RCCL connection would go untested)
+    rccl = {"use_ipc": False} if getattr(c, "ipc", None) is not None else {}
     x = torch.empty(n, dtype=torch.float32, device=dev)
     x.fill_(float(c.rank + 1))
-    c.all_reduce_(x, stream=torch.cuda.current_stream(dev))   # eager: connects the comm
+    c.all_reduce_(x, stream=torch.cuda.current_stream(dev), **rccl)   # eager: connects it
     torch.cuda.synchronize(dev)
     want = float(c.world * (c.world + 1) // 2)
     eager_ok = bool((x == want).all())
@@ -433,7 +452,7 @@ def selftest_in_graph(c: NativeComm, n: int = 4096):
         cur = torch.cuda.current_stream(dev)
         x.fill_(float(c.rank + 1))
         c.stream.wait_stream(cur)
-        c.all_reduce_(x)
+        c.all_reduce_(x, **rccl)
         cur.wait_stream(c.stream)
         x.mul_(2.0)
     for _ in range(2):
@@ -473,6 +492,9 @@ class GradBucketer:
         self.works = []
         self._shadow = None
         self.direct = False          # all-reduce the model's own bf16 twin (no copies)
+        # DG_CHECK_STREAMS=1: the fork / join hand-offs with the comm stream are checked too
+        # (the model's checker when the step attaches it: SegmentedStep)
+        self.sc = None
         if grad_dtype == "bf16":
             if shadow is not None:
                 if shadow.dtype != torch.bfloat16 or shadow.numel() != grads.numel():
@@ -514,7 +536,12 @@ class GradBucketer:
     def enqueue(self, b: int):
         s, e, _ = self.buckets[b]
         cs = self.comm.stream
-        cs.wait_stream(torch.cuda.current_stream())     # bucket's gradients final
+        cur = torch.cuda.current_stream()
+        if self.sc:
+            self.sc.produce(f"bucket{b}->comm", cur)
+        cs.wait_stream(cur)                              # bucket's gradients final
+        if self.sc:
+            self.sc.consume(f"bucket{b}->comm", cs)
         with torch.cuda.stream(cs):
             if self._shadow is not None:
                 sh = self._shadow[s:e]
@@ -528,7 +555,12 @@ class GradBucketer:
                 self.comm.all_reduce_(self.grads[s:e])
 
     def join(self):
-        torch.cuda.current_stream().wait_stream(self.comm.stream)
+        cur = torch.cuda.current_stream()
+        if self.sc:
+            self.sc.produce("comm->join", self.comm.stream)
+        cur.wait_stream(self.comm.stream)
+        if self.sc:
+            self.sc.consume("comm->join", cur)
 
 
 BF16_UNIT_ROUNDOFF = 2.0 ** -8    # bf16: 8 significand bits, round to nearest even

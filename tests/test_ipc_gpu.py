@@ -2,8 +2,8 @@
 two processes sharing ONE GPU: IPC handles through a TCPStore, both ranks' staging buffers
 mapped into each other, rank-order fp32 sums compared bit-exactly with the same sums on the
 host (fp32 and bf16 buckets, several sizes, eager and captured in a hipGraph), and a peer
-that never arrives: the kernel gives up after its time limit and flags the error instead of
-hanging.  (The cross-GPU xGMI path is the same code; the builder has no multi-GPU box.)"""
+that never arrives: the kernel gives up after its time limit, flags the error and writes NaN
+(not a stale sum) instead of hanging.  (The cross-GPU xGMI path is the same code; the builder has no multi-GPU box.)"""
 import multiprocessing as mp
 import socket
 
@@ -44,6 +44,7 @@ def _worker(rank, world, port, mode, q):
                 c.all_reduce_(x, stream=torch.cuda.current_stream())
                 torch.cuda.synchronize()
                 out["error"] = c.error()
+                out["nan"] = bool(torch.isnan(x).all().item())
                 store.set("done", "1")
             else:
                 store.wait(["done"])
@@ -112,3 +113,6 @@ def test_ipc_oneshot_missing_peer_times_out_instead_of_hanging():
     res = _run("absent")
     assert "exc" not in res[0] and "exc" not in res[1], res
     assert res[0]["error"] == 1
+    # the timed-out call left NaN (the optimizer's finite gate skips that step), not a sum
+    # of a peer's stale staging buffer
+    assert res[0]["nan"] is True

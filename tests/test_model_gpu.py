@@ -997,3 +997,39 @@ def test_dropped_frames_and_operand_copies_over_many_steps(dtype, ch):
         torch.cuda.synchronize()
         assert torch.equal(net0.loss, net1.loss), k
         assert torch.equal(net0.params, net1.params), k
+
+
+@pytest.mark.parametrize("args", [["--channels", "128", "--dtype", "bf16"],
+                                  ["--channels", "128", "--dtype", "fp8"],
+                                  ["--channels", "128", "--dtype", "bf16", "--dp"]])
+def test_stream_handoffs_checked_and_serialized_run_bit_identical(args, tmp_path):
+    """SURVEY §5.2's stream/event discipline.  Three eager runs of the
+    fused training step in fresh processes (tools/stream_check_run.py): (1) with
+    DG_CHECK_STREAMS=1 — every cross-stream hand-off (dZ -> side stream, bias partials ->
+    slab reduce / early update, the first layer's chain -> main, side join, DP bucket fork to
+    the comm stream and its join) bracketed by timing events and verified after each step;
+    (2) under AMD_SERIALIZE_KERNEL=3 (the HIP runtime serializes every kernel: no two streams
+    overlap); (3) plainly.  The parameters after 3 steps and the last losses must be bit for
+    bit identical: nothing in the step depends on how its streams interleave.  The fp8 case
+    takes the early update (hidden layers updated beside the first layer's chain); --dp the
+    native RCCL communicator's in-graph buckets at world 1."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for name, env in (("check", {"DG_CHECK_STREAMS": "1"}),
+                      ("serial", {"AMD_SERIALIZE_KERNEL": "3"}), ("plain", {})):
+        out = str(tmp_path / f"{name}.pt")
+        e = dict(os.environ)
+        e.pop("DG_CHECK_STREAMS", None)
+        e.pop("AMD_SERIALIZE_KERNEL", None)
+        e.update(env)
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "stream_check_run.py"),
+                            out, *args], env=e, capture_output=True, text=True, timeout=100)
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        outs[name] = torch.load(out, weights_only=True)
+    assert outs["check"]["checked"] >= 3 * (4 if "--dp" not in args else 6), outs["check"]
+    assert outs["plain"]["checked"] == 0
+    for name in ("check", "serial"):
+        assert torch.equal(outs[name]["params"], outs["plain"]["params"]), name
+        assert torch.equal(outs[name]["loss"], outs["plain"]["loss"]), name
