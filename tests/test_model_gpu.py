@@ -1013,6 +1013,7 @@ def test_stream_handoffs_checked_and_serialized_run_bit_identical(args, tmp_path
     bit identical: nothing in the step depends on how its streams interleave.  The fp8 case
     takes the early update (hidden layers updated beside the first layer's chain); --dp the
     native RCCL communicator's in-graph buckets at world 1."""
+    import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
