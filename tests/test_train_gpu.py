@@ -141,7 +141,7 @@ def test_bf16_gradient_wire_world8_memorisation_curve(tmp_path):
     """The data-parallel bf16 gradient wire at WORLD 8, emulated on one GPU, against the fp32
     wire, in a regime with a real learning signal.  Every step's global
     batch of 64 (cycling a 256-position subset of the real fixture: memorisation; 12x128, rate
-    0.07, no head ReLU) is split into 8 rank shards of 8 boards; each shard's backward runs on
+    0.07, no head ReLU, 1200 steps) is split into 8 rank shards of 8 boards; each shard's backward runs on
     the HIP executor with the global-batch gradient scale, exactly as a rank would.  The bf16
     arm takes each shard's bf16 twin (what the gradient pass 2 writes) and sums them with a
     ring all-reduce's per-hop bf16 rounding (parallel.dp.ring_allreduce_emulate: 7 roundings
@@ -155,7 +155,7 @@ def test_bf16_gradient_wire_world8_memorisation_curve(tmp_path):
     from deep_go_amd.data.loader import BatchLoader
     from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep
     from deep_go_amd.parallel import dp
-    B, R, N, W = 64, 8, 600, 100
+    B, R, N, W = 64, 8, 1200, 100
     pk = PackedDataset.load(os.path.join(FIXTURE, "train.dgpack.npz"))
     ld = BatchLoader(pk, B, threads=2, prefetch=4, seed=9, pin=False)
     subset = [[np.asarray(x) for x in ld.next_numpy()] for _ in range(256 // B)]
