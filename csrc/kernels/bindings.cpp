@@ -48,6 +48,7 @@ hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X
 hipError_t dg_conv_stack2_dgrad_sig(const long long* table, int nl, const void* X0, int B,
                                     unsigned* sig, hipStream_t stream);
 int dg_bias_follow_tasks(int nl, int B, int C);
+void dg_bias_follow_set_variant(int aux, int sleep);
 hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned* sig, int nsig,
                           unsigned* done, int mode, int grid, double timeout_us,
                           hipStream_t s);
@@ -319,6 +320,8 @@ PYBIND11_MODULE(_dghip, m) {
   }, "conv_stack2 backward-data chain storing each row write-through and counting it in sig[row] "
      "(the bias-gradient follower's arrival counters)");
   m.def("bias_follow_tasks", [](int nl, int B, int C) { return dg_bias_follow_tasks(nl, B, C); });
+  m.def("bias_follow_set_variant", [](int aux, int sleep) { dg_bias_follow_set_variant(aux, sleep); },
+        "kbench A/B: the follower's dZ load cache policy (0 / 2 nt / 16 sc1) and poll interval");
   m.def("bias_follow", [](uintptr_t table, int nl, int B, int C, uintptr_t sig, int nsig,
                           uintptr_t done, int mode, int grid, double timeout_us,
                           uintptr_t stream) {

@@ -198,6 +198,7 @@ struct BiasFollowArgs {
   int nsig;
   unsigned* done;             // [nl * tasks per layer]
   long long timeout_ticks;    // follow pass: per-wait limit (s_memrealtime, 100 MHz)
+  int sleep;                  // follow pass: poll interval in s_sleep(16) units (~0.45 us)
 };
 
 __host__ __device__ inline int bf_tasks_per_layer(int nchunks, int C) {
@@ -208,6 +209,7 @@ __host__ __device__ inline int bf_tasks_per_layer(int nchunks, int C) {
 // stack: lane values are recomputed from threadIdx each pass, global traffic goes through
 // buffer resources (uniform bases in SGPRs, one VGPR offset per lane).
 typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+template <int AUX>
 DG_DEV void bias_follow_task(const BiasFollowArgs& a, int l, int t, f32x4* s_comb,
                              float* s_row) {
   const int nq = a.C / BF_CQ;
@@ -238,7 +240,7 @@ DG_DEV void bias_follow_task(const BiasFollowArgs& a, int l, int t, f32x4* s_com
       u32x2v v[BF_SUB];
 #pragma unroll
       for (int i = 0; i < BF_SUB; ++i)
-        v[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, i * bstride, 0);
+        v[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, i * bstride, AUX);
       // one board at a time (sched barriers): unpacked all at once the 8 loads' halves need
       // 32 more VGPRs than the budget beside the stack
 #pragma unroll
@@ -277,7 +279,7 @@ DG_DEV void bias_follow_task(const BiasFollowArgs& a, int l, int t, f32x4* s_com
 }
 
 // mode 0: follow pass (beside the stack); 1: finish pass
-template <int MODE>
+template <int MODE, int AUX>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16)))
 bias_follow_kernel(BiasFollowArgs a) {
   __shared__ f32x4 s_comb[2 * BF_SUB * 32];
@@ -297,7 +299,7 @@ bias_follow_kernel(BiasFollowArgs a) {
           const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
           while (__hip_atomic_load(a.sig + ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                  (unsigned)a.B) {
-            __builtin_amdgcn_s_sleep(8);
+            for (int z = 0; z < a.sleep; ++z) __builtin_amdgcn_s_sleep(16);
             if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
               ok = 0;
               break;
@@ -310,11 +312,11 @@ bias_follow_kernel(BiasFollowArgs a) {
         __syncthreads();
         if (!s_ok) return;   // not ready in time: the finish pass takes the rest
       }
-      bias_follow_task(a, l, t, s_comb, s_row);
+      bias_follow_task<AUX>(a, l, t, s_comb, s_row);
       if (tid == 0) a.done[g] = 1u;
     } else {
       const unsigned d = a.done[g];   // (uniform: every thread reads the same word)
-      if (!d) bias_follow_task(a, l, t, s_comb, s_row);
+      if (!d) bias_follow_task<AUX>(a, l, t, s_comb, s_row);
       __syncthreads();                // every thread read the flag before it is reset
       if (tid == 0 && d) a.done[g] = 0u;
     }
@@ -1094,6 +1096,8 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
 // pass (grid = one workgroup per CU, launched beside the stack; timeout_us bounds each wait);
 // mode 1: the finish pass (after the stack).  done: >= dg_bias_follow_tasks(nl, B, C) zeroed
 // words; sig: the stack's nsig counters.
+int g_bf_aux = 0;     // load cache policy of the follower's dZ stream
+int g_bf_sleep = 4;   // poll interval (s_sleep(16) units)
 int dg_bias_follow_tasks(int nl, int B, int C) {
   return nl * bf_tasks_per_layer((B + BG_BT_MULTI - 1) / BG_BT_MULTI, C);
 }
@@ -1118,11 +1122,25 @@ hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned
   a.nsig = nsig;
   a.done = done;
   a.timeout_ticks = (long long)(timeout_us * 100.0);
-  if (mode == 0)
-    hipLaunchKernelGGL(bias_follow_kernel<0>, dim3(grid), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(bias_follow_kernel<1>, dim3(grid), dim3(256), 0, s, a);
+  a.sleep = g_bf_sleep;
+  // load cache policy of the dZ stream (kbench A/B: tools/kbench_follow.py): 0 default,
+  // 2 nt, 16 sc1
+#define BF_LAUNCH(M, X) hipLaunchKernelGGL((bias_follow_kernel<M, X>), dim3(grid), dim3(256), 0, s, a)
+  if (mode == 0) {
+    if (g_bf_aux == 2) BF_LAUNCH(0, 2);
+    else if (g_bf_aux == 16) BF_LAUNCH(0, 16);
+    else BF_LAUNCH(0, 0);
+  } else {
+    if (g_bf_aux == 2) BF_LAUNCH(1, 2);
+    else if (g_bf_aux == 16) BF_LAUNCH(1, 16);
+    else BF_LAUNCH(1, 0);
+  }
+#undef BF_LAUNCH
   return hipGetLastError();
+}
+void dg_bias_follow_set_variant(int aux, int sleep) {
+  g_bf_aux = aux;
+  g_bf_sleep = sleep < 1 ? 1 : sleep;
 }
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
 int dg_bias_chunks_multi(int B) { return (B + BG_BT_MULTI - 1) / BG_BT_MULTI; }

@@ -331,6 +331,9 @@ class HipGoNet:
         # DG_CHECK_STREAMS=1: every cross-stream hand-off bracketed by timing events, verified
         # after each eager step (utils/streamcheck.py; check_streams())
         self.sc = streamcheck.StreamCheck() if streamcheck.enabled() else None
+        # the first layer's 5x5 weight gradient on the main stream before the window launch
+        # (DG_L0_WGRAD_MAIN=1) instead of on the side stream after the bias partials
+        self._l0_main = os.environ.get("DG_L0_WGRAD_MAIN", "0") == "1"
         self._head_red_defer = False
         self._head_red_pending = False
         self._refresh_table = self._build_refresh_table()
@@ -873,7 +876,7 @@ class HipGoNet:
         computes every task; tests compare it bit for bit with the follower)."""
         self._bf_follow = None
         self._bf_finish = None
-        mode = os.environ.get("DG_BIAS_FOLLOW", "1")
+        mode = os.environ.get("DG_BIAS_FOLLOW", "0")
         h = self.h
         if (mode == "0" or self.dstack_fp8 or self.side_mode != "bias" or len(self.wgroups) != 1
                 or not hasattr(h, "bias_follow")):
@@ -1343,7 +1346,23 @@ class HipGoNet:
                 # gradient then starts ~50 us earlier beside it) stretched the fp8 window
                 # kernel by 100 us: -6% at 12x256 fp8, 0 elsewhere
                 # (profiles/r4_s1_l0_bias_main_ab.txt)
-                if l0_side:
+                if l0_side and self._l0_main and not self._l0_dgrad:
+                    # the first layer's 5x5 weight gradient ALONE on the main stream, right
+                    # before the window launch (beside the window kernel it cannot co-reside
+                    # with its two workgroups per CU and ran stretched after it); its bias
+                    # partial (a launch of its own at d = 256) and slab reduce stay on the side
+                    # stream, the reduce after the partials
+                    l0 = self._layer_ops(0)[:3]
+                    self._run(l0[:1], side.cuda_stream)
+                    self._run(l0[1:2], main.cuda_stream)
+                    ev5 = main.record_event()
+                    if sc:
+                        sc.produce("l0-wgrad->reduce", main)
+                    side.wait_event(ev5)
+                    if sc:
+                        sc.consume("l0-wgrad->reduce", side)
+                    self._run(l0[2:3], side.cuda_stream)
+                elif l0_side:
                     self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
                 self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)

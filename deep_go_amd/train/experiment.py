@@ -17,6 +17,7 @@ Reference map:
 """
 from __future__ import annotations
 
+import collections
 import os
 import time
 from typing import Dict, List, Optional
@@ -108,6 +109,24 @@ class Experiment:
                            prefetch=c.prefetch, seed=c.seed * 1000003 + self.info.rank,
                            sampling=c.sampling, start_seq=self.loader_seq)
 
+    def _regenerate_batch(self, seq):
+        """The training batch the loader produced at sequence number ``seq`` (the loader is
+        deterministic per (seed, rank, sequence): a fresh one started at ``seq`` yields the
+        same batch), or None."""
+        if seq is None:
+            return None
+        try:
+            c = self.cfg
+            ld = BatchLoader(self.sources["train"], self.local_batch, threads=1, prefetch=2,
+                             seed=c.seed * 1000003 + self.info.rank, sampling=c.sampling,
+                             start_seq=seq, pin=False)
+            try:
+                return ld.next_numpy()
+            finally:
+                ld.close()
+        except Exception:  # noqa: BLE001  (the dump is best effort; the raise is what matters)
+            return None
+
     # ------------------------------------------------------------------ validation
     def draw_validation(self, n: int, split: str = "validation", seed_offset: int = 0):
         src = self.sources.get(split) or self._source(split)
@@ -176,6 +195,10 @@ class Experiment:
         ema = self.train_costs[-1] if self.train_costs else None
         skipguard = (SkipGuard(cfg.nan_max_skips, be.bad_steps())
                      if cfg.nan_policy == "guard" else None)
+        # guard: the loader sequence number of each recent step's batch, so the batch dumped
+        # when SkipGuard raises is the FIRST of the skipped run (regenerated from the
+        # deterministic loader), not the batch of the step whose check noticed it
+        seq_ring = collections.deque(maxlen=cfg.nan_max_skips + 2 * cfg.log_interval + 2)
         t_start = time.perf_counter()
         t_log = t_start
         n_log = 0
@@ -183,10 +206,12 @@ class Experiment:
         save_now = False
         try:
             for _ in range(iters):
+                seq0 = loader.consumed
                 with trace.range("load_batch"):
                     batch = be.load_next(loader)
                 self.loader_seq = loader.consumed
                 step = self.iterations + 1
+                seq_ring.append((step, seq0))
                 # nothing reads the pre-update state this iteration (no validation, no host NaN
                 # check before the update): forward/backward + update as one fused step
                 fused = (step % cfg.validation_interval != 0 and cfg.nan_policy != "raise"
@@ -246,8 +271,12 @@ class Experiment:
                         try:
                             skipguard.check(be.bad_steps(), step)
                         except NonFiniteLoss:
-                            dump_batch(batch if batch is not None else be.current_batch(),
-                                       step, cfg.checkpoint_dir)
+                            first = step - skipguard.run + 1
+                            b = self._regenerate_batch(dict(seq_ring).get(first))
+                            if b is None:
+                                first = step
+                                b = batch if batch is not None else be.current_batch()
+                            dump_batch(b, first, cfg.checkpoint_dir)
                             raise
                 if save_now:
                     with trace.range("checkpoint"):

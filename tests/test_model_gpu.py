@@ -89,7 +89,11 @@ def test_model_matches_bf16_storage_oracle(layers, ch, B):
     differ in order), so a few ReLU gates near zero flip and the difference compounds down the
     backward: measured max per-tensor gradient error 6.4% (12x128, since the first layer also
     reads the bf16 bias table: the same flips, different ones) / 4.7% (12x256), 0.17% at 4
-    layers.  The per-layer, depth-independent bound is test_layerwise_teacher_forced."""
+    layers.  Those flips depend on the summation order of both sides, so a benign reorder of
+    a kernel's reduction moves the worst tensor's error: at 12 layers the bound is set by the
+    measured spread (0.15, over 2x the 6.4% measured), with the MEDIAN tensor error held
+    tight (2e-2: a systematic bug moves every tensor), and at 4 layers (no compounding) 1e-2.
+    The per-layer, depth-independent bound is test_layerwise_teacher_forced."""
     cfg, net, data = _setup(layers, ch, B, seed=4)
     net.forward_backward()
     torch.cuda.synchronize()
@@ -107,7 +111,8 @@ def test_model_matches_bf16_storage_oracle(layers, ch, B):
     os.makedirs("gpurun_out", exist_ok=True)
     with open(f"gpurun_out/oracle_errs_{layers}x{ch}.json", "w") as f:
         json.dump(errs, f, indent=0)
-    assert errs[worst] < 7e-2, errs
+    assert errs[worst] < (1e-2 if layers <= 4 else 0.15), errs
+    assert float(np.median(list(errs.values()))) < 2e-2, errs
 
 
 def _interior(frame, pad):

@@ -313,4 +313,18 @@ def test_guard_policy_skips_then_raises_with_dump(tmp_path, ref_data):
     with pytest.raises(NonFiniteLoss, match="consecutive"):
         e.run(40)
     assert e.backend.bad_steps() >= 8
-    assert any(f.startswith("bad_batch_") for f in os.listdir(tmp_path))
+    dumps = [f for f in os.listdir(tmp_path) if f.startswith("bad_batch_")]
+    assert len(dumps) == 1
+    # the dump is the FIRST batch of the skipped run (regenerated from the deterministic
+    # loader), not the batch of the step whose check raised
+    first = int(dumps[0][len("bad_batch_"):-len(".npz")])
+    assert first <= e.iterations - 7, (first, e.iterations)
+    from deep_go_amd.data.loader import BatchLoader
+    z = np.load(os.path.join(tmp_path, dumps[0]))
+    ld = BatchLoader(e.sources["train"], e.local_batch, threads=1, prefetch=2,
+                     seed=cfg.seed * 1000003, sampling=cfg.sampling, start_seq=first - 1,
+                     pin=False)
+    want = ld.next_numpy()
+    ld.close()
+    for k, w in enumerate(want):
+        assert np.array_equal(z[f"arr_{k}"], np.asarray(w))
