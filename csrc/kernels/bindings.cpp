@@ -35,7 +35,7 @@ hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, cons
                             const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
                             const long long* sr_step, hipStream_t stream);
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
-                              int KP, int splits, hipStream_t stream);
+                              int KP, int splits, long long* sf, hipStream_t stream);
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
 hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
@@ -50,7 +50,7 @@ hipError_t dg_conv_stack2_dgrad_sig(const long long* table, int nl, const void* 
 int dg_bias_follow_tasks(int nl, int B, int C);
 void dg_bias_follow_set_variant(int aux, int sleep);
 hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned* sig, int nsig,
-                          unsigned* done, int mode, int grid, double timeout_us,
+                          unsigned* done, int mode, int grid, double timeout_us, long long* sf,
                           hipStream_t s);
 hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int l1, int B,
                                    const float* w, const float* bias, const float* posb,
@@ -94,7 +94,7 @@ hipError_t dg_conv_layer2_multi_head(const long long* table, int nl, int B, cons
 hipError_t dg_conv_layer2_multi(int epi, const long long* table, int nl, int C, int B,
                                 hipStream_t stream);
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
-                             int KP, int splits, hipStream_t stream);
+                             int KP, int splits, long long* sf, hipStream_t stream);
 hipError_t dg_conv_board_fp8(int kw, int bm, const void* A8, int KP, int M, int Mpad,
                              const void* X8, int x_pad, int x_C, int B, void* Y, void* Y8,
                              int y_pad, const float* bias, const float* posb, const float* s_x,
@@ -112,14 +112,14 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
                          hipStream_t stream);
 hipError_t dg_wgrad_reduce_multi(const long long* table, int nl, int cols, hipStream_t stream);
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
-                                      hipStream_t s);
+                                      long long* sf, hipStream_t s);
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
                            float* gposb, float* gbias, void* out16, void* gposb16,
-                           void* gbias16, hipStream_t stream);
+                           void* gbias16, long long* sf, hipStream_t stream);
 hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n, float* gw,
                           float* gbias, float* gposb, void* gw16, void* gbias16, void* gposb16,
-                          hipStream_t stream);
+                          long long* sf, hipStream_t stream);
 hipError_t dg_head(int kw, const void* X, int x_pad, int C, int B, const float* w,
                    const float* bias, const float* posb, const int* labels, float* loss,
                    int* pred, float* logp_out, void* dZ, int dz_pad, float* gw_part,
@@ -148,7 +148,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
                           long long* step, unsigned* tickets, int* bad_steps, int write_grads, int final,
-                          hipStream_t s);
+                          const long long* gflag, hipStream_t s);
 }
 
 namespace {
@@ -269,8 +269,9 @@ PYBIND11_MODULE(_dghip, m) {
      "none) and stochastic rounding seeded by the int64 device step counter sr_step (0: "
      "round to nearest even)");
   m.def("conv_wgrad_win8", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
-                              int splits, uintptr_t stream) {
-    check(dg_conv_wgrad_win8(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
+                              int splits, uintptr_t sf, uintptr_t stream) {
+    check(dg_conv_wgrad_win8(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits,
+                             P<long long>(sf), S(stream)),
           "conv_wgrad_win8");
   }, "MX-fp8 sliding-window weight gradients: table rows {dZ8 (e5m2), X8 (e4m3), slab, s_dz, "
      "s_x} (448-row fp8 frames)");
@@ -323,10 +324,10 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("bias_follow_set_variant", [](int aux, int sleep) { dg_bias_follow_set_variant(aux, sleep); },
         "kbench A/B: the follower's dZ load cache policy (0 / 2 nt / 16 sc1) and poll interval");
   m.def("bias_follow", [](uintptr_t table, int nl, int B, int C, uintptr_t sig, int nsig,
-                          uintptr_t done, int mode, int grid, double timeout_us,
+                          uintptr_t done, int mode, int grid, double timeout_us, uintptr_t sf,
                           uintptr_t stream) {
     check(dg_bias_follow(P<long long>(table), nl, B, C, P<unsigned>(sig), nsig,
-                         P<unsigned>(done), mode, grid, timeout_us, S(stream)),
+                         P<unsigned>(done), mode, grid, timeout_us, P<long long>(sf), S(stream)),
           "bias_follow");
   }, "bias-gradient partials beside the backward-data stack: mode 0 follow pass, 1 finish pass; "
      "table rows {dZ, part, ready row (-1: ready)}");
@@ -377,39 +378,42 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_wgrad_reduce_multi(P<long long>(table), nl, 16, S(stream)), "wgrad_reduce_multi_w");
   }, "wgrad_reduce_multi writing bf16 twins too: rows + {out16, gposb16, gbias16}");
   m.def("bias_grad_partial_multi", [](uintptr_t table, int nl, int B, int C, int pad,
-                                      uintptr_t stream) {
-    check(dg_bias_grad_partial_multi(P<long long>(table), nl, B, C, pad, S(stream)),
+                                      uintptr_t sf, uintptr_t stream) {
+    check(dg_bias_grad_partial_multi(P<long long>(table), nl, B, C, pad, P<long long>(sf),
+                                     S(stream)),
           "bias_grad_partial_multi");
   });
   m.def("wgrad_reduce", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
-                           uintptr_t gposb, uintptr_t gbias, uintptr_t stream) {
+                           uintptr_t gposb, uintptr_t gbias, uintptr_t sf, uintptr_t stream) {
     check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
                           P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias), nullptr,
-                          nullptr, nullptr, S(stream)),
+                          nullptr, nullptr, P<long long>(sf), S(stream)),
           "wgrad_reduce");
   });
   m.def("wgrad_reduce_w", [](uintptr_t slab, uintptr_t out, int splits, int M, int Mpad, int KP,
                              int taps, int cin, int cinp, uintptr_t bpart, int bchunks,
                              uintptr_t gposb, uintptr_t gbias, uintptr_t out16,
-                             uintptr_t gposb16, uintptr_t gbias16, uintptr_t stream) {
+                             uintptr_t gposb16, uintptr_t gbias16, uintptr_t sf,
+                             uintptr_t stream) {
     check(dg_wgrad_reduce(P<float>(slab), P<float>(out), splits, M, Mpad, KP, taps, cin, cinp,
                           P<float>(bpart), bchunks, P<float>(gposb), P<float>(gbias),
-                          P<void>(out16), P<void>(gposb16), P<void>(gbias16), S(stream)),
+                          P<void>(out16), P<void>(gposb16), P<void>(gbias16), P<long long>(sf),
+                          S(stream)),
           "wgrad_reduce_w");
   }, "wgrad_reduce writing bf16 twins of the weight / position-bias / bias gradients too");
   m.def("head_reduce", [](uintptr_t dzb, uintptr_t gw_part, int B, int n, uintptr_t gw,
-                          uintptr_t gbias, uintptr_t gposb, uintptr_t stream) {
+                          uintptr_t gbias, uintptr_t gposb, uintptr_t sf, uintptr_t stream) {
     check(dg_head_reduce(P<float>(dzb), P<float>(gw_part), B, n, P<float>(gw), P<float>(gbias),
-                         P<float>(gposb), nullptr, nullptr, nullptr, S(stream)),
+                         P<float>(gposb), nullptr, nullptr, nullptr, P<long long>(sf), S(stream)),
           "head_reduce");
   });
   m.def("head_reduce_w", [](uintptr_t dzb, uintptr_t gw_part, int B, int n, uintptr_t gw,
                             uintptr_t gbias, uintptr_t gposb, uintptr_t gw16, uintptr_t gbias16,
-                            uintptr_t gposb16, uintptr_t stream) {
+                            uintptr_t gposb16, uintptr_t sf, uintptr_t stream) {
     check(dg_head_reduce(P<float>(dzb), P<float>(gw_part), B, n, P<float>(gw), P<float>(gbias),
                          P<float>(gposb), P<void>(gw16), P<void>(gbias16), P<void>(gposb16),
-                         S(stream)),
+                         P<long long>(sf), S(stream)),
           "head_reduce_w");
   }, "head_reduce writing bf16 twins too");
   m.def("head", [](int kw, uintptr_t X, int x_pad, int C, int B, uintptr_t w, uintptr_t bias,
@@ -494,11 +498,11 @@ PYBIND11_MODULE(_dghip, m) {
                           uintptr_t p, uintptr_t g, uintptr_t g16, uintptr_t ms, float rms_decay,
                           float gscale, uintptr_t gate, uintptr_t lr, double decay,
                           uintptr_t step, uintptr_t tickets, uintptr_t bad, int write_grads,
-                          int final, uintptr_t stream) {
+                          int final, uintptr_t gflag, uintptr_t stream) {
     check(dg_grad_update(P<long long>(table), n, plain_off, plain_n, P<float>(p), P<float>(g),
                          P<void>(g16), P<float>(ms), rms_decay, gscale, P<float>(gate),
                          P<double>(lr), decay, P<long long>(step), P<unsigned>(tickets),
-                         P<int>(bad), write_grads, final, S(stream)),
+                         P<int>(bad), write_grads, final, P<long long>(gflag), S(stream)),
           "grad_update");
   }, "fused gradient pass 2 (slabs / bias partials, or the flat gradient) + SGD / RMSProp + "
      "operand refresh + LR decay (elementwise.hip grad_update_kernel)");
@@ -562,8 +566,9 @@ PYBIND11_MODULE(_dghip, m) {
   }, "a run of nl conv_layer2 layers in one launch (one workgroup per board, the layers "
      "chained through the board's own L2-resident output); table rows {A, pbias, X, Y, mask}");
   m.def("conv_wgrad_win", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
-                             int splits, uintptr_t stream) {
-    check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits, S(stream)),
+                             int splits, uintptr_t sf, uintptr_t stream) {
+    check(dg_conv_wgrad_win(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits,
+                            P<long long>(sf), S(stream)),
           "conv_wgrad_win");
   }, "sliding-window 3x3 weight gradients (frame-linear K, 9 taps per staged X window)");
   m.def("conv_wgrad_win_splits", [](int nl, int M, int Cx, int B, int num_cus) {

@@ -656,6 +656,7 @@ struct ReduceLayers {  // blockIdx.y = layer (several layers, each with its own 
   bf16_t* gbias16[RD_MAXL];
   int splits[RD_MAXL], M[RD_MAXL], Mpad[RD_MAXL], KP[RD_MAXL], taps[RD_MAXL], cin[RD_MAXL],
       cinp[RD_MAXL], bchunks[RD_MAXL], main_blocks[RD_MAXL];
+  long long* sf;   // the fused update's step tag (dg_common.h): an output out of range sets it
 };
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
   const int ly = blockIdx.y;
@@ -679,6 +680,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
       if (threadIdx.x == 0) {
         gbias[c] = v;
         if (Ls.gbias16[ly]) Ls.gbias16[ly][c] = f2bf(v);
+        if (Ls.sf && grad_out_of_range(v)) flag_bad_step(Ls.sf);
       }
     }
     return;
@@ -692,6 +694,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
       const float v = chunk_sum(bpart + j, bchunks, (size_t)np);
       gposb[j] = v;
       if (Ls.gposb16[ly]) Ls.gposb16[ly][j] = f2bf(v);
+      if (Ls.sf && grad_out_of_range(v)) flag_bad_step(Ls.sf);
     }
     return;
   }
@@ -714,6 +717,9 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(ReduceLayers Ls) {
         if (Ls.out16[ly]) Ls.out16[ly][o] = f2bf(s[e]);
       }
     }
+    if (Ls.sf && (grad_out_of_range(s[0]) || grad_out_of_range(s[1]) ||
+                  grad_out_of_range(s[2]) || grad_out_of_range(s[3])))
+      flag_bad_step(Ls.sf);
   }
 }
 
@@ -954,8 +960,9 @@ static int reduce_grid_x(const ReduceLayers& Ls, int i) {
 hipError_t dg_wgrad_reduce(const float* slab, float* out, int splits, int M, int Mpad, int KP,
                            int taps, int cin, int cinp, const float* bpart, int bchunks,
                            float* gposb, float* gbias, void* out16, void* gposb16, void* gbias16,
-                           hipStream_t stream) {
+                           long long* sf, hipStream_t stream) {
   ReduceLayers Ls{};
+  Ls.sf = sf;
   reduce_layer(Ls, 0, slab, out, bpart, gposb, gbias, splits, M, Mpad, KP, taps, cin, cinp,
                bchunks);
   Ls.out16[0] = (bf16_t*)out16;

@@ -43,6 +43,7 @@ struct WinLayers {
 };
 
 struct WinArgs {
+  long long* sf;  // the fused update's step tag (dg_common.h): a slab value out of range sets it
   int M;       // dZ channels (co), multiple of 128
   int Mpad;    // slab rows
   int Cx;      // X channels (ci), multiple of 64
@@ -286,6 +287,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv_wgrad_win_kernel(WinArgs
       }
     }
   }
+  if (a.sf) {
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bad |= grad_out_of_range(acc[i][t][r]);
+    if (bad) flag_bad_step(a.sf);
+  }
 }
 
 int g_win_ablate = 0;
@@ -316,7 +327,7 @@ int dg_conv_wgrad_win_splits(int nl, int M, int Cx, int B, int num_cus) {
 
 // table = nl rows of {dZ frame (pad 1, M channels), X frame (pad 1, Cx channels), slab}.
 hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, int Cx, int B,
-                             int KP, int splits, hipStream_t stream) {
+                             int KP, int splits, long long* sf, hipStream_t stream) {
   const int coch = 16 * WIN_NW;
   if (nl <= 0 || nl > MAXL || M % coch != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || splits <= 0 || splits > B * STEPS_PER_BOARD)
@@ -328,7 +339,7 @@ hipError_t dg_conv_wgrad_win(const long long* table, int nl, int M, int Mpad, in
     Ls.slab[i] = (float*)table[3 * i + 2];
     if (!Ls.dZ[i] || !Ls.X[i] || !Ls.slab[i]) return hipErrorInvalidValue;
   }
-  WinArgs a{M, Mpad, Cx, KP, B, splits, nl};
+  WinArgs a{sf, M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / coch) * (Cx / 64) * splits);
   // d >= 256: s_setprio 1 around each tap's MFMAs (ABL bit 32).  This kernel is the step's
   // critical path there and the side stream's bias partials / 5x5 weight gradient share its

@@ -77,6 +77,7 @@ struct Win8Layers {
 };
 
 struct Win8Args {
+  long long* sf;   // the fused update's step tag (dg_common.h)
   int M, Mpad, Cx, KP, B, splits, nl;
 };
 
@@ -285,6 +286,16 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
       }
     }
   }
+  if (a.sf) {
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bad |= grad_out_of_range(acc[i][t][r] * scale);
+    if (bad) flag_bad_step(a.sf);
+  }
 }
 
 }  // namespace
@@ -317,7 +328,7 @@ int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
 // table = nl rows of {dZ8 frame (pad 1, M channels, e5m2), X8 frame (pad 1, Cx channels,
 // e4m3), slab, s_dz, s_x} (int64)
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
-                              int KP, int splits, hipStream_t stream) {
+                              int KP, int splits, long long* sf, hipStream_t stream) {
   if (nl <= 0 || nl > MAXL || M % 64 != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || B % 4 != 0 || splits <= 0 || splits > B * SPB / 4)
     return hipErrorInvalidValue;
@@ -332,7 +343,7 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
     if (!Ls.dZ[i] || !Ls.X[i] || !Ls.slab[i] || !Ls.s_dz[i] || !Ls.s_x[i])
       return hipErrorInvalidValue;
   }
-  Win8Args a{M, Mpad, Cx, KP, B, splits, nl};
+  Win8Args a{sf, M, Mpad, Cx, KP, B, splits, nl};
   const dim3 grid(nl * (M / 64) * (Cx / 64) * splits);
   // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
   // the same — profiles/r3_fp8_wgrad_ab.txt)

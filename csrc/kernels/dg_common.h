@@ -188,6 +188,21 @@ DG_DEV float rows_sum4(const float* rowpart, int R, int C, int c, int q) {
   return s;
 }
 
+// ---- the fused update's all-or-nothing gate ----------------------------------------------
+// A training step whose gradient pass 2 is deferred into grad_update has no reduced gradient
+// to check before the parameters change.  So every producer of that pass's inputs (window
+// weight-gradient slabs, bias-gradient partials, the head / first-layer reduces) checks what
+// it writes (or, for the bias partials, every dZ value it reads) and tags the step when any
+// value is non-finite or |v| >= 2^120 (2^100 for dZ): sf[1] = sf[0] + 1, sf[0] being the
+// device step counter.  Those bounds keep every sum the deferred pass 2 forms finite (<= 64
+// split slabs, <= 16 bias chunks of <= 64 boards, a first-layer weight gradient over 92k
+// pixels of 0/1 inputs), so grad_update can skip the WHOLE step on the tag before writing any
+// parameter (HipGoNet._stepflag; the reference's pcall around the step, train.lua:106-111).
+constexpr float GRAD_BOUND = 0x1p120f;
+constexpr float DZ_BOUND = 0x1p100f;
+DG_DEV bool grad_out_of_range(float v) { return !(__builtin_fabsf(v) < GRAD_BOUND); }
+DG_DEV void flag_bad_step(long long* sf) { sf[1] = sf[0] + 1; }
+
 // Exact floor(n / d) for 0 <= n < 2^22 and 1 <= d <= 4096 via a 64-bit magic
 // m = floor(2^32 / d) + 1 (host computes it; checked exhaustively in tests/tools).
 DG_DEV uint32_t fastdiv(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }

@@ -65,6 +65,7 @@ struct BiasLayers {  // blockIdx.z = layer (several same-shape layers in one lau
   // 21x21 frame in rows 0..440) and *s8 its power-of-two scale — the bf16 frame it replaces
   // is exactly e5m2 x s8, so the partials are bit-identical (null: a bf16 frame)
   const float* s8[BG_MAXL];
+  long long* sf;   // the fused update's step tag (dg_common.h): a dZ value out of range sets it
 };
 constexpr int BG_FP8_ROWS = 448;
 // LD: 16-B loads in flight per thread.  The multi-layer launch runs beside the window weight
@@ -94,6 +95,8 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
   float* prow = part + ((size_t)chunk * NPTS + h * BOARD) * C;
   // blockDim covers all 19*C/8 items of the row in ONE pass (the 256-thread version ran a
   // second pass on 48 threads whose load latency the whole workgroup waited for)
+  float dzmax = 0.f;   // max |dZ| read (the step tag; NaN shows in the sums)
+  bool nonfinite = false;
   for (int it = tid; it < items; it += blockDim.x) {
     const int w = it / G, g = it - (it / G) * G;
     const char* src = row0 + ((size_t)w * C + g * 8) * esz;
@@ -117,6 +120,8 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
             acc[4 * e + 1] += lo[1] * s8;
             acc[4 * e + 2] += hi[0] * s8;
             acc[4 * e + 3] += hi[1] * s8;
+            dzmax = fmaxf(dzmax, fmaxf(fmaxf(fabsf(lo[0]), fabsf(lo[1])),
+                                       fmaxf(fabsf(hi[0]), fabsf(hi[1]))) * s8);
           }
         }
       }
@@ -135,10 +140,14 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
           for (int e = 0; e < 4; ++e) {
             acc[2 * e] += __uint_as_float(u[e] << 16);
             acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+            dzmax = fmaxf(dzmax, fmaxf(fabsf(__uint_as_float(u[e] << 16)),
+                                       fabsf(__uint_as_float(u[e] & 0xFFFF0000u))));
           }
         }
       }
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) nonfinite |= !__builtin_isfinite(acc[e]);
     f32x4* dst = (f32x4*)(prow + w * C + g * 8);
     dst[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
     dst[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -146,6 +155,7 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
 #pragma unroll
     for (int e = 0; e < 8; ++e) sr[e] = acc[e];
   }
+  if (Ls.sf && (nonfinite || !(dzmax < DZ_BOUND))) flag_bad_step(Ls.sf);
   __syncthreads();
   float* rowpart = part + (size_t)nchunks * NPTS * C + ((size_t)chunk * BOARD + h) * C;
   for (int c = tid; c < C; c += blockDim.x) {
@@ -199,6 +209,7 @@ struct BiasFollowArgs {
   unsigned* done;             // [nl * tasks per layer]
   long long timeout_ticks;    // follow pass: per-wait limit (s_memrealtime, 100 MHz)
   int sleep;                  // follow pass: poll interval in s_sleep(16) units (~0.45 us)
+  long long* sf;              // the fused update's step tag (dg_common.h)
 };
 
 __host__ __device__ inline int bf_tasks_per_layer(int nchunks, int C) {
@@ -243,14 +254,21 @@ DG_DEV void bias_follow_task(const BiasFollowArgs& a, int l, int t, f32x4* s_com
         v[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, i * bstride, AUX);
       // one board at a time (sched barriers): unpacked all at once the 8 loads' halves need
       // 32 more VGPRs than the budget beside the stack
+      float m = 0.f;
 #pragma unroll
       for (int i = 0; i < BF_SUB; ++i) {
         __builtin_amdgcn_sched_barrier(0);
-        acc[0] += __uint_as_float(v[i].x << 16);
-        acc[1] += __uint_as_float(v[i].x & 0xFFFF0000u);
-        acc[2] += __uint_as_float(v[i].y << 16);
-        acc[3] += __uint_as_float(v[i].y & 0xFFFF0000u);
+        const float x0 = __uint_as_float(v[i].x << 16), x1 = __uint_as_float(v[i].x & 0xFFFF0000u);
+        const float x2 = __uint_as_float(v[i].y << 16), x3 = __uint_as_float(v[i].y & 0xFFFF0000u);
+        acc[0] += x0;
+        acc[1] += x1;
+        acc[2] += x2;
+        acc[3] += x3;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(x0), fabsf(x1)), fmaxf(fabsf(x2), fabsf(x3))));
       }
+      // the step tag (NaN shows in the sums); rare, so the branch stays cheap
+      if (a.sf && (!(m < DZ_BOUND) || !__builtin_isfinite(acc[0] + acc[1] + acc[2] + acc[3])))
+        flag_bad_step(a.sf);
     }
     f32x4* cb = s_comb + (pass & 1) * (BF_SUB * 32);   // double-buffered: one barrier a pass
     cb[tid] = acc;                                      // [k][j]
@@ -732,6 +750,10 @@ struct GUArgs {
                        // << 16)
   int write_grads;     // slab mode: also write the reduced fp32 gradient (tests / tools)
   int* bad_steps;
+  // the step tag the gradient producers set (dg_common.h; null: none): when it equals
+  // *step + 1 NO parameter of this launch changes (all-or-nothing with the producers'
+  // bounds; the per-entry non-finite skip below is only a last line)
+  const long long* gflag;
   // 1: the step's last (or only) update launch — decays the LR, counts the step, consumes a
   // pending non-finite flag; 0: an earlier part (e.g. the hidden layers, issued as soon as
   // their gradients exist) — leaves the LR alone and parks its non-finite flag
@@ -773,7 +795,9 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
   __shared__ unsigned s_flag[2];
   const int ly = blockIdx.y;
   const int tid = threadIdx.x;
-  const bool apply = !(a.gate && *a.gate == 0.f);
+  const bool gate_ok = !(a.gate && *a.gate == 0.f);
+  const bool tagged = a.gflag && a.step && *a.gflag == *a.step + 1;
+  const bool apply = gate_ok && !tagged;
   // SGD: l = lr * gscale (as sgd_kernel); RMSProp: l = lr, gscale inside
   const float l = a.MS ? (float)(*a.lr) : (float)(*a.lr) * a.gscale;
   unsigned bad = 0u;
@@ -996,8 +1020,9 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
             double* lrw = const_cast<double*>(a.lr);
             *lrw = *lrw * (1.0 - a.decay);
             if (a.step) *a.step += 1;
-            const bool any = flagged || T[GU_T_PEND] != 0u;
-            if (any && a.bad_steps && apply) *a.bad_steps += 1;
+            // (a non-finite loss was counted by the gate kernel; a tagged step here)
+            const bool any = flagged || tagged || T[GU_T_PEND] != 0u;
+            if (any && a.bad_steps && gate_ok) *a.bad_steps += 1;
             T[GU_T_PEND] = 0u;
           } else if (flagged) {
             T[GU_T_PEND] = 1u;
@@ -1074,7 +1099,7 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
 // (s8: 0 = bf16 frame, else the e5m2 copy's scale pointer; pad must be 1 then);
 // chunks of BG_BT_MULTI boards (dg_bias_chunks_multi).
 hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int C, int pad,
-                                      hipStream_t s) {
+                                      long long* sf, hipStream_t s) {
   if (C % 8 != 0 || C > 2048 || nl <= 0 || nl > BG_MAXL) return hipErrorInvalidValue;
   const int nchunks = (B + BG_BT_MULTI - 1) / BG_BT_MULTI;
   int threads = (BOARD * (C / 8) + 63) / 64 * 64;
@@ -1087,6 +1112,7 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
     Ls.s8[i] = (const float*)table[3 * i + 2];
     if (Ls.s8[i] && pad != 1) return hipErrorInvalidValue;
   }
+  Ls.sf = sf;
   hipLaunchKernelGGL(bias_grad_partial_kernel<2>, dim3(BOARD, nchunks, nl), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);
   return hipGetLastError();
@@ -1102,7 +1128,7 @@ int dg_bias_follow_tasks(int nl, int B, int C) {
   return nl * bf_tasks_per_layer((B + BG_BT_MULTI - 1) / BG_BT_MULTI, C);
 }
 hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned* sig, int nsig,
-                          unsigned* done, int mode, int grid, double timeout_us,
+                          unsigned* done, int mode, int grid, double timeout_us, long long* sf,
                           hipStream_t s) {
   if (nl <= 0 || nl > BF_MAXL || C % BF_CQ != 0 || C > 1024 || !sig || !done || grid < 1 ||
       nsig < 1 || nsig > 256 || (size_t)B * 441 * C * 2 > 0x7fffffffull)
@@ -1123,6 +1149,7 @@ hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned
   a.done = done;
   a.timeout_ticks = (long long)(timeout_us * 100.0);
   a.sleep = g_bf_sleep;
+  a.sf = sf;
   // load cache policy of the dZ stream (kbench A/B: tools/kbench_follow.py): 0 default,
   // 2 nt, 16 sc1
 #define BF_LAUNCH(M, X) hipLaunchKernelGGL((bias_follow_kernel<M, X>), dim3(grid), dim3(256), 0, s, a)
@@ -1278,7 +1305,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
                           float* P, float* G, const void* G16, float* MS, float rms_decay,
                           float gscale, const float* gate, double* lr, double decay,
                           long long* step, unsigned* tickets, int* bad_steps, int write_grads,
-                          int final, hipStream_t s) {
+                          int final, const long long* gflag, hipStream_t s) {
   if (n <= 0 || n > MAX_GU || !P || !G || !lr || !tickets || plain_n < 0)
     return hipErrorInvalidValue;
   GUArgs a;
@@ -1327,6 +1354,7 @@ hipError_t dg_grad_update(const long long* table, int n, long long plain_off, lo
   a.bad_steps = bad_steps;
   a.write_grads = write_grads;
   a.final = final;
+  a.gflag = gflag;
   a.tblocks = maxtotal < REFRESH_PARTS ? maxtotal : REFRESH_PARTS;
   const int blocks = a.tblocks + GU_NB * maxncb;
   if (blocks > GU_TG * GU_MAXG) return hipErrorInvalidValue;   // the ticket tree's groups

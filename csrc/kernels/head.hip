@@ -317,7 +317,8 @@ constexpr int HR_G = 16;
 __global__ void __launch_bounds__(1024)
 head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_part, int B, int n,
                    float* __restrict__ gw, float* __restrict__ gbias, float* __restrict__ gposb,
-                   bf16_t* gw16, bf16_t* gbias16, bf16_t* gposb16) {
+                   bf16_t* gw16, bf16_t* gbias16, bf16_t* gposb16, long long* sf) {
+  // (sf: the fused update's step tag, dg_common.h — set when an output is out of range)
   // (gw16 / gbias16 / gposb16: optional bf16 twins for the data-parallel bf16 wire format)
   __shared__ float s_red[HR_G][64];
   const int nout = n + NPTS;
@@ -341,6 +342,7 @@ head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_p
       for (int w = 0; w < 16; ++w) t += s_red[0][w];
       *gbias = t;
       if (gbias16) *gbias16 = f2bf(t);
+      if (sf && grad_out_of_range(t)) flag_bad_step(sf);
     }
     return;
   }
@@ -376,6 +378,7 @@ head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_p
       gposb[o - n] = v;
       if (gposb16) gposb16[o - n] = f2bf(v);
     }
+    if (sf && grad_out_of_range(v)) flag_bad_step(sf);
   }
 }
 
@@ -383,10 +386,11 @@ head_reduce_kernel(const float* __restrict__ dzb, const float* __restrict__ gw_p
 
 extern "C" hipError_t dg_head_reduce(const float* dzb, const float* gw_part, int B, int n,
                                      float* gw, float* gbias, float* gposb, void* gw16,
-                                     void* gbias16, void* gposb16, hipStream_t stream) {
+                                     void* gbias16, void* gposb16, long long* sf,
+                                     hipStream_t stream) {
   const int blocks = (n + NPTS + 63) / 64 + 1;  // + the gbias workgroup
   hipLaunchKernelGGL(head_reduce_kernel, dim3(blocks), dim3(1024), 0, stream, dzb, gw_part, B, n,
-                     gw, gbias, gposb, (bf16_t*)gw16, (bf16_t*)gbias16, (bf16_t*)gposb16);
+                     gw, gbias, gposb, (bf16_t*)gw16, (bf16_t*)gbias16, (bf16_t*)gposb16, sf);
   return hipGetLastError();
 }
 

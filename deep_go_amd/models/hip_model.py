@@ -121,7 +121,14 @@ class HipGoNet:
         self.grads16 = (torch.zeros(self.params.numel(), dtype=torch.bfloat16, device=dev)
                         if grad_wire == "bf16" else None)
         self.lr = torch.tensor([cfg.rate], dtype=torch.float64, device=dev)
-        self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        # [0] the device step counter (the fused update and the weight refresh count it); [1]
+        # the step tag: a gradient producer that writes a non-finite / out-of-range value sets
+        # it to step + 1 and the fused update then skips the WHOLE step (dg_common.h
+        # grad_out_of_range; nan_policy guard / skip stay all-or-nothing with the gradient
+        # pass 2 deferred into the update)
+        self._stepflag = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.step_count = self._stepflag[0:1]
+        self._sf = self._stepflag.data_ptr()
         self.ms = None
         if cfg.optimizer == "rmsprop":
             self.ms = torch.ones_like(self.params)
@@ -475,10 +482,10 @@ class HipGoNet:
                                      int(self.cfg.head_relu), 1.0 / self.global_batch))
         self._head_red = (h.head_reduce, (self.head_dzb.data_ptr(), self.head_gw_part.data_ptr(),
                                           self.B, hd.k * hd.k * hd.cin, G + hd.w_off * f4,
-                                          G + hd.b_off * f4, G + hd.pos_off * f4))
+                                          G + hd.b_off * f4, G + hd.pos_off * f4, self._sf))
         if self.grads16 is not None:
-            self._head_red = (h.head_reduce_w, self._head_red[1] + (
-                self._g16(hd.w_off), self._g16(hd.b_off), self._g16(hd.pos_off)))
+            self._head_red = (h.head_reduce_w, self._head_red[1][:-1] + (
+                self._g16(hd.w_off), self._g16(hd.b_off), self._g16(hd.pos_off), self._sf))
         self._head_eval = (h.head, (hd.k, hx.data_ptr(), hd.pad, hd.cin, self.B,
                                     P + hd.w_off * f4, P + hd.b_off * f4, P + hd.pos_off * f4,
                                     self.labels.data_ptr(), self.eval_loss.data_ptr(),
@@ -558,7 +565,7 @@ class HipGoNet:
                     np.array([[self.dz[i].data_ptr(), bpart, 0]], dtype=np.int64))
                 bch = self.bchunks_g
                 ops.append((h.bias_grad_partial_multi, (self._l0_btab.ctypes.data, 1, self.B,
-                                                        p.cout, dzp)))
+                                                        p.cout, dzp, self._sf)))
             else:
                 ops.append((h.bias_grad_partial, (self.dz[i].data_ptr(), self.B, p.cout, dzp,
                                                   bpart)))
@@ -574,9 +581,9 @@ class HipGoNet:
             if self.grads16 is not None:
                 ops.append((h.wgrad_reduce_w, red + (self._g16(spec.w_off),
                                                      self._g16(spec.pos_off),
-                                                     self._g16(spec.b_off))))
+                                                     self._g16(spec.b_off), self._sf)))
             else:
-                ops.append((h.wgrad_reduce, red))
+                ops.append((h.wgrad_reduce, red + (self._sf,)))
             if i > 0:
                 prev = lay.layers[i - 1]
                 if (p.board_d and self.wdfrag[i] is not None and p.cout == 256
@@ -909,7 +916,7 @@ class HipGoNet:
         self._bf_done = torch.zeros(ntask, dtype=torch.int32, device=self.device)
         base = (self._bf_table.ctypes.data, nl, self.B, C, self._bf_sig.data_ptr(), len(run),
                 self._bf_done.data_ptr())
-        self._bf_finish = (h.bias_follow, base + (1, ntask, 0.0))
+        self._bf_finish = (h.bias_follow, base + (1, ntask, 0.0, self._sf))
         self._bwd[g[0]][0] = self._bf_finish
         if l0_sep:
             self._bwd[0][0] = (self._noop, ())
@@ -917,7 +924,7 @@ class HipGoNet:
             return
         # per-wait bound of the follow pass: a stack row takes ~24 us at 12x128; a follower that
         # does not see one within this (the stack not beside it) leaves the rest to the finish
-        self._bf_follow = (h.bias_follow, base + (0, self.num_cus, 200.0))
+        self._bf_follow = (h.bias_follow, base + (0, self.num_cus, 200.0, self._sf))
         self._bwd_pre = [(h.conv_stack2_dgrad_sig, (a[1], a[2], a[3], a[5], self._bf_sig.data_ptr()))
                          if (f is h.conv_stack2 and a[0] == h.EPI_DGRAD) else (f, a)
                          for f, a in self._bwd_pre]
@@ -1142,9 +1149,10 @@ class HipGoNet:
             wt, bt, rt = tabs
             self._bwd[g[0]][0:3] = [
                 (h.bias_grad_partial_multi, (bt.ctypes.data, len(bt), self.B, p0.cout,
-                                             self.dzp[g[0]])),
+                                             self.dzp[g[0]], self._sf)),
                 (h.conv_wgrad_win8 if w8 else h.conv_wgrad_win,
-                 (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp, self.B, p0.KPw, S))
+                 (wt.ctypes.data, len(g), p0.cout, p0.Mpad_w, p0.cinp, self.B, p0.KPw, S,
+                  self._sf))
                 if tuple(g) in self.win_groups else
                 (h.conv_wgrad_multi, (p0.k, wt.ctypes.data, len(g), self.dzp[g[0]],
                                       p0.cout, p0.Mpad_w, spec0.pad, p0.cinp, self.B, p0.KPw,
@@ -1508,7 +1516,10 @@ class HipGoNet:
                            float(self.cfg.rmsprop_decay), grad_scale, gate, self.lr.data_ptr(),
                            float(self.cfg.rateDecay), self.step_count.data_ptr(),
                            self.gu_tickets.data_ptr(), self.bad_steps.data_ptr(),
-                           int(self.keep_grads), final, s)
+                           int(self.keep_grads), final,
+                           # the step tag is rank-local: under DP the all-reduced gradient's
+                           # full finite gate decides (the same on every rank)
+                           self._sf + 8 if self.global_batch == self.B else 0, s)
 
     def _gu_split(self, t):
         """(early rows, late rows) of a deferred step's grad_update table: the grouped

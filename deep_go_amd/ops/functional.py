@@ -229,9 +229,9 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
         out = torch.empty((cout, k, k, cin), dtype=torch.float32, device=dev)
         table = torch.tensor([[dzf.data_ptr(), xf.data_ptr(), slab.data_ptr()]], dtype=torch.int64)
         s = stream_handle()
-        h.conv_wgrad_win(table.data_ptr(), 1, cout, Mpad, cinp, B, KPw, splits, s)
+        h.conv_wgrad_win(table.data_ptr(), 1, cout, Mpad, cinp, B, KPw, splits, 0, s)
         h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, 9, cin, cinp,
-                       0, 0, 0, 0, s)
+                       0, 0, 0, 0, 0, s)
         torch.cuda.synchronize(dev)
         return out
     splits = splits or LY.pick_wgrad_splits(npix, KPw, Mpad,
@@ -250,7 +250,7 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, k: int, splits: int | None = N
     h.conv_wgrad(k, dzf.data_ptr(), max(1, pad), cout, Mpad, xf.data_ptr(), pad, cinp, B,
                  KPw, splits, slab.data_ptr(), s)
     h.wgrad_reduce(slab.data_ptr(), out.data_ptr(), splits, cout, Mpad, KPw, k * k, cin, cinp,
-                   bpart.data_ptr(), nch, gp.data_ptr(), gb.data_ptr(), s)
+                   bpart.data_ptr(), nch, gp.data_ptr(), gb.data_ptr(), 0, s)
     if with_bias:
         return out, gp, gb
     return out
@@ -289,7 +289,7 @@ def head(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, posb: torch.Tenso
            _ptr(dzb), int(head_relu), float(grad_scale if grad_scale is not None else 1.0 / B), s)
     if train:
         h.head_reduce(dzb.data_ptr(), gwp.data_ptr(), B, k * k * C, gw.data_ptr(), gb.data_ptr(),
-                      gp.data_ptr(), s)
+                      gp.data_ptr(), 0, s)
     if train:
         out.update(dz=LY.from_frame(dzf, 1, C), gw=gw.view(1, k, k, C), gbias=gb, gposb=gp)
     return out

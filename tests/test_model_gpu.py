@@ -645,13 +645,70 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
     check()
 
 
+@pytest.mark.parametrize("early,where", [(True, "hidden"), (False, "hidden"), (True, "layer0"),
+                                         (False, "head")])
+def test_fused_update_all_or_nothing_on_producer_tag(early, where):
+    """nan_policy guard / skip with the gradient pass 2 deferred into the fused update
+    (ADVICE r4): the gradient does not exist before the update, so its PRODUCERS check what
+    they write — the window weight-gradient slabs, the bias partials (every dZ value they read,
+    |dZ| < 2^100, which also bounds the first layer's 5x5 gradient), the head and first-layer
+    reduces — and tag the step (HipGoNet._stepflag[1] = step + 1).  The update then skips the
+    WHOLE step: no parameter, operand copy or bias table changes, the step counts once in
+    bad_steps, the LR still decays.  hidden: a NaN in a hidden layer's dZ frame (window slabs
+    + bias partials tag); layer0: a huge finite dZ_0 (the bias bound tags before the early
+    update launch, so the hidden layers it updates do not move either); head: a NaN in the
+    head's dZ partials.  early: the grouped layers' update runs before the first layer's
+    chain ends."""
+    cfg, net, _ = _setup(4, 128, 4, seed=1)
+    net._early_ok, net._early_env = early, ("1" if early else "0")
+    net.forward_backward()
+    torch.cuda.synchronize()
+    p0 = net.params.clone()
+    copies0 = [t.clone() for t in (*net.wfrag, *net.wdfrag, *net.pbias_frag) if t is not None]
+    lr0, st0 = net.lr.item(), int(net.step_count.item())
+    net.set_defer(True)
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        net._run(net._pre_train, s)
+        net._run(net._fwd_train, s)
+        net._run([net._head_train], s)
+        if where == "head":
+            net.head_dzb.view(-1)[5] = float("nan")
+        net.head_reduce()
+        net.start_bias_follow()
+        net._run(net._bwd_pre, s)
+        if where == "hidden":
+            net.dz[net.wgroups[0][0]].view(-1)[3000] = float("nan")
+        elif where == "layer0":
+            net.dz[0].view(-1)[3000] = 1e35
+        for i in range(net.L - 2, -1, -1):
+            net.backward_layer(i)
+        net.join_side()
+        assert net._early_issued == early
+        net.optimizer_step()
+    finally:
+        net._defer = False
+    torch.cuda.synchronize()
+    assert int(net._stepflag[1].item()) == st0 + 1          # tagged this step
+    assert torch.equal(net.params, p0)
+    assert all(torch.equal(a, b) for a, b in zip(
+        [t for t in (*net.wfrag, *net.wdfrag, *net.pbias_frag) if t is not None], copies0))
+    assert net.bad_steps.item() == 1
+    assert net.lr.item() < lr0 and int(net.step_count.item()) == st0 + 1
+    net.train_step()                         # the next, healthy step updates again
+    torch.cuda.synchronize()
+    assert not torch.equal(net.params, p0) and torch.isfinite(net.params).all()
+    assert net.bad_steps.item() == 1
+
+
 @pytest.mark.parametrize("early", [True, False])
 def test_fused_update_skips_non_finite_gradient_entries(early):
-    """With the pass 2 deferred the gradient does not exist before the update: a non-finite
-    gradient entry is left unapplied (that parameter keeps its value), the step is counted
-    in bad_steps, every other parameter still updates.  early: the grouped layers' update
-    runs right after their weight-gradient launch (its flag parked for the final launch);
-    else one launch at the end."""
+    """Defence in depth behind the producers' step tag: a non-finite value that reaches the
+    deferred pass 2 WITHOUT a producer having seen it (here poked into a slab after the
+    window kernel wrote it) is left unapplied entry by entry (that parameter keeps its value)
+    and the step is counted in bad_steps.  early: the grouped layers' update runs right after
+    their weight-gradient launch (its flag parked for the final launch); else one launch at
+    the end."""
     cfg, net, _ = _setup(4, 128, 4, seed=1)
     net.keep_grads = True
     net._early_ok, net._early_env = early, ("1" if early else "0")

@@ -94,7 +94,7 @@ def main():
         def red(sp):
             def f():
                 h.wgrad_reduce(slab.data_ptr(),
-                               gw.data_ptr(), sp, C, 128, KPw, 9, C, C, 0, 0, 0, 0, s)
+                               gw.data_ptr(), sp, C, 128, KPw, 9, C, C, 0, 0, 0, 0, 0, s)
             return f
         res.setdefault("reduce_im2col_splits", []).append(round(timeit(red(splits)), 2))
     out = {k: {"us": v, "tflops": round(flops / (min(v) * 1e-6) / 1e12, 1)} for k, v in res.items()}

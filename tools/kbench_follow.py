@@ -84,7 +84,7 @@ def main():
     bt = net._bf_table
     old_tab = np.ascontiguousarray(np.array([[int(r[0]), int(r[1]), 0] for r in bt], dtype=np.int64))
     out["old_partials_alone"] = timed(lambda: h.bias_grad_partial_multi(
-        old_tab.ctypes.data, len(old_tab), B, 128, 1, s))
+        old_tab.ctypes.data, len(old_tab), B, 128, 1, 0, s))
 
     for aux in (0, 2, 16):
         for slp in (1, 4, 16):

@@ -57,7 +57,7 @@ def main():
                           net.params.data_ptr(), net.grads.data_ptr(), 0, 0, 0.9, 1.0,
                           net.gate.data_ptr(), net.lr.data_ptr(), 0.0,
                           net.step_count.data_ptr(), net.gu_tickets.data_ptr(),
-                          net.bad_steps.data_ptr(), 0, 1, s)
+                          net.bad_steps.data_ptr(), 0, 1, 0, s)
         return run
 
     variants = {"full": base}

@@ -41,7 +41,7 @@ def main():
 
         def red():
             h.wgrad_reduce(slab.data_ptr(), gw.data_ptr(), splits, C, 128, KPw, 9, C, C, 0, 0,
-                           0, 0, s)
+                           0, 0, 0, s)
         for rnd in range(2):
             for mode in (0, 1, 2, 4, 8, 3, 6, 12, 14, 15):
                 h.conv_wgrad_set_ablate(mode)

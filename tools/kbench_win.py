@@ -48,7 +48,7 @@ def main():
     cfg = {"C": C, "NL": NL, "win_splits": Sw, "t3_splits": St}
 
     def win():
-        h.conv_wgrad_win(tw.ctypes.data, NL, C, C, C, B, KPw, Sw, s)
+        h.conv_wgrad_win(tw.ctypes.data, NL, C, C, C, B, KPw, Sw, 0, s)
 
     def t3():
         h.conv_wgrad_multi(3, tt.ctypes.data, NL, 1, C, C, 1, C, B, KPw, St, s)
