@@ -140,6 +140,9 @@ hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const doubl
 hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t ng, float* gate,
                           int* bad_count, const void* grads16, hipStream_t s);
 hipError_t dg_lr_decay(double* lr, double decay, long long* step, hipStream_t s);
+hipError_t dg_finite_gate1(const float* loss, int n, const float* grads, const void* grads16,
+                           size_t ng, float* gate, int* bad_count, unsigned* ticket,
+                           hipStream_t s);
 hipError_t dg_weight_refresh(const long long* table, int n, double* lr, double decay,
                              long long* step, hipStream_t s);
 int dg_grad_update_tickets();
@@ -480,6 +483,12 @@ PYBIND11_MODULE(_dghip, m) {
                          P<void>(grads16), S(stream)),
           "finite_gate_bf16");
   }, "finite_gate over the bf16 (wire-format) gradient");
+  m.def("finite_gate1", [](uintptr_t loss, int n, uintptr_t grads, uintptr_t grads16, size_t ng,
+                           uintptr_t gate, uintptr_t bad, uintptr_t ticket, uintptr_t stream) {
+    check(dg_finite_gate1(P<float>(loss), n, P<float>(grads), P<void>(grads16), ng,
+                          P<float>(gate), P<int>(bad), P<unsigned>(ticket), S(stream)),
+          "finite_gate1");
+  }, "loss + gradient finite gate in one launch (fp32 grads or the bf16 twin grads16)");
   m.def("lr_decay", [](uintptr_t lr, double decay, uintptr_t step, uintptr_t stream) {
     check(dg_lr_decay(P<double>(lr), decay, P<long long>(step), S(stream)), "lr_decay");
   });

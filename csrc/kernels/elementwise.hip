@@ -436,6 +436,47 @@ __global__ void grad_gate_kernel(const G* __restrict__ g, size_t n, float* __res
   }
 }
 
+// The whole gate in ONE launch (the loss check and the gradient scan were two, in series on
+// the data-parallel step's tail): every block scans its share of the (all-reduced) gradient,
+// block 0 also the loss; each block's verdict rides on its ticket (count | bad << 16, one
+// device atomic) and the LAST block writes the gate, counts a bad step once and re-zeroes the
+// ticket (graph-replayable).
+template <typename G>
+__global__ void __launch_bounds__(256) gate_all_kernel(const float* __restrict__ loss, int nloss,
+                                                       const G* __restrict__ g, size_t n,
+                                                       float* __restrict__ gate,
+                                                       int* __restrict__ bad_count,
+                                                       unsigned* __restrict__ ticket) {
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  bool bad = false;
+  if (blockIdx.x == 0 && loss)
+    for (int i = threadIdx.x; i < nloss; i += blockDim.x) bad |= !isfinite(loss[i]);
+  if (g) {
+    const size_t n4 = n / 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+         i += (size_t)gridDim.x * blockDim.x) {
+      const f32x4 v = grad4_at(g, i);
+      bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
+    }
+    for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+      bad |= !isfinite(grad_at(g, i));
+  }
+  if (bad) s_bad = 1;   // (benign same-value race)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = atomicAdd(ticket, 1u + (s_bad ? 0x10000u : 0u));
+    if ((old & 0xFFFFu) == gridDim.x - 1) {
+      const bool any = (old >> 16) != 0u || s_bad;
+      *gate = any ? 0.f : 1.f;
+      if (any && bad_count) *bad_count += 1;
+      *ticket = 0u;
+    }
+  }
+}
+
 __global__ void lr_decay_kernel(double* lr, double decay, long long* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     *lr = *lr * (1.0 - decay);
@@ -822,6 +863,9 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
     const float inv8 = L.s_w ? 1.f / *L.s_w : 0.f;
     const size_t zstride = (size_t)S.Mpad * S.KP;
     const bool vec = S.slab && (L.cin & 3) == 0 && (L.cinp & 3) == 0 && (S.KP & 3) == 0;
+    // the flat (all-reduced, data-parallel) gradient: 4 consecutive ci per thread too (the
+    // per-element form below loaded one bf16 per lane: +8 us on the DP step at 12x128)
+    const bool vecf = !S.slab && (L.cin & 3) == 0 && (S.w_off & 3) == 0;
     const bool tile_block = (int)blockIdx.x < a.tblocks;
     for (int tix = blockIdx.x; tile_block && tix < tiles; tix += a.tblocks) {
       const int t = tix / (nct * nit);
@@ -868,6 +912,44 @@ __global__ void __launch_bounds__(256) grad_update_kernel(GUArgs a) {
             }
             *(f32x4*)(Pw + o) = v;
             if (MSw) *(f32x4*)(MSw + o) = m4;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tileS[rr][cc + k] = v[k];
+        }
+      } else if (vecf) {
+        // the same 4-ci units over the flat gradient (G or its bf16 twin G16)
+        f32x4 gs[4], pp[4];
+        bool ok[4];
+        size_t os[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + 256 * u;
+          const int rr = e4 >> 4, cc = (e4 & 15) * 4;
+          const int co = cot * 64 + rr, ci = cit * 64 + cc;
+          ok[u] = co < L.cout && ci < L.cin;
+          os[u] = ok[u] ? ((size_t)co * L.taps + t) * L.cin + ci : 0;
+          gs[u] = a.G16 ? grad4_at(a.G16 + S.w_off, os[u] / 4) : *(const f32x4*)(Gw + os[u]);
+          pp[u] = *(const f32x4*)(Pw + os[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + 256 * u;
+          const int rr = e4 >> 4, cc = (e4 & 15) * 4;
+          const int co = cot * 64 + rr, ci = cit * 64 + cc;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (ok[u]) {
+            f32x4 m4 = {0.f, 0.f, 0.f, 0.f};
+            if (MSw) m4 = *(const f32x4*)(MSw + os[u]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              float m = m4[k];
+              v[k] = gu_update(pp[u][k], gs[u][k], MSw != nullptr, m, l, a.rms_decay, a.gscale,
+                               apply, bad);
+              m4[k] = m;
+              refresh_elem(L, co, ci + k, t, v[k], inv8, wmax);
+            }
+            *(f32x4*)(Pw + os[u]) = v;
+            if (MSw) *(f32x4*)(MSw + os[u]) = m4;
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) tileS[rr][cc + k] = v[k];
@@ -1221,6 +1303,27 @@ hipError_t dg_finite_gate(const float* loss, int n, const float* grads, size_t n
       hipLaunchKernelGGL(grad_gate_kernel<float>, dim3(blocks), dim3(256), 0, s, grads, ng,
                          gate, bad_count);
   }
+  return hipGetLastError();
+}
+
+// gate = finite(loss) && finite(grads | grads16) in one launch (gate_all_kernel); ticket: one
+// zeroed word the launch leaves zeroed
+hipError_t dg_finite_gate1(const float* loss, int n, const float* grads, const void* grads16,
+                           size_t ng, float* gate, int* bad_count, unsigned* ticket,
+                           hipStream_t s) {
+  if (!gate || !ticket) return hipErrorInvalidValue;
+  int blocks = 1;
+  if ((grads || grads16) && ng) {
+    blocks = (int)((ng / 4 + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
+  }
+  if (grads16)
+    hipLaunchKernelGGL(gate_all_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, loss, n,
+                       (const bf16_t*)grads16, ng, gate, bad_count, ticket);
+  else
+    hipLaunchKernelGGL(gate_all_kernel<float>, dim3(blocks), dim3(256), 0, s, loss, n,
+                       grads, grads ? ng : (size_t)0, gate, bad_count, ticket);
   return hipGetLastError();
 }
 

@@ -134,6 +134,7 @@ class HipGoNet:
             self.ms = torch.ones_like(self.params)
         # non-finite loss guard (cfg.nan_policy == "skip"): device gate read by the optimizer
         self.gate = torch.ones(1, dtype=torch.float32, device=dev)
+        self._gate_ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # finite_gate1
         self.bad_steps = torch.zeros(1, dtype=torch.int32, device=dev)
         # fused end of step (grad_update): per-layer + grid tickets, zero between launches
         self.gu_tickets = torch.zeros(self.h.grad_update_tickets(), dtype=torch.int32, device=dev)
@@ -1474,9 +1475,11 @@ class HipGoNet:
             # gradient does not exist yet: the gate is the loss, and the fused update leaves
             # any non-finite gradient entry unapplied (and counts the step in bad_steps)
             dp = self.global_batch != self.B
-            (self.h.finite_gate_bf16 if w16 else self.h.finite_gate)(
-                0 if dp else self.loss.data_ptr(), self.B, 0 if slabs else g,
-                0 if slabs else n, self.gate.data_ptr(), self.bad_steps.data_ptr(), s)
+            # (one launch: the loss check and the gradient scan together)
+            self.h.finite_gate1(0 if dp else self.loss.data_ptr(), self.B,
+                                0 if (slabs or w16) else g, g if (w16 and not slabs) else 0,
+                                0 if slabs else n, self.gate.data_ptr(),
+                                self.bad_steps.data_ptr(), self._gate_ticket.data_ptr(), s)
             gate = self.gate.data_ptr()
         if self.cfg.nan_policy != "raise":
             gate = self.gate.data_ptr()
