@@ -455,8 +455,18 @@ __global__ void __launch_bounds__(256) gate_all_kernel(const float* __restrict__
     for (int i = threadIdx.x; i < nloss; i += blockDim.x) bad |= !isfinite(loss[i]);
   if (g) {
     const size_t n4 = n / 4;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
-         i += (size_t)gridDim.x * blockDim.x) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {   // 4 loads in flight per thread
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = grad4_at(g, i + u * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        bad |= !(isfinite(v[u][0]) && isfinite(v[u][1]) && isfinite(v[u][2]) &&
+                 isfinite(v[u][3]));
+    }
+    for (; i < n4; i += stride) {
       const f32x4 v = grad4_at(g, i);
       bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
     }
@@ -1312,10 +1322,12 @@ hipError_t dg_finite_gate1(const float* loss, int n, const float* grads, const v
                            size_t ng, float* gate, int* bad_count, unsigned* ticket,
                            hipStream_t s) {
   if (!gate || !ticket) return hipErrorInvalidValue;
+  // (<= 128 blocks: the tickets serialize on one address, ~11 ns each — 1024 blocks cost
+  // 15 us at 2.1M gradients, more than the scan)
   int blocks = 1;
   if ((grads || grads16) && ng) {
-    blocks = (int)((ng / 4 + 255) / 256);
-    if (blocks > 1024) blocks = 1024;
+    blocks = (int)((ng / 4 + 1023) / 1024);
+    if (blocks > 128) blocks = 128;
     if (blocks < 1) blocks = 1;
   }
   if (grads16)
