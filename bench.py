@@ -89,7 +89,7 @@ def parse(argv=None):
                          "group | bottom group | first layer)")
     ap.add_argument("--wgrad-group", type=int, default=0,
                     help="DP: hidden layers per grouped weight-gradient launch.  0 = auto: at "
-                         "d >= 256 half of them (the top group's all-reduce runs beside the "
+                         "d >= 256 and world > 1 half of them (the top group's all-reduce runs beside the "
                          "bottom group's launch: 3.138 vs 3.178 ms/step with the RCCL-shaped "
                          "proxy), at d = 128 one launch (the split doubles the split-K slab "
                          "traffic: +6%% compute for ~5 us less exposed comm); "
@@ -419,7 +419,13 @@ class _Case:
         n_hidden = args.layers - 2
         wg = None
         if use_dp:
-            wg = args.wgrad_group or (max(1, (n_hidden + 1) // 2) if channels >= 256 else 16)
+            # auto: split the hidden layers' weight-gradient launch in two at d >= 256 only
+            # when there is communication to hide (world > 1): the top group's all-reduce
+            # then runs beside the second launch.  At world 1 (--force-dp) the split is pure
+            # cost: -2.5% (12x256 bf16) / -4.5% (fp8) vs one launch, which matches the plain
+            # step (profiles/r5_dp_fusion.txt)
+            wg = args.wgrad_group or (max(1, (n_hidden + 1) // 2)
+                                      if channels >= 256 and world > 1 else 16)
         # (--grad-dtype bf16: the gradient reduces write the bf16 wire twin themselves)
         self.net = net = HipGoNet(self.cfg, B, device=dev, global_batch=B * world,
                                   wgrad_group=wg,

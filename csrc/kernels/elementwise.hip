@@ -457,12 +457,12 @@ __global__ void __launch_bounds__(256) gate_all_kernel(const float* __restrict__
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {   // 4 loads in flight per thread
-      f32x4 v[4];
+    for (; i + 7 * stride < n4; i += 8 * stride) {   // 8 loads in flight per thread
+      f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = grad4_at(g, i + u * stride);
+      for (int u = 0; u < 8; ++u) v[u] = grad4_at(g, i + u * stride);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
         bad |= !(isfinite(v[u][0]) && isfinite(v[u][1]) && isfinite(v[u][2]) &&
                  isfinite(v[u][3]));
     }
@@ -1322,12 +1322,13 @@ hipError_t dg_finite_gate1(const float* loss, int n, const float* grads, const v
                            size_t ng, float* gate, int* bad_count, unsigned* ticket,
                            hipStream_t s) {
   if (!gate || !ticket) return hipErrorInvalidValue;
-  // (<= 128 blocks: the tickets serialize on one address, ~11 ns each — 1024 blocks cost
-  // 15 us at 2.1M gradients, more than the scan)
+  // (<= 256 blocks: the tickets serialize on one address, ~11 ns each — 1024 blocks cost
+  // 15 us at 2.1M gradients, more than the scan; 128 blocks of 4 loads in flight per lane
+  // were latency-bound at 7.2M: 12.7 us)
   int blocks = 1;
   if ((grads || grads16) && ng) {
-    blocks = (int)((ng / 4 + 1023) / 1024);
-    if (blocks > 128) blocks = 128;
+    blocks = (int)((ng / 4 + 2047) / 2048);
+    if (blocks > 256) blocks = 256;
     if (blocks < 1) blocks = 1;
   }
   if (grads16)
