@@ -30,6 +30,7 @@ hipError_t dg_conv_board(int epi, int kw, int bm, const void* A, int KP, int M, 
                          hipStream_t stream);
 void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
+void dg_conv_stack2_set_sched(int stag, int prio, int delay);
 void dg_conv_stack_f8_set_mode(int m);
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
                             const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
@@ -311,6 +312,10 @@ PYBIND11_MODULE(_dghip, m) {
         "conv_stack_f8 timing-ablation mode (0 = production)");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
         "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
+  m.def("conv_stack2_set_sched", [](int stag, int prio, int delay) {
+    dg_conv_stack2_set_sched(stag, prio, delay);
+  }, "conv_stack2 schedule: staggered two-group on / off (overrides DG_STACK2_STAG), co-half-0 "
+     "MFMA priority 0..2, co-half-1 start delay");
   m.def("conv_stack2", [](int epi, uintptr_t table, int nl, uintptr_t X0, int l1, int B,
                           uintptr_t stream) {
     check(dg_conv_stack2(epi, P<long long>(table), nl, P<void>(X0), l1, B, S(stream)),

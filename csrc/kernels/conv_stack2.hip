@@ -37,6 +37,7 @@
 //
 // Reference ops: nn.SpatialZeroPadding + SpatialConvolutionMM + Add + ReLU per layer
 // (experiments.lua:137-147) and their backward through the stack (train.lua:10).
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "dg_common.h"
@@ -88,6 +89,11 @@ struct StackArgs {
   const uint8_t* in_rank;     // [B]
   StackLayer L[MAXL];
   dghead::HeadMArgs head;  // (head_body.h; X unused: the image is resident)
+  // STAG: the staggered two-group schedule (see the K loop): the co-half-0 group's MFMA
+  // priority (0: none, 1 | 2: s_setprio) and an initial delay of the co-half-1 group
+  // (s_sleep 127 rounds)
+  int stag_prio;
+  int stag_delay;
   // EPI_DGRAD with the bias-gradient follower (SIG): per-row arrival counters.  Row r's output
   // frame is stored write-through (sc1) and, once every wave of the workgroup has drained its
   // stores (s_waitcnt vmcnt(0) + barrier), one lane adds 1 to sig[r] (agent scope): the
@@ -153,11 +159,46 @@ DG_DEV uint32_t pair_mask(uint32_t nib) {
   return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
 
+// Staggered two-group schedule (STAG): LDS counters instead of workgroup barriers.  A wave
+// counts itself in (+1 from one lane) once its LDS accesses are done (lgkmcnt(0)); waiters
+// poll with s_sleep between reads.  Both in inline asm: as C++ (a lane-0 branch, a polling
+// loop) the control flow inside the rolled K loop costs 100-160 spilled VGPRs.  (An asm
+// ds_add / ds_read outstanding ahead of the compiler's own LDS reads only lengthens its
+// in-order lgkmcnt waits.)
+DG_DEV void grp_signal(LDS_AS unsigned* c) {
+  unsigned long long sv;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %1, %2\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv) : "v"((unsigned)(size_t)c), "v"(1u) : "memory");
+}
+DG_DEV void grp_wait(LDS_AS unsigned* c, unsigned target) {
+  unsigned v, sc;
+  asm volatile(
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_nop 4\n\t"
+      "s_cmp_ge_u32 %1, %3\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : "=&v"(v), "=&s"(sc) : "v"((unsigned)(size_t)c), "s"(target) : "memory", "scc");
+}
+
 // MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop
-template <int EPI, int MODE, bool SIG = false>
+// 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop, 16 = no
+// epilogue (nothing written back into the image)
+template <int EPI, int MODE, bool SIG = false, bool STAG = false>
 __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
-  constexpr bool TWO_GROUP = EPI == EPI_DGRAD;  // epilogue schedule (see the K loop)
+  // epilogue schedule (see the K loop)
+  constexpr bool TWO_GROUP = EPI == EPI_DGRAD && !STAG;
+  static_assert(!(SIG && STAG), "the follower's row signals need the barrier schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -165,6 +206,18 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   const int wm = wave >> 2, wn = wave & 3;
   const int b = blockIdx.x;
   char* sH = smem + SCRATCH;  // image c at sH + c * H_BYTES
+  // STAG counters R0 R1 (waves past their reads of image 0 / 1 in this layer, 8 per layer)
+  // and W0 W1 (waves of co-half 0 / 1 that wrote their image, 4 per layer), in the head
+  // scratch (unused until the head, after the final barrier)
+  LDS_AS unsigned* cnt = (LDS_AS unsigned*)(smem + SCRATCH - 16);
+  if constexpr (STAG) {
+    if (tid < 4) cnt[tid] = 0u;
+    const int wmu = __builtin_amdgcn_readfirstlane(wm);
+    if (wmu == 0 && a.stag_prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (wmu == 0 && a.stag_prio == 2) __builtin_amdgcn_s_setprio(2);
+    if (wmu == 1)
+      for (int d = 0; d < a.stag_delay; ++d) __builtin_amdgcn_s_sleep(127);
+  }
 
   // ---- prologue: the first layer's input frame (both 64-channel images) by LDS-DMA ----
   if (EPI == EPI_FWD && a.l1 && a.in_planes) {
@@ -389,6 +442,8 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       }
     };
     int s = 0;
+    // STAG: layer index among the staggered layers (the fused first layer keeps barriers)
+    const unsigned kx = (unsigned)(l - (EPI == EPI_FWD && a.l1 ? 1 : 0));
     if (EPI == EPI_FWD && l == 0 && a.l1) {
       // the fused first layer: 16 K-steps over the staged input frame (nothing to copy out)
 #pragma unroll 1
@@ -407,9 +462,10 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     } else {
-#pragma unroll 1
-      for (int h2 = 0; h2 < 2; ++h2) {
+      auto chunk = [&](const int h2) {
         if (h2 == 1 && TWO_GROUP) lds_barrier();  // A
+        // STAG: image h2 holds the previous layer's output once its co-half wrote it
+        if constexpr (STAG) grp_wait(cnt + 2 + h2, 4u * kx);
         if (!(MODE & 4) && co_on) {
 #pragma unroll 1
           for (; s < h2 * T + CO_STEPS; ++s) {
@@ -423,6 +479,15 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
           if (EPI == EPI_DGRAD && s == NSTEP - 2) load_em();
           kstep(s, false);
         }
+        if constexpr (STAG) grp_signal(cnt + h2);   // past this layer's reads of image h2
+      };
+      if constexpr (STAG) {
+        // (two inlined chunks: a rolled chunk loop around the counter asm costs ~100 spills)
+        chunk(0);
+        chunk(1);
+      } else {
+#pragma unroll 1
+        for (int h2 = 0; h2 < 2; ++h2) chunk(h2);
       }
     }
 
@@ -443,6 +508,13 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
       }
     }
     auto write_out = [&]() {
+      if constexpr ((MODE & 16) != 0) {   // (the accumulators stay live: no MFMA is dropped)
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int j = 0; j < NF; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+      }
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int p = wn * NF * 16 + j * 16 + lr;
@@ -474,6 +546,21 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
         }
       }
     };
+    // Staggered two-group schedule (STAG): no workgroup barrier inside the run.  Co-half g's
+    // waves write image g once all 8 waves are past their reads of it in this layer (R_g),
+    // then count themselves in W_g; a wave reads image c of a layer once co-half c has
+    // written it (W_c).  Both groups run chunk 0 (image 0) first, so co-half 0 may run up to
+    // half a layer ahead of co-half 1: its epilogue runs beside co-half 1's last K-steps and
+    // co-half 1's beside co-half 0's next image-0 K-steps — every wave's epilogue overlaps
+    // the other group's MFMAs (the barrier schedules below idle the MFMA pipes through it).
+    if constexpr (STAG) {
+      if (!(EPI == EPI_FWD && l == 0 && a.l1)) {
+        grp_wait(cnt + wm, 8u * (kx + 1));
+        write_out();
+        grp_signal(cnt + 2 + wm);
+        continue;
+      }
+    }
     if constexpr (TWO_GROUP) {
       if (wm == 0) write_out();  // image 0: dead since barrier A
       // SIG: every wave's copy-out stores of the previous row's output (K-steps 0..14 of this
@@ -522,21 +609,37 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   }
 }
 
-template <int EPI, int MODE, bool SIG = false>
+template <int EPI, int MODE, bool SIG = false, bool STAG = false>
 hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
   constexpr size_t lds = SCRATCH + 2 * (size_t)H_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack2_kernel<EPI, MODE, SIG>,
+    (void)hipFuncSetAttribute((const void*)conv_stack2_kernel<EPI, MODE, SIG, STAG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack2_kernel<EPI, MODE, SIG>), dim3(B), dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((conv_stack2_kernel<EPI, MODE, SIG, STAG>), dim3(B), dim3(NT), lds, stream,
+                     a);
   return hipGetLastError();
 }
 
 int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
+// the staggered schedule: -1 = not yet read from DG_STACK2_STAG ("0" off, "1" on, or
+// "1,PRIO,DELAY"), else 0 / 1; its co-half-0 priority and co-half-1 start delay
+int g_stack2_stag = -1, g_stack2_prio = 1, g_stack2_delay = 0;
+void stack2_sched_from_env() {
+  if (g_stack2_stag >= 0) return;
+  const char* e = getenv("DG_STACK2_STAG");
+  g_stack2_stag = 0;
+  if (e && *e) {
+    int v = 0, p = g_stack2_prio, d = g_stack2_delay;
+    const int n = sscanf(e, "%d,%d,%d", &v, &p, &d);
+    g_stack2_stag = n >= 1 && v ? 1 : 0;
+    if (n >= 2) g_stack2_prio = p;
+    if (n >= 3) g_stack2_delay = d;
+  }
+}
 
 hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                          const dghead::HeadMArgs* head, hipStream_t stream,
@@ -555,6 +658,10 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
   a.fuse_head = 0;
   a.head = dghead::HeadMArgs{};
   a.sig = sig;
+  stack2_sched_from_env();
+  a.stag_prio = g_stack2_prio;
+  a.stag_delay = g_stack2_delay;
+  const bool stag = g_stack2_stag == 1 && !sig;
   if (sig && epi != EPI_DGRAD) return hipErrorInvalidValue;
   // (the buffer stores address a row's frame with 32-bit offsets)
   if (sig && (size_t)B * FF * C * 2 > 0x7fffffffull) return hipErrorInvalidValue;
@@ -575,8 +682,17 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     a.head = *head;
   }
   if (epi == EPI_DGRAD) {
-    return sig ? launch_stack2<EPI_DGRAD, 0, true>(a, B, stream)
-               : launch_stack2<EPI_DGRAD, 0>(a, B, stream);
+    if (sig) return launch_stack2<EPI_DGRAD, 0, true>(a, B, stream);
+    if (stag) {
+      if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16, false, true>(a, B, stream);
+      return launch_stack2<EPI_DGRAD, 0, false, true>(a, B, stream);
+    }
+    if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16>(a, B, stream);
+    return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
+  }
+  if (stag) {
+    if (g_stack2_mode == 16) return launch_stack2<EPI_FWD, 16, false, true>(a, B, stream);
+    return launch_stack2<EPI_FWD, 0, false, true>(a, B, stream);
   }
   switch (g_stack2_mode) {  // forward: the MODE ablations too (kbench_stack.py)
     case 2: return launch_stack2<EPI_FWD, 2>(a, B, stream);
@@ -584,6 +700,7 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     case 14: return launch_stack2<EPI_FWD, 14>(a, B, stream);
     case 4: return launch_stack2<EPI_FWD, 4>(a, B, stream);
     case 10: return launch_stack2<EPI_FWD, 10>(a, B, stream);
+    case 16: return launch_stack2<EPI_FWD, 16>(a, B, stream);
     default: return launch_stack2<EPI_FWD, 0>(a, B, stream);
   }
 }
@@ -593,6 +710,14 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
 extern "C" {
 
 void dg_conv_stack2_set_mode(int m) { g_stack2_mode = m; }
+
+// the staggered two-group schedule (overrides DG_STACK2_STAG): on 0 / 1, co-half-0 MFMA
+// priority 0..2, co-half-1 start delay (s_sleep 127 rounds)
+void dg_conv_stack2_set_sched(int stag, int prio, int delay) {
+  g_stack2_stag = stag ? 1 : 0;
+  g_stack2_prio = prio;
+  g_stack2_delay = delay;
+}
 
 // table: nl rows of {A (fragment-ordered weights), pbias_frag, Y, mask} (int64 pointers)
 //   epi 1 (forward): pbias required, mask optional (written)

@@ -220,7 +220,8 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // EPI_DGRAD: the backward-data chain dZ_{l-1} = mask_{l-1} * (W_l^T dZ_l) (e5m2 gradients,
 // e4m3 weights: MX MFMA with A e4m3 / B e5m2), dequantized bf16 dZ frames out.
 // MODE: 0 in production; timing ablations (tools/kbench_stack.py, wrong results):
-// 2 = no A loads in the K loop, 4 = no copy-out.  MODE bit 8 (production, fp8 weight
+// 2 = no A loads in the K loop, 4 = no copy-out, 64 = no epilogue (bias / quantize / image
+// writes), 128 = no B reads (register operands).  MODE bit 8 (production, fp8 weight
 // gradients): also store the raw fp8 copies (X8_0, every non-last layer's Y8) — a compile-time
 // switch: a runtime null test around the store splits the K loop's blocks and costs 24-45
 // spilled VGPRs.  MODE bit 16 (with 8): no dequantized bf16 copy-out of the non-last layers —
@@ -409,7 +410,17 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       auto kstep = [&](const int st, const int cs, const bool co) {
         const char* An = st + 1 < G::STEPS ? Ap + (st + 1) * STEP_BYTES : A_after;
         i32x8 bfr[NF];
-        read_B(st, bfr);
+        if constexpr ((MODE & 128) != 0) {
+          // (ablation: no B reads — opaque register operands)
+#pragma unroll
+          for (int j = 0; j < NF; ++j) {
+            int z = (int)pk[j];
+            asm volatile("" : "+v"(z));
+            bfr[j] = i32x8{z, z, z, z, z, z, z, z};
+          }
+        } else {
+          read_B(st, bfr);
+        }
         mma(Ak, 0, bfr, acc);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(MODE & 2)) load_A(An, 0, Ak);
@@ -437,6 +448,15 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       for (; st < G::STEPS; ++st) kstep(st, 0, false);
 
       // ---- pass epilogue ----
+      if constexpr ((MODE & 64) != 0) {
+        // (ablation: no epilogue — the accumulators only feed the amax)
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int j = 0; j < NF; ++j) vmax = fmaxf(vmax, acc[i][j][0]);
+        if (C == 128 || hp == NC - 1) lds_barrier();
+        continue;
+      }
       // an opaque zero added to the epilogue's addresses: otherwise the compiler hoists all
       // per-fragment table / LDS addresses out of the layer loop and spills them
       int z0 = 0;
@@ -630,15 +650,35 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
   if (epi == EPI_DGRAD) {
     if (a.sr_step) {
       if (!y8) return launch_f8<C, EPI_DGRAD, 32>(a, B, stream);
-      return any_y ? launch_f8<C, EPI_DGRAD, 40>(a, B, stream)
-                   : launch_f8<C, EPI_DGRAD, 56>(a, B, stream);
+      if (any_y) return launch_f8<C, EPI_DGRAD, 40>(a, B, stream);
+      // the production backward-data chain and its timing ablations
+      switch (g_f8_mode) {
+        case 2: return launch_f8<C, EPI_DGRAD, 56 | 2>(a, B, stream);
+        case 4: return launch_f8<C, EPI_DGRAD, 56 | 4>(a, B, stream);
+        case 64: return launch_f8<C, EPI_DGRAD, 56 | 64>(a, B, stream);
+        case 68: return launch_f8<C, EPI_DGRAD, 56 | 68>(a, B, stream);
+        case 198: return launch_f8<C, EPI_DGRAD, 56 | 198>(a, B, stream);
+        default: return launch_f8<C, EPI_DGRAD, 56>(a, B, stream);
+      }
     }
     if (!y8) return launch_f8<C, EPI_DGRAD, 0>(a, B, stream);
     return any_y ? launch_f8<C, EPI_DGRAD, 8>(a, B, stream)
                  : launch_f8<C, EPI_DGRAD, 24>(a, B, stream);
   }
-  if (y8)
-    return any_y ? launch_f8<C, EPI_FWD, 8>(a, B, stream) : launch_f8<C, EPI_FWD, 24>(a, B, stream);
+  if (y8 && any_y) return launch_f8<C, EPI_FWD, 8>(a, B, stream);
+  if (y8) {
+    // the production forward (fp8 copies only) and its timing ablations
+    switch (g_f8_mode) {
+      case 2: return launch_f8<C, EPI_FWD, 24 | 2>(a, B, stream);
+      case 4: return launch_f8<C, EPI_FWD, 24 | 4>(a, B, stream);
+      case 64: return launch_f8<C, EPI_FWD, 24 | 64>(a, B, stream);
+      case 68: return launch_f8<C, EPI_FWD, 24 | 68>(a, B, stream);
+      case 128: return launch_f8<C, EPI_FWD, 24 | 128>(a, B, stream);
+      case 196: return launch_f8<C, EPI_FWD, 24 | 196>(a, B, stream);
+      case 198: return launch_f8<C, EPI_FWD, 24 | 198>(a, B, stream);
+      default: return launch_f8<C, EPI_FWD, 24>(a, B, stream);
+    }
+  }
   switch (g_f8_mode) {
     case 2: return launch_f8<C, EPI_FWD, 2>(a, B, stream);
     case 4: return launch_f8<C, EPI_FWD, 4>(a, B, stream);
