@@ -32,6 +32,8 @@ void dg_conv_board_set_ablate(int mode);
 void dg_conv_stack2_set_mode(int on);
 void dg_conv_stack2_set_sched(int stag, int prio, int delay);
 void dg_conv_stack_f8_set_mode(int m);
+void dg_conv_stack_f8_set_sched(int stag, int delay);
+void dg_conv_stack_f8_set_debug(unsigned long long* dbg);
 hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, const void* X0,
                             const float* s_x0, unsigned* amax_x0, int B, const long long* y8,
                             const long long* sr_step, hipStream_t stream);
@@ -310,6 +312,14 @@ PYBIND11_MODULE(_dghip, m) {
   }, "conv_stack_f8_fwd_head + fp8 copy-out (y8 as conv_stack_f8_y8)");
   m.def("conv_stack_f8_set_mode", [](int m) { dg_conv_stack_f8_set_mode(m); },
         "conv_stack_f8 timing-ablation mode (0 = production)");
+  m.def("conv_stack_f8_set_debug", [](uintptr_t dbg) {
+    dg_conv_stack_f8_set_debug(P<unsigned long long>(dbg));
+  }, "conv_stack_f8 diagnostics: s_memtime phase stamps of boards 0..7 into dbg "
+     "([8][8 waves][24 layers][8] uint64; 0 = off; C = 128 production variants)");
+  m.def("conv_stack_f8_set_sched", [](int stag, int delay) {
+    dg_conv_stack_f8_set_sched(stag, delay);
+  }, "conv_stack_f8 (C = 128) schedule: staggered two-group on / off (overrides "
+     "DG_STACK_F8_STAG), co-half-1 start delay");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
         "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
   m.def("conv_stack2_set_sched", [](int stag, int prio, int delay) {

@@ -159,37 +159,7 @@ DG_DEV uint32_t pair_mask(uint32_t nib) {
   return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
 
-// Staggered two-group schedule (STAG): LDS counters instead of workgroup barriers.  A wave
-// counts itself in (+1 from one lane) once its LDS accesses are done (lgkmcnt(0)); waiters
-// poll with s_sleep between reads.  Both in inline asm: as C++ (a lane-0 branch, a polling
-// loop) the control flow inside the rolled K loop costs 100-160 spilled VGPRs.  (An asm
-// ds_add / ds_read outstanding ahead of the compiler's own LDS reads only lengthens its
-// in-order lgkmcnt waits.)
-DG_DEV void grp_signal(LDS_AS unsigned* c) {
-  unsigned long long sv;
-  asm volatile(
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "s_mov_b64 %0, exec\n\t"
-      "s_mov_b64 exec, 1\n\t"
-      "ds_add_u32 %1, %2\n\t"
-      "s_mov_b64 exec, %0"
-      : "=&s"(sv) : "v"((unsigned)(size_t)c), "v"(1u) : "memory");
-}
-DG_DEV void grp_wait(LDS_AS unsigned* c, unsigned target) {
-  unsigned v, sc;
-  asm volatile(
-      "1:\n\t"
-      "ds_read_b32 %0, %2\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_readfirstlane_b32 %1, %0\n\t"
-      "s_nop 4\n\t"
-      "s_cmp_ge_u32 %1, %3\n\t"
-      "s_cbranch_scc1 2f\n\t"
-      "s_sleep 1\n\t"
-      "s_branch 1b\n"
-      "2:"
-      : "=&v"(v), "=&s"(sc) : "v"((unsigned)(size_t)c), "s"(target) : "memory", "scc");
-}
+// (the staggered schedule's LDS counters: grp_signal / grp_wait, dg_common.h)
 
 // MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
 // 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop, 16 = no

@@ -45,6 +45,9 @@
 //
 // Reference ops: nn.SpatialConvolutionMM + nn.Add + nn.ReLU per hidden layer
 // (experiments.lua:137-147).
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "dg_common.h"
 #include "head_body.h"
 
@@ -74,7 +77,7 @@ constexpr int EPI_FWD = 1;
 constexpr int EPI_DGRAD = 2;
 constexpr int FP8P = 448;             // fp8 copy-out frames: rows per board
 
-static_assert(dghead::scratch_bytes(128) + 64 <= SCRATCH, "head scratch");
+static_assert(dghead::scratch_bytes(128) + 64 + 16 + 4 * 24 <= SCRATCH, "head scratch");
 
 // per-channel-count geometry
 template <int C>
@@ -116,6 +119,9 @@ struct F8Args {
   // EPI_DGRAD: stochastic rounding of the e5m2 gradient quantization (MODE bit 32), random
   // bits from a hash of (step counter, layer, element); null: round to nearest even
   const long long* sr_step;
+  int stag_delay;       // STAG: co-half-1 start delay (s_sleep 127 rounds; 0 in production)
+  unsigned long long* dbg;   // MODE bit 256 (diagnostics): s_memtime stamps of boards 0..7,
+                             // [board][wave][layer][8]
   F8Layer L[MAXL];
   dghead::HeadMArgs head;
 };
@@ -229,8 +235,9 @@ DG_DEV uint32_t nzbits4(uint32_t w) {
 // backward-data chain reads ReLU bits; backward-data: the weight gradient and the bias-gradient
 // partials read the e5m2 copies); the table's Y is null there.  MODE bit 32 (EPI_DGRAD):
 // stochastic rounding of the e5m2 quantization (pack_bf8x4_sr)
-template <int C, int EPI, int MODE>
+template <int C, int EPI, int MODE, bool STAG = false>
 __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
+  static_assert(!STAG || C == 128, "the staggered schedule needs the half-major K-steps");
   using G = Geo<C>;
   constexpr int NC = G::NC;
   constexpr int ROWB = G::ROWB;
@@ -245,7 +252,28 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   const int b = blockIdx.x;
   char* sI = smem + SCRATCH;                       // e4m3 image (C = 128 last layer: bf16)
   float* s_amax = (float*)(smem + G::AMAX_OFF);    // 2 x 8 floats (alternating per layer)
+  // STAG (C = 128): counters R0 R1 W0 W1 (conv_stack2.hip) and each layer's |y| max (float
+  // bits, ds_max per wave; folded into amax_out once at the end) below the wg_amax slots, in
+  // the head scratch (the head runs after the last of them is read)
+  LDS_AS unsigned* cnt = (LDS_AS unsigned*)(smem + SCRATCH - 64 - 16);
+  LDS_AS unsigned* s_lmax = (LDS_AS unsigned*)(smem + SCRATCH - 64 - 16 - 4 * MAXL);
+  if constexpr (STAG) {
+    if (tid < 4) cnt[tid] = 0u;
+    if (tid < MAXL) s_lmax[tid] = 0u;
+    const int wmu = __builtin_amdgcn_readfirstlane(wm);
+    if (wmu == 1)
+      for (int d = 0; d < a.stag_delay; ++d) __builtin_amdgcn_s_sleep(127);
+  }
 
+  // (MODE bit 256: per-wave s_memtime stamps of the layer phases, boards 0..7)
+  auto stamp = [&](int l, int k) {
+    if constexpr ((MODE & 256) != 0) {
+      if (b < 8) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (lane == 0) a.dbg[((b * NW + wave) * MAXL + l) * 8 + k] = t;
+      }
+    }
+  };
   // stochastic-rounding key base of this step (EPI_DGRAD, MODE bit 32)
   uint32_t sr_seed = 0;
   if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0)
@@ -280,16 +308,29 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
   const int lr = lane & 15;
   const int lq = lane >> 4;
-  // per fragment: row byte offset f*ROWB (20 bits) | v = (x + 3y) & 7 << 20
+  // per fragment: row byte offset f*ROWB (20 bits) | v = (x + 3y) & 7 << 20.  C = 128: the
+  // 23 pixel slots past the board (wave 3's last fragment) sit on dump rows 441..463 of the
+  // LDS past the e4m3 image (free until the last layer's bf16 image), so the lean epilogue
+  // stores them without a branch; C = 256 reads pixel 0 there
+  // (recomputed at every layer's start from an opaque lane index: kept live across the
+  // epilogue, the 6 words get spilled there and reloaded on its critical path)
   uint32_t pk[NF];
+  auto make_pk = [&]() {
+    int lro = lr;
+    asm volatile("" : "+v"(lro));
 #pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    int p = wn * NF * 16 + j * 16 + lr;
-    if (p >= NPTS) p = 0;
-    const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
-    const int f = (h + 1) * F + (w + 1);
-    pk[j] = (uint32_t)(f * ROWB) | ((uint32_t)fv(f) << 20);
-  }
+    for (int j = 0; j < NF; ++j) {
+      int p = wn * NF * 16 + j * 16 + lro;
+      int f;
+      if (p >= NPTS) {
+        f = C == 128 ? FF + (p - NPTS) : F + 1;
+      } else {
+        const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
+        f = (h + 1) * F + (w + 1);
+      }
+      pk[j] = (uint32_t)(f * ROWB) | ((uint32_t)fv(f) << 20);
+    }
+  };
   const uint32_t a_lane = (uint32_t)(wm * WM_BYTES + lane * 16);
 
   // A fragments i0, i0+1 of one K-step (A = the step's 16 KB): 2 KB per fragment
@@ -306,14 +347,26 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   // layout's [tap][chunk] order): lane group lq reads slots 8c + 2lq, 8c + 2lq + 1 (XOR the
   // row signature; the odd slot = even ^ 16 B)
   auto read_B = [&](int st, i32x8 (&bfr)[NF]) {
-    const int t = st / NC, c = st - (st / NC) * NC;
+    int t, slot0;
+    if constexpr (C == 128) {
+      // half-major K-steps: step st = units 2 st (lane groups 0, 1) and 2 st + 1 (2, 3) of
+      // n = 9 * half + tap (64 channels of one tap each): steps 0..3 read only channels 0..63
+      // (co-half 0's output), 5..8 only 64..127, step 4 both (the staggered schedule's order)
+      const int n = 2 * st + (lq >> 1);
+      const int hh = n >= T ? 1 : 0;
+      t = n - T * hh;
+      slot0 = 4 * hh + 2 * (lq & 1);
+    } else {
+      t = st / NC;
+      slot0 = 8 * (st - (st / NC) * NC) + 2 * lq;
+    }
     const int toff = (t / 3 - 1) * F + (t % 3 - 1);
     const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
     const LDS_AS char* base = (const LDS_AS char*)sI;
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int off = (int)(pk[j] & 0xFFFFFu) + toff * ROWB +
-                      (((8 * c + 2 * lq) ^ sig_of<C>((int)(pk[j] >> 20) + tsig)) * 16);
+                      ((slot0 ^ sig_of<C>((int)(pk[j] >> 20) + tsig)) * 16);
       const i32x4 lo = *(const LDS_AS i32x4*)(base + off);
       const i32x4 hi = *(const LDS_AS i32x4*)(base + (off ^ 16));
       bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -336,9 +389,22 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   // thread tid handles 16-B piece u = tid + 512 s (pixel u / SLOTS, channels 16 (u % SLOTS)),
   // read from LDS in the step before it is stored.  Pieces past the board repeat the last
   // one (same bytes): every wave issues the same stores.
+  // (C = 128: the waves of co-half wm copy out channels 64 wm .. 64 wm + 63 — the half they
+  // wrote themselves — 256 threads x 6 steps, as the staggered schedule requires)
+  auto co_pq = [&](int s_, int tq, int& p, int& q) {
+    if constexpr (C == 128) {
+      const int u = min((tq & 255) + 256 * s_, NPTS * 4 - 1);
+      p = u >> 2;
+      q = 4 * (tq >> 8) + (u & 3);
+    } else {
+      const int u = min(tq + NT * s_, G::PIECES - 1);
+      p = u / G::SLOTS;
+      q = u % G::SLOTS;
+    }
+  };
   auto co_read = [&](int s_) -> uint4 {
-    const int u = min(tid + NT * s_, G::PIECES - 1);
-    const int p = u / G::SLOTS, q = u % G::SLOTS;
+    int p, q;
+    co_pq(s_, tid, p, q);
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
     return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
@@ -351,8 +417,8 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     // out of the layer loop and spills them — reloaded with vmcnt(0) in every layer)
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    const int u = min(tq + NT * s_, G::PIECES - 1);
-    const int p = u / G::SLOTS, q = u % G::SLOTS;
+    int p, q;
+    co_pq(s_, tq, p, q);
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
     const int inner = f * C + q * 16;                  // element offset within the board
@@ -381,7 +447,9 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   load_A(a.L[0].A8, 0, Ak);
   load_A(a.L[0].A8, 2, Ak);
 
+  if constexpr (C != 128) make_pk();
   for (int l = 0; l < a.nl; ++l) {
+    if constexpr (C == 128) make_pk();
     const F8Layer L = a.L[l];
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
@@ -435,17 +503,56 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       // the copy-out steps (the first CO_STEPS of pass 0) and the rest as separate loops
       // (no per-step branch; the step index laundered so the compiler does not precompute
       // every step's copy-out addresses)
-      int st = 0;
-      if (!(MODE & 4) && co_on && hp == 0) {
+      if constexpr (C == 128) {
+        // half-major K-steps (read_B): 0..3 channels 0..63, 4 both halves, 5..8 channels
+        // 64..127.  Staggered schedule (STAG): no workgroup barrier between the layers of
+        // the run.  A wave reads image half c of a layer once co-half c has written it (W_c:
+        // 4 waves per layer); co-half g's waves write their output channels once all 8
+        // waves are past their reads of half g (R_g: 8 per layer; R0 after step 5, the last
+        // copy-out step).  Co-half 0 may run ahead of co-half 1, so each group's epilogue
+        // can overlap the other group's MFMAs instead of idling the pipes between two
+        // barriers (conv_stack2.hip).  The copy-out (steps 0..5) of each half is done by its
+        // own co-half: before its own next epilogue, once its own group has written it (W_wm).
+        stamp(l, 0);
+        if constexpr (STAG) {
+          grp_wait(cnt + 2, 4u * (unsigned)l);                        // W0
+          if (wm == 1) grp_wait(cnt + 3, 4u * (unsigned)l);           // W1 (own copy-out)
+        }
+        stamp(l, 1);
+        int st = 0;
+        if (!(MODE & 4) && co_on) {
 #pragma unroll 1
-        for (; st < G::CO_STEPS; ++st) {
+          for (; st < G::CO_STEPS; ++st) {
+            int tt = st;
+            asm volatile("" : "+s"(tt));
+            if constexpr (STAG) grp_wait_at(cnt + 3, 4u * (unsigned)l, tt, 4);   // W1
+            kstep(tt, tt, true);
+            if constexpr (STAG) grp_signal_at(cnt + 0, tt, 5);                   // R0
+          }
+        }
+#pragma unroll 1
+        for (; st < G::STEPS; ++st) {
           int tt = st;
           asm volatile("" : "+s"(tt));
-          kstep(tt, tt, true);
+          if constexpr (STAG) grp_wait_at(cnt + 3, 4u * (unsigned)l, tt, 4);     // W1
+          kstep(tt, 0, false);
+          if constexpr (STAG) grp_signal_at(cnt + 0, tt, 5);                     // R0
         }
-      }
+        if constexpr (STAG) grp_signal(cnt + 1);                    // R1
+        stamp(l, 2);
+      } else {
+        int st = 0;
+        if (!(MODE & 4) && co_on && hp == 0) {
 #pragma unroll 1
-      for (; st < G::STEPS; ++st) kstep(st, 0, false);
+          for (; st < G::CO_STEPS; ++st) {
+            int tt = st;
+            asm volatile("" : "+s"(tt));
+            kstep(tt, tt, true);
+          }
+        }
+#pragma unroll 1
+        for (; st < G::STEPS; ++st) kstep(st, 0, false);
+      }
 
       // ---- pass epilogue ----
       if constexpr ((MODE & 64) != 0) {
@@ -480,7 +587,15 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       // C = 128 and the last pass of C = 256: every wave is past its last read of the
       // image before it is overwritten (pass 0 of C = 256 only writes the park area)
       const bool to_image = !last && hp == NC - 1;
-      if (C == 128 || hp == NC - 1) lds_barrier();
+      if (STAG && !last)
+        grp_wait(cnt + wm, 8u * (unsigned)(l + 1));   // R_wm: every wave past its reads
+      else if (C == 128 || hp == NC - 1)
+        lds_barrier();
+      stamp(l, 3);
+      if constexpr ((MODE & 256) != 0) {   // (diagnostics: the epilogue's loads landed)
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+        stamp(l, 6);
+      }
       char* sIe = smem + SCRATCH + z0;
       if (BF16_LAST_IMAGE && last) {
         // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
@@ -497,6 +612,62 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0)
         sr_lane = sr_seed + (uint32_t)(l + 1) * 0x85EBCA6Bu +
                   (uint32_t)((b * NPTS + wn * NF * 16 + lr) * C + 128 * hp + wm * 64 + lq * 4);
+      if (C == 128 && !last) {
+        // Lean epilogue (C = 128, non-last layers): straight-line — no per-fragment branch
+        // (the pixels past the board store to the dump rows, a select keeps them out of the
+        // |y| max), one XOR per fragment for its LDS address, and per value: forward
+        // fma + ReLU max + scale + clamp; backward-data mask AND (v_bfe_i32 gives the lane
+        // mask) + scale + clamp, the |dz| max taken before the (power-of-two) dequantization.
+        // Same results as the general loop below: every scale is a power of two.
+        const float s1 = EPI == EPI_FWD ? inv_y : deq * inv_y;
+        float m_all = 0.f;
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          uint32_t pkj = pk[j];
+          asm volatile("" : "+v"(pkj));
+          // row + byte lq*4 + slot (wm*4 ^ sig) << 4; fragment i's slot is (wm*4 + i) ^ sig
+          const uint32_t a_j = ((pkj & 0xFFFFFu) + (uint32_t)(lq * 4)) |
+                               ((uint32_t)((wm * 4) ^ sig_of<C>((int)(pkj >> 20))) << 4);
+          uint32_t wx = 0, wy = 0;
+          if constexpr (EPI == EPI_DGRAD) {
+            wx = em[j].x >> (lq * 4);
+            wy = em[j].y >> (lq * 4);
+          }
+          float mj = 0.f;
+#pragma unroll
+          for (int i = 0; i < MF; ++i) {
+            const f32x4 v = acc[i][j];
+            float x[4];
+            if constexpr (EPI == EPI_FWD) {
+              const uint2 u = eb[j][i];
+              x[0] = fmaxf(fmaf(v[0], deq, __uint_as_float(u.x << 16)), 0.f);
+              x[1] = fmaxf(fmaf(v[1], deq, __uint_as_float(u.x & 0xFFFF0000u)), 0.f);
+              x[2] = fmaxf(fmaf(v[2], deq, __uint_as_float(u.y << 16)), 0.f);
+              x[3] = fmaxf(fmaf(v[3], deq, __uint_as_float(u.y & 0xFFFF0000u)), 0.f);
+              mj = fmaxf(mj, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[r] = fminf(x[r] * s1, QMAX);
+            } else {
+              const uint32_t w = (i < 2 ? wx : wy) >> ((i & 1) * 16);
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                x[r] = __uint_as_float(__float_as_uint(v[r]) &
+                                       (uint32_t)__builtin_amdgcn_sbfe((int)w, r, 1));
+              mj = fmaxf(mj, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])),
+                                   fmaxf(fabsf(x[2]), fabsf(x[3]))));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[r] = __builtin_amdgcn_fmed3f(x[r] * s1, -QMAX, QMAX);
+            }
+            const uint32_t key = sr_lane + (uint32_t)(j * 16 * C + i * 16);
+            const uint32_t q8 = pack8x4q<EPI, MODE>(x[0], x[1], x[2], x[3], key);
+            *(LDS_AS uint32_t*)((LDS_AS char*)sIe + (a_j ^ (uint32_t)(i << 4))) = q8;
+          }
+          m_all = fmaxf(m_all, wn * NF * 16 + j * 16 + lr < NPTS ? mj : 0.f);
+          __builtin_amdgcn_sched_barrier(0);   // (one fragment column at a time)
+        }
+        vmax = EPI == EPI_FWD ? m_all : m_all * deq;
+        stamp(l, 7);
+      } else
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int p = wn * NF * 16 + j * 16 + lr;
@@ -587,8 +758,24 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
         }
       }
     }
-    if (!last) wg_amax(vmax, L.amax_out, s_amax + 8 * (l & 1));  // (barrier inside)
-    lds_barrier();  // the next layer's input is complete
+    if (STAG && !last) {
+      grp_signal(cnt + 2 + wm);                                    // W_wm
+      const float m = wave_max(vmax);
+      if (lane == 0)
+        __hip_atomic_fetch_max(s_lmax + l, __float_as_uint(m), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      stamp(l, 4);
+    } else {
+      if (!last) wg_amax(vmax, L.amax_out, s_amax + 8 * (l & 1));  // (barrier inside)
+      stamp(l, 4);
+      lds_barrier();  // the next layer's input is complete
+      stamp(l, 5);
+    }
+  }
+  if constexpr (STAG) {
+    // every layer's |y| max (the last layer's barrier ordered every wave's ds_max before it)
+    if (tid < a.nl - 1) atomicMax(a.L[tid].amax_out, s_lmax[tid]);
+    __syncthreads();   // (the slots sit in the head scratch)
   }
   if constexpr (BF16_LAST_IMAGE) {
     // last layer's output (bf16 image): exposed copy-out + mask, as conv_stack2 (skipped with
@@ -628,17 +815,50 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
 int g_f8_mode = 0;
 
-template <int C, int EPI, int MODE>
-hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
+// the staggered schedule (C = 128): -1 = not yet read from DG_STACK_F8_STAG ("0" off, "1"
+// on, "1,DELAY"), else 0 / 1; co-half-1 start delay
+int g_f8_stag = -1, g_f8_delay = 0;
+void f8_sched_from_env() {
+  if (g_f8_stag >= 0) return;
+  const char* e = getenv("DG_STACK_F8_STAG");
+  g_f8_stag = 0;
+  if (e && *e) {
+    int v = 0, d = g_f8_delay;
+    const int n = sscanf(e, "%d,%d", &v, &d);
+    g_f8_stag = n >= 1 && v ? 1 : 0;
+    if (n >= 2) g_f8_delay = d;
+  }
+}
+
+template <int C, int EPI, int MODE, bool STAG>
+hipError_t launch_f8_s(const F8Args& a, int B, hipStream_t stream) {
   constexpr size_t lds = Geo<C>::LDS;
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<C, EPI, MODE>,
+    (void)hipFuncSetAttribute((const void*)conv_stack_f8_kernel<C, EPI, MODE, STAG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack_f8_kernel<C, EPI, MODE>), dim3(B), dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((conv_stack_f8_kernel<C, EPI, MODE, STAG>), dim3(B), dim3(NT), lds, stream,
+                     a);
   return hipGetLastError();
+}
+
+// (the timing ablations run the barrier schedule only)
+unsigned long long* g_f8_dbg = nullptr;   // MODE bit 256 stamps (diagnostics)
+
+template <int C, int EPI, int MODE>
+hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
+  if constexpr (C == 128 && (MODE & (2 | 4 | 64 | 128)) == 0) {
+    if constexpr (MODE == 24 || MODE == 56) {
+      if (g_f8_dbg) {
+        return g_f8_stag == 1 ? launch_f8_s<C, EPI, MODE | 256, true>(a, B, stream)
+                              : launch_f8_s<C, EPI, MODE | 256, false>(a, B, stream);
+      }
+    }
+    if (g_f8_stag == 1) return launch_f8_s<C, EPI, MODE, true>(a, B, stream);
+  }
+  return launch_f8_s<C, EPI, MODE, false>(a, B, stream);
 }
 
 template <int C>
@@ -697,6 +917,9 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
   if (head && epi != EPI_FWD) return hipErrorInvalidValue;
   if (sr_step && epi != EPI_DGRAD) return hipErrorInvalidValue;
   F8Args a;
+  f8_sched_from_env();
+  a.stag_delay = g_f8_delay;
+  a.dbg = g_f8_dbg;
   a.sr_step = sr_step;
   a.X0 = (const char*)X0;
   a.s_x0 = s_x0;
@@ -736,6 +959,15 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
 extern "C" {
 
 void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
+
+// the staggered schedule of C = 128 (overrides DG_STACK_F8_STAG): on 0 / 1, co-half-1 start
+// delay (s_sleep 127 rounds)
+void dg_conv_stack_f8_set_debug(unsigned long long* dbg) { g_f8_dbg = dbg; }
+
+void dg_conv_stack_f8_set_sched(int stag, int delay) {
+  g_f8_stag = stag ? 1 : 0;
+  g_f8_delay = delay;
+}
 
 // table: nl rows of {A8 (fragment-ordered e4m3 weights), pbias_frag, Y, mask, s_in, s_w,
 // s_out, amax_out} (int64); epi 1 forward, 2 backward-data; sr_step (backward-data): the

@@ -59,6 +59,75 @@ DG_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 
 DG_DEV bf16x8 lds_read_b128(const LDS_AS char* p) { return *(const LDS_AS bf16x8*)p; }
 
+// Staggered two-group schedules of the board-resident stacks (conv_stack2 / conv_stack_f8
+// STAG): LDS counters instead of workgroup barriers.  A wave
+// counts itself in (+1 from one lane) once its LDS accesses are done (lgkmcnt(0)); waiters
+// poll with s_sleep between reads.  Both in inline asm: as C++ (a lane-0 branch, a polling
+// loop) the control flow inside the rolled K loop costs 100-160 spilled VGPRs.  (An asm
+// ds_add / ds_read outstanding ahead of the compiler's own LDS reads only lengthens its
+// in-order lgkmcnt waits.)
+DG_DEV void grp_signal(LDS_AS unsigned* c) {
+  unsigned long long sv;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %1, %2\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv) : "v"((unsigned)(size_t)c), "v"(1u) : "memory");
+}
+DG_DEV void grp_wait(LDS_AS unsigned* c, unsigned target) {
+  unsigned v, sc;
+  asm volatile(
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_nop 4\n\t"
+      "s_cmp_ge_u32 %1, %3\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : "=&v"(v), "=&s"(sc) : "v"((unsigned)(size_t)c), "s"(target) : "memory", "scc");
+}
+// The same only when the (wave-uniform, SGPR) step index st equals at: the test is inside the
+// asm, so a rolled K loop keeps straight-line code (a C++ branch around the asm there costs
+// ~30-40 spilled VGPRs)
+DG_DEV void grp_signal_at(LDS_AS unsigned* c, int st, int at) {
+  unsigned long long sv;
+  asm volatile(
+      "s_cmp_eq_u32 %3, %4\n\t"
+      "s_cbranch_scc0 3f\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %1, %2\n\t"
+      "s_mov_b64 exec, %0\n"
+      "3:"
+      : "=&s"(sv) : "v"((unsigned)(size_t)c), "v"(1u), "s"(st), "s"(at) : "memory", "scc");
+}
+DG_DEV void grp_wait_at(LDS_AS unsigned* c, unsigned target, int st, int at) {
+  unsigned v, sc;
+  asm volatile(
+      "s_cmp_eq_u32 %4, %5\n\t"
+      "s_cbranch_scc0 2f\n"
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_nop 4\n\t"
+      "s_cmp_ge_u32 %1, %3\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : "=&v"(v), "=&s"(sc)
+      : "v"((unsigned)(size_t)c), "s"(target), "s"(st), "s"(at)
+      : "memory", "scc");
+}
+
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies &row q, cols 4p..4p+3;
 // lane i receives column i of the 4 rows (row q in element q).
 DG_DEV s16x4 lds_read_tr(const LDS_AS char* p) {

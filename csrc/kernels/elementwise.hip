@@ -547,6 +547,21 @@ DG_DEV bool refresh_needs_tile(const WRefreshLayer& L) {
   return L.wd || L.wf_frag || L.wd_frag || L.wf8_frag || L.wd8_frag;
 }
 
+// conv_stack_f8's K-step of (tap t, 128-channel chunk c, 64-channel half kh) and the first of
+// the two lane groups holding it: C = 128 (nc = 1) runs half-major steps — unit n = 9 kh + t
+// is step n / 2, lane groups 2 (n % 2), +1 (conv_stack_f8.hip read_B); C = 256 steps are
+// (tap, chunk) with the half in lane groups 2 kh, +1
+DG_DEV void f8_step_of(int nc, int t, int c, int kh, int& st, int& lg) {
+  if (nc == 1) {
+    const int n = 9 * kh + t;
+    st = n >> 1;
+    lg = 2 * (n & 1);
+  } else {
+    st = t * nc + c;
+    lg = 2 * kh;
+  }
+}
+
 // The whole-tile operand copies of tile (t, cot, cit) from tileS[co - 64 cot][ci - 64 cit]
 // (fp32 weights, written and made visible by the caller): the transposed / flipped dgrad
 // operand and the MFMA fragment orders of the stacks.  Ends with a barrier.
@@ -624,8 +639,10 @@ DG_DEV void refresh_tile_copies(const WRefreshLayer& L, int t, int cot, int cit,
         q[e] = (uint32_t)pkd;
       }
       const int nc = L.cout / 128, h = cot >> 1, wm = cot & 1, c = cit >> 1;
-      const int lane = (2 * (cit & 1) + lql) * 16 + lr;
-      L.wf8_frag[((((((size_t)h * 9 + t) * nc + c) * 2 + wm) * 4 + i) * 2 + hf) * 64 + lane] =
+      int st, lg;
+      f8_step_of(nc, t, c, cit & 1, st, lg);
+      const int lane = (lg + lql) * 16 + lr;
+      L.wf8_frag[(((((size_t)h * 9 * nc + st) * 2 + wm) * 4 + i) * 2 + hf) * 64 + lane] =
           uint4{q[0], q[1], q[2], q[3]};
     }
     if (L.wd8_frag) {
@@ -646,9 +663,11 @@ DG_DEV void refresh_tile_copies(const WRefreshLayer& L, int t, int cot, int cit,
         q[e] = (uint32_t)pkd;
       }
       const int nc = L.cout / 128, h = cit >> 1, wm = cit & 1, c = cot >> 1;
-      const int lane = (2 * (cot & 1) + lql) * 16 + lr;
-      L.wd8_frag[((((((size_t)h * 9 + (8 - t)) * nc + c) * 2 + wm) * 4 + i) * 2 + hf) * 64 +
-                 lane] = uint4{q[0], q[1], q[2], q[3]};
+      int st, lg;
+      f8_step_of(nc, 8 - t, c, cot & 1, st, lg);
+      const int lane = (lg + lql) * 16 + lr;
+      L.wd8_frag[(((((size_t)h * 9 * nc + st) * 2 + wm) * 4 + i) * 2 + hf) * 64 + lane] =
+          uint4{q[0], q[1], q[2], q[3]};
     }
     __syncthreads();
 }

@@ -100,11 +100,21 @@ def stack_pbias_frag(bias: torch.Tensor, posb: torch.Tensor) -> torch.Tensor:
 
 def stack_frag_f8(w8: torch.Tensor) -> torch.Tensor:
     """conv_stack_f8 A-operand order of e4m3 forward weights ``w8`` [C co][9 taps][C ci]
-    (uint8 bytes, C = 128 | 256): flat [h C/128][tap 9][c C/128][wm 2][i 4][half 2][lane 64]
-    [e 16] with co = 128h + wm*64 + i*16 + (lane & 15), ci = 128c + 32*(lane >> 4) + 16*half
-    + e (the MX-MFMA lane group g holds k = 32g .. 32g + 31; h = output pass, c = K chunk)."""
+    (uint8 bytes, C = 128 | 256).
+    C = 256: flat [h 2][tap 9][c 2][wm 2][i 4][half 2][lane 64][e 16] with co = 128h + wm*64 +
+    i*16 + (lane & 15), ci = 128c + 32*(lane >> 4) + 16*half + e (the MX-MFMA lane group g
+    holds k = 32g .. 32g + 31; h = output pass, c = K chunk).
+    C = 128 (half-major K-steps, the staggered schedule's order): unit n = 9*kh + tap (64
+    channels kh of one tap) is K-step n // 2 in lane groups 2*(n % 2), +1: flat [st 9][wm 2]
+    [i 4][half 2][lane 64][e 16] with lane group g = 2p + q holding unit 2*st + p, ci = 64*kh +
+    32*q + 16*half + e."""
     C = w8.shape[0]
     assert C in (128, 256) and tuple(w8.shape) == (C, 9, C)
+    if C == 128:
+        a = w8.reshape(128, 9, 2, 2, 2, 16)                 # co | tap | kh q half e
+        a = a.permute(0, 2, 1, 3, 4, 5).reshape(128, 18, 2, 2, 16)   # co | n = 9kh+tap | q..
+        a = a.reshape(2, 4, 16, 9, 2, 2, 2, 16)             # wm i lr | st p | q half e
+        return a.permute(3, 0, 1, 6, 4, 5, 2, 7).reshape(-1).contiguous()
     n = C // 128
     a = w8.reshape(n, 2, 4, 16, 9, n, 4, 2, 16)         # h wm i lr | tap | c lq half e
     return a.permute(0, 4, 5, 1, 2, 7, 6, 3, 8).reshape(-1).contiguous()

@@ -236,12 +236,18 @@ def test_stack_frag_f8_layout_indexing():
     w = torch.arange(128 * 9 * 128, dtype=torch.int64).reshape(128, 9, 128)
     f = LY.stack_frag_f8(w)
     rng = np.random.default_rng(1)
+    # 128 channels: half-major K-steps [st][wm][i][half][lane][e]: lane group g = 2p + q holds
+    # unit n = 2 st + p = 9 kh + tap, channels 64 kh + 32 q + 16 half + e
     for _ in range(200):
-        t, wm, i, half, lane, e = (int(rng.integers(n)) for n in (9, 2, 4, 2, 64, 16))
+        st, wm, i, half, lane, e = (int(rng.integers(n)) for n in (9, 2, 4, 2, 64, 16))
+        g = lane >> 4
+        kh, t = divmod(2 * st + (g >> 1), 9)
         co = wm * 64 + i * 16 + (lane & 15)
-        ci = 32 * (lane >> 4) + 16 * half + e
-        idx = ((((t * 2 + wm) * 4 + i) * 2 + half) * 64 + lane) * 16 + e
+        ci = 64 * kh + 32 * (g & 1) + 16 * half + e
+        idx = ((((st * 2 + wm) * 4 + i) * 2 + half) * 64 + lane) * 16 + e
         assert f[idx].item() == w[co, t, ci].item()
+    # every (co, tap, ci) exactly once
+    assert torch.equal(torch.sort(f).values, torch.arange(128 * 9 * 128))
     # 256 channels: [h][tap][c][wm][i][half][lane][e]
     w = torch.arange(256 * 9 * 256, dtype=torch.int64).reshape(256, 9, 256)
     f = LY.stack_frag_f8(w)
