@@ -40,6 +40,7 @@ hipError_t dg_conv_stack_f8(int C, int epi, const long long* table, int nl, cons
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, long long* sf, hipStream_t stream);
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
+void dg_conv_wgrad_win8_set_ablate(int mode);
 hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
@@ -274,6 +275,9 @@ PYBIND11_MODULE(_dghip, m) {
   }, "the e5m2 backward-data stack (conv_stack_f8 epi 2) with optional fp8 copies (y8, 0: "
      "none) and stochastic rounding seeded by the int64 device step counter sr_step (0: "
      "round to nearest even)");
+  m.def("conv_wgrad_win8_set_ablate", [](int mode) { dg_conv_wgrad_win8_set_ablate(mode); },
+        "conv_wgrad_win8 timing ablation (tools/kbench_win8.py; 0 = production): 1 no MFMA, "
+        "2 no LDS reads, 4 no LDS-DMA, 8 no slab store, 16 no barrier (sums of these)");
   m.def("conv_wgrad_win8", [](uintptr_t table, int nl, int M, int Mpad, int Cx, int B, int KP,
                               int splits, uintptr_t sf, uintptr_t stream) {
     check(dg_conv_wgrad_win8(P<long long>(table), nl, M, Mpad, Cx, B, KP, splits,
@@ -319,7 +323,7 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_stack_f8_set_sched", [](int stag, int delay) {
     dg_conv_stack_f8_set_sched(stag, delay);
   }, "conv_stack_f8 (C = 128) schedule: staggered two-group on / off (overrides "
-     "DG_STACK_F8_STAG), co-half-1 start delay");
+     "DG_STACK_F8_STAG; 0 off, 1 both stacks, 2 backward-data only), co-half-1 start delay");
   m.def("conv_stack2_set_mode", [](int on) { dg_conv_stack2_set_mode(on); },
         "conv_stack2 timing-ablation mode (tools/kbench_stack.py; 0 = production)");
   m.def("conv_stack2_set_sched", [](int stag, int prio, int delay) {

@@ -120,6 +120,7 @@ struct F8Args {
   // bits from a hash of (step counter, layer, element); null: round to nearest even
   const long long* sr_step;
   int stag_delay;       // STAG: co-half-1 start delay (s_sleep 127 rounds; 0 in production)
+  int stag_on;          // (host) this launch runs the staggered schedule
   unsigned long long* dbg;   // MODE bit 256 (diagnostics): s_memtime stamps of boards 0..7,
                              // [board][wave][layer][8]
   F8Layer L[MAXL];
@@ -592,10 +593,6 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       else if (C == 128 || hp == NC - 1)
         lds_barrier();
       stamp(l, 3);
-      if constexpr ((MODE & 256) != 0) {   // (diagnostics: the epilogue's loads landed)
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-        stamp(l, 6);
-      }
       char* sIe = smem + SCRATCH + z0;
       if (BF16_LAST_IMAGE && last) {
         // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
@@ -666,7 +663,6 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
           __builtin_amdgcn_sched_barrier(0);   // (one fragment column at a time)
         }
         vmax = EPI == EPI_FWD ? m_all : m_all * deq;
-        stamp(l, 7);
       } else
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
@@ -815,17 +811,19 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
 int g_f8_mode = 0;
 
-// the staggered schedule (C = 128): -1 = not yet read from DG_STACK_F8_STAG ("0" off, "1"
-// on, "1,DELAY"), else 0 / 1; co-half-1 start delay
+// The staggered schedule (C = 128): -1 = not yet read from DG_STACK_F8_STAG ("MODE[,DELAY]"),
+// else 0 off, 1 both stacks, 2 the backward-data stack only (default: 12x128 kernel bench and
+// step A/B, profiles/r5_stack_f8_stag.txt — the forward gains nothing: its co-half 0 waits
+// for co-half 1 either way); co-half-1 start delay
 int g_f8_stag = -1, g_f8_delay = 0;
 void f8_sched_from_env() {
   if (g_f8_stag >= 0) return;
   const char* e = getenv("DG_STACK_F8_STAG");
-  g_f8_stag = 0;
+  g_f8_stag = 2;
   if (e && *e) {
     int v = 0, d = g_f8_delay;
     const int n = sscanf(e, "%d,%d", &v, &d);
-    g_f8_stag = n >= 1 && v ? 1 : 0;
+    g_f8_stag = n >= 1 && v >= 0 && v <= 2 ? v : 2;
     if (n >= 2) g_f8_delay = d;
   }
 }
@@ -852,11 +850,11 @@ hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
   if constexpr (C == 128 && (MODE & (2 | 4 | 64 | 128)) == 0) {
     if constexpr (MODE == 24 || MODE == 56) {
       if (g_f8_dbg) {
-        return g_f8_stag == 1 ? launch_f8_s<C, EPI, MODE | 256, true>(a, B, stream)
-                              : launch_f8_s<C, EPI, MODE | 256, false>(a, B, stream);
+        return a.stag_on ? launch_f8_s<C, EPI, MODE | 256, true>(a, B, stream)
+                         : launch_f8_s<C, EPI, MODE | 256, false>(a, B, stream);
       }
     }
-    if (g_f8_stag == 1) return launch_f8_s<C, EPI, MODE, true>(a, B, stream);
+    if (a.stag_on) return launch_f8_s<C, EPI, MODE, true>(a, B, stream);
   }
   return launch_f8_s<C, EPI, MODE, false>(a, B, stream);
 }
@@ -919,6 +917,7 @@ hipError_t f8_launch(int C, int epi, const long long* table, int nl, const void*
   F8Args a;
   f8_sched_from_env();
   a.stag_delay = g_f8_delay;
+  a.stag_on = C == 128 && (g_f8_stag == 1 || (g_f8_stag == 2 && epi == EPI_DGRAD)) ? 1 : 0;
   a.dbg = g_f8_dbg;
   a.sr_step = sr_step;
   a.X0 = (const char*)X0;
@@ -960,12 +959,12 @@ extern "C" {
 
 void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 
-// the staggered schedule of C = 128 (overrides DG_STACK_F8_STAG): on 0 / 1, co-half-1 start
-// delay (s_sleep 127 rounds)
+// the staggered schedule of C = 128 (overrides DG_STACK_F8_STAG): 0 off, 1 both stacks, 2
+// backward-data only; co-half-1 start delay (s_sleep 127 rounds)
 void dg_conv_stack_f8_set_debug(unsigned long long* dbg) { g_f8_dbg = dbg; }
 
 void dg_conv_stack_f8_set_sched(int stag, int delay) {
-  g_f8_stag = stag ? 1 : 0;
+  g_f8_stag = stag >= 0 && stag <= 2 ? stag : 2;
   g_f8_delay = delay;
 }
 

@@ -97,7 +97,10 @@ DG_DEV i32x2 tr8(const LDS_AS char* p) {
 // the DMA schedule (20 1-KB blocks per super-step: 8 dZ + 12 X) are the same.
 // RA: B (X) fragments read RA taps ahead of their MFMAs (each tap's 4 tr8 reads then have
 // RA x MI MFMAs to land)
-template <int NW, int RA, int PD>
+// MODE: 0 in production; timing ablations (tools/kbench_win8.py, wrong results): 1 no MFMA,
+// 2 no LDS fragment reads (register operands), 4 no LDS-DMA (nothing issued or waited for),
+// 8 no slab store, 16 no per-super-step barrier
+template <int NW, int RA, int PD, int MODE = 0>
 __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Args a, Win8Layers Ls) {
   static_assert(PD >= 2 && PD <= PD_MAX, "prefetch distance");
   constexpr int MI = 16 / NW;            // 16-co accumulator fragments per wave (4 | 2)
@@ -204,7 +207,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
 #pragma unroll
   for (int t = 0; t < 9; ++t) rel[t] = rel_of(t);
 
-  if (s0 < s1) {
+  if (s0 < s1 && !(MODE & 4)) {
     const int lo = (sub_g0(4 * s0) - 22) & ~15;
     loaded_hi = (sub_g0(4 * s0 + 3) + 54 + 15) & ~15;
     for (int k = wave; k < ((loaded_hi - lo) >> 4); k += NW) x_block(lo + 16 * k);
@@ -217,7 +220,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   }
 
   for (int S = s0; S < s1; ++S) {
-    if (S + PD < s1) issue(S + PD, (S + PD) % (PD + 1));
+    if (!(MODE & 4) && S + PD < s1) issue(S + PD, (S + PD) % (PD + 1));
     int so[4];                             // wave-uniform ring byte offsets per sub-step
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -232,8 +235,18 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = tr8(sD + (a_off ^ (16 * ig)) + r * 2048);
       af[i] = i32x8{v[0].x, v[0].y, v[1].x, v[1].y, v[2].x, v[2].y, v[3].x, v[3].y};
+      if constexpr ((MODE & 2) != 0) {
+        int z = lane + ig;
+        asm volatile("" : "+v"(z));
+        af[i] = i32x8{z, z, z, z, z, z, z, z};
+      }
     }
     auto read_b = [&](int t) -> i32x8 {
+      if constexpr ((MODE & 2) != 0) {
+        int z = lane + t;
+        asm volatile("" : "+v"(z));
+        return i32x8{z, z, z, z, z, z, z, z};
+      }
       i32x2 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -250,14 +263,18 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
       if (t + RA < 9) bb[t + RA] = read_b(t + RA);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        acc[i][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bb[t], acc[i][t],
-                                                                     1, 0, 0, 127, 0, 127);
+      for (int i = 0; i < MI; ++i) {
+        if constexpr ((MODE & 1) != 0)
+          asm volatile("" ::"v"(af[i]), "v"(bb[t]));
+        else
+          acc[i][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bb[t], acc[i][t],
+                                                                       1, 0, 0, 127, 0, 127);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     // this wave's DMAs of super-step S + 1 landed (those of S + 2 .. S + PD may remain),
     // then every wave's (barrier): the next super-step's rows are visible and S's free
-    {
+    if constexpr (!(MODE & 4)) {
       // in flight beyond S + 1: super-steps S + 2 .. min(S + PD, s1 - 1)
       const int ahead = min(PD - 1, s1 - S - 2);
       if (ahead >= PD - 1)
@@ -269,11 +286,15 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
       else
         dma_wait<0>();
     }
-    __syncthreads();
+    if constexpr (!(MODE & 16)) __syncthreads();
   }
 
   const float scale = *Ls.s_dz[layer] * *Ls.s_x[layer];
   float* slab = Ls.slab[layer] + (size_t)zsplit * a.Mpad * a.KP;
+  // the step tag's range check on the stored values themselves: an unsigned max of their |v|
+  // bits (NaN bits exceed every finite and infinite value) — checked after the stores, the
+  // accumulators stayed live past them (181 -> 212 VGPRs)
+  unsigned vmx = 0u;
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -282,23 +303,21 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int k = t * a.Cx + cich * 64 + wn * 16 + li;
-        slab[(size_t)co * a.KP + k] = acc[i][t][r] * scale;
+        const float v = acc[i][t][r] * scale;
+        if constexpr ((MODE & 8) != 0)
+          asm volatile("" ::"v"(v));
+        else
+          slab[(size_t)co * a.KP + k] = v;
+        vmx = max(vmx, __float_as_uint(v) & 0x7FFFFFFFu);
       }
     }
   }
-  if (a.sf) {
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bad |= grad_out_of_range(acc[i][t][r] * scale);
-    if (bad) flag_bad_step(a.sf);
-  }
+  if (a.sf && vmx >= __float_as_uint(GRAD_BOUND)) flag_bad_step(a.sf);
 }
 
 }  // namespace
+
+int g_win8_ablate = 0;
 
 extern "C" {
 
@@ -350,8 +369,17 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   // (B reads 2 taps ahead measured the same as 1: profiles/r4_s1_fused_update_and_fp8_bisection.txt)
   // prefetch distance 3: 4 measured equal (12x256 fp8 133.7k vs 133.9k,
   // profiles/r4_s2_sr_hash_win8_pd_ab.txt)
-  hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3>), grid, dim3(512), 0, stream, a, Ls);
+  switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
+#define DG_W8(m) \
+  case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, m>), grid, dim3(512), 0, stream, a, Ls); break;
+    DG_W8(1) DG_W8(2) DG_W8(3) DG_W8(4) DG_W8(6) DG_W8(7) DG_W8(8) DG_W8(16) DG_W8(20) DG_W8(31)
+#undef DG_W8
+    default:
+      hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3>), grid, dim3(512), 0, stream, a, Ls);
+  }
   return hipGetLastError();
 }
+
+void dg_conv_wgrad_win8_set_ablate(int mode) { g_win8_ablate = mode; }
 
 }  // extern "C"

@@ -149,7 +149,7 @@ def fp8_stag(h, B, NL, s, rounds, timeline=False):
                 torch.cuda.synchronize()
                 h.conv_stack_f8_set_debug(0)
                 out[f"{name}_stag{stag}"] = summarize(dbg.view(8, 8, 24, 8).cpu().numpy(), NL)
-        h.conv_stack_f8_set_sched(0, 0)
+        h.conv_stack_f8_set_sched(2, 0)
         return out
     for fwd, name in ((True, "fwd"), (False, "dgrad")):
         outs = []
@@ -166,7 +166,7 @@ def fp8_stag(h, B, NL, s, rounds, timeline=False):
             times.setdefault(f"{name}_barrier", []).append(timeit(run(fwd, 0)))
             times.setdefault(f"{name}_stag", []).append(timeit(run(fwd, 1)))
             times.setdefault(f"{name}_stag_delay1", []).append(timeit(run(fwd, 1, 1)))
-    h.conv_stack_f8_set_sched(0, 0)
+    h.conv_stack_f8_set_sched(2, 0)
     out["us"] = {k: round(min(v), 1) for k, v in times.items()}
     return out
 
@@ -174,9 +174,8 @@ def fp8_stag(h, B, NL, s, rounds, timeline=False):
 def summarize(t, NL):
     """Phase lengths (cycles, mean over boards 0..7 and layers 1..NL-2) per co-half from the
     stamps [board][wave][layer][k]: k 0 layer top, 1 after the input waits, 2 K loop end,
-    3 after the epilogue's wait (R or barrier), 6 the epilogue's loads landed (vmcnt(0)), 7
-    fragments written, 4 epilogue end (+ amax), 5 after the barrier schedule's closing
-    barrier; and the co-half-1 lag (its layer top minus co-half 0's)."""
+    3 after the epilogue's wait (R or barrier), 4 epilogue end (+ amax), 5 after the barrier
+    schedule's closing barrier; and the co-half-1 lag (its layer top minus co-half 0's)."""
     t = t.astype(np.int64)
     ls = slice(1, NL - 1)
     out = {}
@@ -188,9 +187,6 @@ def summarize(t, NL):
             "kloop": float(np.mean(w[..., 2] - w[..., 1])),
             "epi_wait": float(np.mean(w[..., 3] - w[..., 2])),
             "epi": float(np.mean(w[..., 4] - w[..., 3])),
-            "epi_loads": float(np.mean(w[..., 6] - w[..., 3])),
-            "epi_frags": float(np.mean(w[..., 7] - w[..., 6])),
-            "epi_tail": float(np.mean(w[..., 4] - w[..., 7])),
             "layer": float(np.mean(nxt - w[..., 0])),
         }
     out["g1_lag"] = float(np.mean(t[:, 4:8, ls, 0] - t[:, 0:4, ls, 0]))
