@@ -45,6 +45,7 @@
 //
 // Reference semantics: SpatialConvolutionMM accGradParameters of the hidden 3x3 layers
 // (experiments.lua:135-149, EXTERNAL nn; the backward of train.lua:10).
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "dg_common.h"
@@ -61,7 +62,6 @@ constexpr int FP = 448;           // fp8 frame pitch: rows per board (441 + 7 ze
 constexpr int SPB = 13;           // 32-row sub-steps per board (rows 21 .. 436)
 constexpr int XR = 1024;          // X ring rows (64 B each)
 constexpr int XRING = XR * 64;    // 64 KB
-constexpr int DZB = 128 * 64;     // one super-step of dZ rows: 8 KB
 constexpr int PD_MAX = 4;         // DMA distance (super-steps): PD - 1 in flight beyond the next
 constexpr int MAXL = 16;
 // ring capacity at prefetch distance PD (see the header): PD + 1 super-steps of at most
@@ -99,14 +99,25 @@ DG_DEV i32x2 tr8(const LDS_AS char* p) {
 // RA x MI MFMAs to land)
 // MODE: 0 in production; timing ablations (tools/kbench_win8.py, wrong results): 1 no MFMA,
 // 2 no LDS fragment reads (register operands), 4 no LDS-DMA (nothing issued or waited for),
-// 8 no slab store, 16 no per-super-step barrier
-template <int NW, int RA, int PD, int MODE = 0>
+// 8 no slab store, 16 no per-super-step barrier.
+// COT: the workgroup's co tile, 64 or 128.  128 (MI = 4 fragments per wave at NW = 8): the
+// X slice (64 ci) of a (layer, split) is streamed by one workgroup instead of two (C = 128;
+// 2 instead of 4 at C = 256) and a wave reads 52 tr8 fragments per 36 MFMAs instead of 44
+// per 18 (tools/kbench_win8.py ablations: the 64-co kernel is DMA- and LDS-bound, not MFMA-
+// bound); dZ rows of 128 B in LDS, 16-B chunk c at c ^ ((R >> 1) & 7) (any 16 consecutive
+// rows: 16 distinct (bank half, chunk) pairs for the tr8 reads).
+template <int NW, int RA, int PD, int MODE = 0, int COT = 64>
 __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Args a, Win8Layers Ls) {
   static_assert(PD >= 2 && PD <= PD_MAX, "prefetch distance");
-  constexpr int MI = 16 / NW;            // 16-co accumulator fragments per wave (4 | 2)
+  static_assert(COT == 64 || COT == 128, "co tile");
+  constexpr int MI = COT / 16 / (NW / 4);   // 16-co accumulator fragments per wave
   constexpr int XPW = NW == 4 ? 3 : 2;   // X blocks per wave per super-step (12 | 16 >= 11)
-  constexpr int DPW = 8 / NW;            // dZ blocks per wave per super-step (2 | 1)
-  constexpr int PER = XPW + DPW;         // DMAs per wave per super-step (5 | 3)
+  constexpr int DZB = 128 * COT;         // one super-step of dZ rows (8 | 16 KB)
+  constexpr int DPW = COT / 8 / NW;      // dZ blocks (1 KB) per wave per super-step
+  constexpr int PER = XPW + DPW;         // DMAs per wave per super-step
+  constexpr int RPB = 1024 / COT;        // dZ rows per 1-KB block (16 | 8)
+  constexpr int LPR = COT / 16;          // lanes per dZ row (4 | 8)
+  static_assert(DPW * NW * RPB == 128, "dZ blocks");
   __shared__ __attribute__((aligned(16))) char smem[XRING + (PD + 1) * DZB];
   char* xring = smem;
   char* dzbuf = smem + XRING;
@@ -119,7 +130,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   const int wn = wave & 3;               // ci quarter (16 ci)
   const int wm = wave >> 2;              // co half (NW = 8)
 
-  const int nci = a.Cx / 64, nco = a.M / 64;
+  const int nci = a.Cx / 64, nco = a.M / COT;
   const int nwg = a.nl * nco * nci * a.splits;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, xslot = bid >> 3;
@@ -132,7 +143,9 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   const int zsplit = rest % a.splits;
   const int layer = rest / a.splits;
 
-  const uint8_t* __restrict__ dZl = Ls.dZ[layer] + coch * 64;
+  const uint8_t* __restrict__ dZl = Ls.dZ[layer] + coch * COT;
+  // dZ ring-row swizzle (chunk c of buffer row R at c ^ dz_swz(R))
+  auto dz_swz = [](int R) { return COT == 64 ? (R >> 2) & 3 : (R >> 1) & 7; };
   const uint8_t* __restrict__ Xl = Ls.X[layer] + cich * 64;
   const int Gmax = a.B * FP;
   const int TS = a.B * SPB / 4;                         // super-steps
@@ -149,15 +162,17 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
     dma16(Xl + (size_t)gr * a.Cx + c * 16,
           __builtin_amdgcn_readfirstlane(xring_u + (r0 & (XR - 1)) * 64));
   };
-  // dZ rows of super-step S into buffer buf: 8 blocks of 16 rows (DPW per wave)
+  // dZ rows of super-step S into buffer buf: 128 / RPB blocks of RPB rows (DPW per wave)
   auto dz_blocks = [&](int buf, int S) {
 #pragma unroll
     for (int u = 0; u < DPW; ++u) {
-      const int k = wave + NW * u;            // block: sub-step k / 2, rows 16 (k & 1) ..
-      const int r = k >> 1;
-      const int R = 32 * r + 16 * (k & 1) + (lane >> 2);   // buffer row
-      const int c = (lane & 3) ^ swz(R);
-      const int g = sub_g0(4 * S + r) + 16 * (k & 1) + (lane >> 2);
+      const int k = wave + NW * u;            // block: sub-step r, rows rr ..
+      constexpr int BPS = 32 / RPB;           // blocks per 32-row sub-step
+      const int r = k / BPS;
+      const int rr = RPB * (k % BPS) + lane / LPR;
+      const int R = 32 * r + rr;              // buffer row
+      const int c = (lane % LPR) ^ dz_swz(R);
+      const int g = sub_g0(4 * S + r) + rr;
       dma16(dZl + (size_t)g * a.M + c * 16,
             __builtin_amdgcn_readfirstlane(dz_u + buf * DZB + k * 1024));
     }
@@ -193,7 +208,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   int a_off;
   {
     const int R0 = 8 * g + q;
-    a_off = R0 * 64 + (swz(R0) * 16) + 8 * p;
+    a_off = R0 * COT + (dz_swz(R0) * 16) + 8 * p;
   }
   // B (X) read offsets: ring slot of row 21 + off_t + 8 g + q (board 0, sub-step 0); a
   // sub-step starting at row g0 adds (g0 - 21) rows (a multiple of 32: swizzle unchanged)
@@ -233,7 +248,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
       const int ig = wm * MI + i;          // the 16-co chunk of the 64-co tile
       i32x2 v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = tr8(sD + (a_off ^ (16 * ig)) + r * 2048);
+      for (int r = 0; r < 4; ++r) v[r] = tr8(sD + (a_off ^ (16 * ig)) + r * 32 * COT);
       af[i] = i32x8{v[0].x, v[0].y, v[1].x, v[1].y, v[2].x, v[2].y, v[3].x, v[3].y};
       if constexpr ((MODE & 2) != 0) {
         int z = lane + ig;
@@ -299,7 +314,7 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = coch * 64 + (wm * MI + i) * 16 + g * 4 + r;
+      const int co = coch * COT + (wm * MI + i) * 16 + g * 4 + r;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int k = t * a.Cx + cich * 64 + wn * 16 + li;
@@ -318,6 +333,19 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
 }  // namespace
 
 int g_win8_ablate = 0;
+// the workgroup co tile: 0 = not yet read from DG_WIN8_COT ("64" | "128" | "128,4": 4 waves,
+// one per SIMD with the whole register file), else 64 / 128; its wave count (8 | 4)
+int g_win8_cot = 0, g_win8_nw = 8;
+int win8_cot() {
+  if (g_win8_cot == 0) {
+    const char* e = getenv("DG_WIN8_COT");
+    int c = 64, w = 8;
+    if (e) sscanf(e, "%d,%d", &c, &w);
+    g_win8_cot = c == 128 ? 128 : 64;
+    g_win8_nw = g_win8_cot == 128 && w == 4 ? 4 : 8;
+  }
+  return g_win8_cot;
+}
 
 extern "C" {
 
@@ -328,14 +356,15 @@ extern "C" {
 // (256 + 224) of 278 super-steps; d = 128 (40 pairs): 6 splits = 1 round of 139 (1 split
 // would leave 96 CUs idle; a perfect fill at 8 / 32 splits writes 2.7x / 5x the slabs).
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
-  const int pairs = nl * (M / 64) * (Cx / 64);
+  const int cot = win8_cot();
+  const int pairs = nl * (M / cot) * (Cx / 64);
   const int TS = B * SPB / 4;
   if (pairs <= 0 || num_cus <= 0) return 1;
   int best = 1;
   double best_t = -1.0;
   for (int s = 1; s <= 32 && s <= TS / 4; ++s) {
     const long long rounds = (pairs * (long long)s + num_cus - 1) / num_cus;
-    const double t = (double)(rounds * ((TS + s - 1) / s)) + 0.11 * pairs * s;
+    const double t = (double)(rounds * ((TS + s - 1) / s)) + 0.11 * (cot / 64) * pairs * s;
     if (best_t < 0 || t < best_t) {
       best_t = t;
       best = s;
@@ -348,7 +377,8 @@ int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
 // e4m3), slab, s_dz, s_x} (int64)
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, long long* sf, hipStream_t stream) {
-  if (nl <= 0 || nl > MAXL || M % 64 != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
+  const int cot = win8_cot();
+  if (nl <= 0 || nl > MAXL || M % cot != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || B % 4 != 0 || splits <= 0 || splits > B * SPB / 4)
     return hipErrorInvalidValue;
   Win8Layers Ls{};
@@ -363,12 +393,47 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
       return hipErrorInvalidValue;
   }
   Win8Args a{sf, M, Mpad, Cx, KP, B, splits, nl};
-  const dim3 grid(nl * (M / 64) * (Cx / 64) * splits);
+  const dim3 grid(nl * (M / cot) * (Cx / 64) * splits);
   // (8 waves: the 4-wave variant, 1 wave per SIMD with the whole register file, measured
   // the same — profiles/r3_fp8_wgrad_ab.txt)
   // (B reads 2 taps ahead measured the same as 1: profiles/r4_s1_fused_update_and_fp8_bisection.txt)
   // prefetch distance 3: 4 measured equal (12x256 fp8 133.7k vs 133.9k,
   // profiles/r4_s2_sr_hash_win8_pd_ab.txt)
+  if (cot == 128 && g_win8_nw == 4) {
+    // (read-ahead experiments: ablate 64 / 65 = RA 1 / 3)
+    if (g_win8_ablate == 64) {
+      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 1, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
+      return hipGetLastError();
+    }
+    if (g_win8_ablate == 65) {
+      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 3, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
+      return hipGetLastError();
+    }
+    if (g_win8_ablate == 66) {
+      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 4, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
+      return hipGetLastError();
+    }
+    switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
+#define DG_W8(m) \
+    case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 3, m, 128>), grid, dim3(256), 0, stream, a, Ls); break;
+      DG_W8(1) DG_W8(2) DG_W8(4) DG_W8(6) DG_W8(16)
+#undef DG_W8
+      default:
+        hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
+    }
+    return hipGetLastError();
+  }
+  if (cot == 128) {
+    switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
+#define DG_W8(m) \
+    case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, m, 128>), grid, dim3(512), 0, stream, a, Ls); break;
+      DG_W8(1) DG_W8(2) DG_W8(3) DG_W8(4) DG_W8(6) DG_W8(7) DG_W8(8) DG_W8(16) DG_W8(20) DG_W8(31)
+#undef DG_W8
+      default:
+        hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, 0, 128>), grid, dim3(512), 0, stream, a, Ls);
+    }
+    return hipGetLastError();
+  }
   switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
 #define DG_W8(m) \
   case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, m>), grid, dim3(512), 0, stream, a, Ls); break;
@@ -381,5 +446,12 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
 }
 
 void dg_conv_wgrad_win8_set_ablate(int mode) { g_win8_ablate = mode; }
+
+// the workgroup co tile (64 | 128; overrides DG_WIN8_COT): the split count query and every
+// later launch follow it, so set it before sizing slabs
+void dg_conv_wgrad_win8_set_cot(int cot, int nw) {
+  g_win8_cot = cot == 128 ? 128 : 64;
+  g_win8_nw = g_win8_cot == 128 && nw == 4 ? 4 : 8;
+}
 
 }  // extern "C"
