@@ -595,8 +595,9 @@ hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
 }
 
 int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
-// the staggered schedule: -1 = not yet read from DG_STACK2_STAG ("0" off, "1" on, or
-// "1,PRIO,DELAY"), else 0 / 1; its co-half-0 priority and co-half-1 start delay
+// the staggered schedule: -1 = not yet read from DG_STACK2_STAG ("MODE[,PRIO[,DELAY]]"), else
+// 0 off, 1 both stacks, 2 the backward-data stack only; its co-half-0 priority and co-half-1
+// start delay
 int g_stack2_stag = -1, g_stack2_prio = 1, g_stack2_delay = 0;
 void stack2_sched_from_env() {
   if (g_stack2_stag >= 0) return;
@@ -605,7 +606,7 @@ void stack2_sched_from_env() {
   if (e && *e) {
     int v = 0, p = g_stack2_prio, d = g_stack2_delay;
     const int n = sscanf(e, "%d,%d,%d", &v, &p, &d);
-    g_stack2_stag = n >= 1 && v ? 1 : 0;
+    g_stack2_stag = n >= 1 && v >= 0 && v <= 2 ? v : 0;
     if (n >= 2) g_stack2_prio = p;
     if (n >= 3) g_stack2_delay = d;
   }
@@ -631,7 +632,7 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
   stack2_sched_from_env();
   a.stag_prio = g_stack2_prio;
   a.stag_delay = g_stack2_delay;
-  const bool stag = g_stack2_stag == 1 && !sig;
+  const bool stag = (g_stack2_stag == 1 || (g_stack2_stag == 2 && epi == EPI_DGRAD)) && !sig;
   if (sig && epi != EPI_DGRAD) return hipErrorInvalidValue;
   // (the buffer stores address a row's frame with 32-bit offsets)
   if (sig && (size_t)B * FF * C * 2 > 0x7fffffffull) return hipErrorInvalidValue;
@@ -684,7 +685,7 @@ void dg_conv_stack2_set_mode(int m) { g_stack2_mode = m; }
 // the staggered two-group schedule (overrides DG_STACK2_STAG): on 0 / 1, co-half-0 MFMA
 // priority 0..2, co-half-1 start delay (s_sleep 127 rounds)
 void dg_conv_stack2_set_sched(int stag, int prio, int delay) {
-  g_stack2_stag = stag ? 1 : 0;
+  g_stack2_stag = stag >= 0 && stag <= 2 ? stag : 0;
   g_stack2_prio = prio;
   g_stack2_delay = delay;
 }

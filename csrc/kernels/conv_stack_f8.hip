@@ -76,6 +76,7 @@ constexpr float BF8_MAX = 57344.f;    // e5m2
 constexpr int EPI_FWD = 1;
 constexpr int EPI_DGRAD = 2;
 constexpr int FP8P = 448;             // fp8 copy-out frames: rows per board
+constexpr int IMG2 = 61440;           // C = 128 staggered schedule: second image's offset
 
 static_assert(dghead::scratch_bytes(128) + 64 + 16 + 4 * 24 <= SCRATCH, "head scratch");
 
@@ -91,7 +92,9 @@ struct Geo {
   static constexpr int CO_STEPS = (PIECES + NT - 1) / NT;   // 6 | 12
   static constexpr int IMG = FF * ROWB;           // image bytes
   static constexpr int PARK1 = SCRATCH / 128;     // C = 256: pass-0 pixels parked in [0, 12K)
-  static constexpr int LDS = C == 128 ? SCRATCH + 2 * H_BYTES : 160 * 1024;
+  // (C = 128: the staggered schedule's second e4m3 image at IMG2, its dump rows and tap
+  // over-reads up to row 487 inside the allocation; the last layer's bf16 image 2 x H_BYTES)
+  static constexpr int LDS = C == 128 ? SCRATCH + IMG2 + 488 * 128 : 160 * 1024;
   static constexpr int AMAX_OFF = C == 128 ? SCRATCH - 64 : SCRATCH + IMG + (NPTS - PARK1) * 128;
   static_assert(LDS <= 160 * 1024, "LDS");
   static_assert(C == 128 || AMAX_OFF + 64 <= LDS, "park area");
@@ -252,10 +255,15 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   const int wm = wave >> 2, wn = wave & 3;
   const int b = blockIdx.x;
   char* sI = smem + SCRATCH;                       // e4m3 image (C = 128 last layer: bf16)
+  // STAG (C = 128): double-buffered image — layer l reads image l & 1 (at img_rd) and writes
+  // its output into the other one, so a group's epilogue never waits for the other group's
+  // reads of the layer's input
+  int img_rd = 0;
   float* s_amax = (float*)(smem + G::AMAX_OFF);    // 2 x 8 floats (alternating per layer)
-  // STAG (C = 128): counters R0 R1 W0 W1 (conv_stack2.hip) and each layer's |y| max (float
-  // bits, ds_max per wave; folded into amax_out once at the end) below the wg_amax slots, in
-  // the head scratch (the head runs after the last of them is read)
+  // STAG (C = 128): counters W0 W1 (at cnt + 2, + 3: the waves of co-half 0 / 1 that wrote
+  // their half of a layer's output, 4 per layer) and each layer's |y| max (float bits, ds_max
+  // per wave; folded into amax_out once at the end) below the wg_amax slots, in the head
+  // scratch (the head runs after the last of them is read)
   LDS_AS unsigned* cnt = (LDS_AS unsigned*)(smem + SCRATCH - 64 - 16);
   LDS_AS unsigned* s_lmax = (LDS_AS unsigned*)(smem + SCRATCH - 64 - 16 - 4 * MAXL);
   if constexpr (STAG) {
@@ -303,6 +311,16 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       *(uint2*)(sI + f * ROWB + (((q >> 1) ^ fsig<C>(f)) * 16) + (q & 1) * 8) = o;
       // the fp8 copy of the quantized input (the fp8 weight gradient's operand)
       if constexpr ((MODE & 8) != 0) *(uint2*)(a.X8_0 + ((size_t)(b * FP8P + f) * C + q * 8)) = o;
+    }
+    if constexpr (STAG) {
+      // the second image's zero border (frame rows 0 / 20, columns 0 / 20: the taps' padding;
+      // the epilogues write interior pixels only) and its rows 441..447
+      for (int u = tid; u < 87 * 8; u += NT) {
+        const int k = u >> 3, q = u & 7;
+        const int row = k < 21 ? k : k < 42 ? 420 + (k - 21) : k < 61 ? (k - 41) * 21
+                        : k < 80 ? (k - 60) * 21 + 20 : 441 + (k - 80);
+        *(uint4*)(sI + IMG2 + row * ROWB + q * 16) = uint4{0, 0, 0, 0};
+      }
     }
     wg_amax(m, a.amax_x0, s_amax + 8);  // (contains the barrier: image complete)
   }
@@ -363,7 +381,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     }
     const int toff = (t / 3 - 1) * F + (t % 3 - 1);
     const int tsig = (t % 3 - 1) + 3 * (t / 3 - 1);
-    const LDS_AS char* base = (const LDS_AS char*)sI;
+    const LDS_AS char* base = (const LDS_AS char*)(sI + img_rd);
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int off = (int)(pk[j] & 0xFFFFFu) + toff * ROWB +
@@ -408,7 +426,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
     co_pq(s_, tid, p, q);
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
-    return *(const uint4*)(sI + f * ROWB + ((q ^ fsig<C>(f)) * 16));
+    return *(const uint4*)(sI + img_rd + f * ROWB + ((q ^ fsig<C>(f)) * 16));
   };
   // (y8: the fp8 copy of the previous layer's output, or null)
   // (yb / y8b: the bf16 / fp8 output frames advanced to this board, per layer)
@@ -451,6 +469,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
   if constexpr (C != 128) make_pk();
   for (int l = 0; l < a.nl; ++l) {
     if constexpr (C == 128) make_pk();
+    if constexpr (STAG) img_rd = (l & 1) * IMG2;
     const F8Layer L = a.L[l];
     const char* A_next = l + 1 < a.nl ? a.L[l + 1].A8 : L.A8;
     const F8Layer Lprev = a.L[l > 0 ? l - 1 : 0];
@@ -507,13 +526,16 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (C == 128) {
         // half-major K-steps (read_B): 0..3 channels 0..63, 4 both halves, 5..8 channels
         // 64..127.  Staggered schedule (STAG): no workgroup barrier between the layers of
-        // the run.  A wave reads image half c of a layer once co-half c has written it (W_c:
-        // 4 waves per layer); co-half g's waves write their output channels once all 8
-        // waves are past their reads of half g (R_g: 8 per layer; R0 after step 5, the last
-        // copy-out step).  Co-half 0 may run ahead of co-half 1, so each group's epilogue
-        // can overlap the other group's MFMAs instead of idling the pipes between two
-        // barriers (conv_stack2.hip).  The copy-out (steps 0..5) of each half is done by its
-        // own co-half: before its own next epilogue, once its own group has written it (W_wm).
+        // the run, and a double-buffered image.  A wave reads image half c of a layer once
+        // co-half c has written it (W_c: 4 waves per layer) — half 0 from step 0, half 1 from
+        // step 4; a group writes its output into the other image as soon as its K loop ends
+        // (that image was layer l - 1's input: every wave is past those reads, since each
+        // group waited for the other's layer l - 1 output inside layer l).  The co-halves
+        // drift apart (the older waves win issue arbitration: co-half 0 finishes its K loop
+        // ~30% earlier), so co-half 0's epilogue runs beside co-half 1's last K-steps and
+        // co-half 1's beside co-half 0's first four, instead of idling the MFMA pipes between
+        // two barriers.  The copy-out (steps 0..5) of each half is done by its own co-half
+        // (own writes: W_wm).
         stamp(l, 0);
         if constexpr (STAG) {
           grp_wait(cnt + 2, 4u * (unsigned)l);                        // W0
@@ -528,7 +550,6 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
             asm volatile("" : "+s"(tt));
             if constexpr (STAG) grp_wait_at(cnt + 3, 4u * (unsigned)l, tt, 4);   // W1
             kstep(tt, tt, true);
-            if constexpr (STAG) grp_signal_at(cnt + 0, tt, 5);                   // R0
           }
         }
 #pragma unroll 1
@@ -537,9 +558,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
           asm volatile("" : "+s"(tt));
           if constexpr (STAG) grp_wait_at(cnt + 3, 4u * (unsigned)l, tt, 4);     // W1
           kstep(tt, 0, false);
-          if constexpr (STAG) grp_signal_at(cnt + 0, tt, 5);                     // R0
         }
-        if constexpr (STAG) grp_signal(cnt + 1);                    // R1
         stamp(l, 2);
       } else {
         int st = 0;
@@ -588,12 +607,12 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       // C = 128 and the last pass of C = 256: every wave is past its last read of the
       // image before it is overwritten (pass 0 of C = 256 only writes the park area)
       const bool to_image = !last && hp == NC - 1;
-      if (STAG && !last)
-        grp_wait(cnt + wm, 8u * (unsigned)(l + 1));   // R_wm: every wave past its reads
-      else if (C == 128 || hp == NC - 1)
-        lds_barrier();
+      // (STAG, non-last layers: no wait — the output goes into the other image)
+      if (!(STAG && !last) && (C == 128 || hp == NC - 1)) lds_barrier();
       stamp(l, 3);
       char* sIe = smem + SCRATCH + z0;
+      // (the lean epilogue's output image: STAG writes the other one)
+      const int img_wr = STAG ? IMG2 - img_rd : 0;
       if (BF16_LAST_IMAGE && last) {
         // the bf16 two-image layout needs zero border rows (and rows 441..447, which the
         // head's weight-gradient pass reads against zero dz): the region held e4m3 data
@@ -657,7 +676,7 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
             }
             const uint32_t key = sr_lane + (uint32_t)(j * 16 * C + i * 16);
             const uint32_t q8 = pack8x4q<EPI, MODE>(x[0], x[1], x[2], x[3], key);
-            *(LDS_AS uint32_t*)((LDS_AS char*)sIe + (a_j ^ (uint32_t)(i << 4))) = q8;
+            *(LDS_AS uint32_t*)((LDS_AS char*)sIe + img_wr + (a_j ^ (uint32_t)(i << 4))) = q8;
           }
           m_all = fmaxf(m_all, wn * NF * 16 + j * 16 + lr < NPTS ? mj : 0.f);
           __builtin_amdgcn_sched_barrier(0);   // (one fragment column at a time)
@@ -812,18 +831,18 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 int g_f8_mode = 0;
 
 // The staggered schedule (C = 128): -1 = not yet read from DG_STACK_F8_STAG ("MODE[,DELAY]"),
-// else 0 off, 1 both stacks, 2 the backward-data stack only (default: 12x128 kernel bench and
-// step A/B, profiles/r5_stack_f8_stag.txt — the forward gains nothing: its co-half 0 waits
-// for co-half 1 either way); co-half-1 start delay
+// else 0 off, 1 both stacks (default: 12x128 fp8 step 408.6-409.1k vs 395.9-397.9k with the
+// backward-data stack only, profiles/r5_stack_f8_stag.txt), 2 the backward-data stack only;
+// co-half-1 start delay
 int g_f8_stag = -1, g_f8_delay = 0;
 void f8_sched_from_env() {
   if (g_f8_stag >= 0) return;
   const char* e = getenv("DG_STACK_F8_STAG");
-  g_f8_stag = 2;
+  g_f8_stag = 1;
   if (e && *e) {
     int v = 0, d = g_f8_delay;
     const int n = sscanf(e, "%d,%d", &v, &d);
-    g_f8_stag = n >= 1 && v >= 0 && v <= 2 ? v : 2;
+    g_f8_stag = n >= 1 && v >= 0 && v <= 2 ? v : 1;
     if (n >= 2) g_f8_delay = d;
   }
 }
@@ -850,6 +869,8 @@ hipError_t launch_f8(const F8Args& a, int B, hipStream_t stream) {
   if constexpr (C == 128 && (MODE & (2 | 4 | 64 | 128)) == 0) {
     if constexpr (MODE == 24 || MODE == 56) {
       if (g_f8_dbg) {
+        if (g_f8_mode == 4)   // (stamps of the no-copy-out ablation, barrier schedule)
+          return launch_f8_s<C, EPI, MODE | 256 | 4, false>(a, B, stream);
         return a.stag_on ? launch_f8_s<C, EPI, MODE | 256, true>(a, B, stream)
                          : launch_f8_s<C, EPI, MODE | 256, false>(a, B, stream);
       }
@@ -872,7 +893,9 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
       // the production backward-data chain and its timing ablations
       switch (g_f8_mode) {
         case 2: return launch_f8<C, EPI_DGRAD, 56 | 2>(a, B, stream);
-        case 4: return launch_f8<C, EPI_DGRAD, 56 | 4>(a, B, stream);
+        case 4:
+          if (g_f8_dbg) return launch_f8<C, EPI_DGRAD, 56>(a, B, stream);   // (stamped variant)
+          return launch_f8<C, EPI_DGRAD, 56 | 4>(a, B, stream);
         case 64: return launch_f8<C, EPI_DGRAD, 56 | 64>(a, B, stream);
         case 68: return launch_f8<C, EPI_DGRAD, 56 | 68>(a, B, stream);
         case 198: return launch_f8<C, EPI_DGRAD, 56 | 198>(a, B, stream);
@@ -888,7 +911,9 @@ hipError_t launch_mode(int epi, const F8Args& a, int B, hipStream_t stream) {
     // the production forward (fp8 copies only) and its timing ablations
     switch (g_f8_mode) {
       case 2: return launch_f8<C, EPI_FWD, 24 | 2>(a, B, stream);
-      case 4: return launch_f8<C, EPI_FWD, 24 | 4>(a, B, stream);
+      case 4:
+        if (g_f8_dbg) return launch_f8<C, EPI_FWD, 24>(a, B, stream);   // (stamped variant)
+        return launch_f8<C, EPI_FWD, 24 | 4>(a, B, stream);
       case 64: return launch_f8<C, EPI_FWD, 24 | 64>(a, B, stream);
       case 68: return launch_f8<C, EPI_FWD, 24 | 68>(a, B, stream);
       case 128: return launch_f8<C, EPI_FWD, 24 | 128>(a, B, stream);
@@ -964,7 +989,7 @@ void dg_conv_stack_f8_set_mode(int m) { g_f8_mode = m; }
 void dg_conv_stack_f8_set_debug(unsigned long long* dbg) { g_f8_dbg = dbg; }
 
 void dg_conv_stack_f8_set_sched(int stag, int delay) {
-  g_f8_stag = stag >= 0 && stag <= 2 ? stag : 2;
+  g_f8_stag = stag >= 0 && stag <= 2 ? stag : 1;
   g_f8_delay = delay;
 }
 
