@@ -9,7 +9,7 @@
 #   bench[:ARGS]     python bench.py ARGS (default: --steps 50 --warmup 10); JSON appended to
 #                    gpurun_out/bench.jsonl
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS (graphs off unless ARGS
-#                    says otherwise) -> gpurun_out/prof_<n>/
+#                    says otherwise; no accuracy phase) -> gpurun_out/prof_<n>/
 #   pmc[:ARGS]       rocprofv3 --kernel-trace --pmc (MFMA busy, waits, LDS conflicts, clock) of
 #                    bench.py --steps 3 --warmup 1 --no-graph ARGS -> gpurun_out/pmc_<n>/ and
 #                    a per-kernel summary (tools/pmc_summary.py)
@@ -49,7 +49,7 @@ for step in "$@"; do
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
         --output-format csv -d $R/gpurun_out/prof_$n -o run -- \
-        python3 $R/bench.py ${arg:---steps 10 --warmup 3} > $R/gpurun_out/prof_$n.log 2>&1)
+        python3 $R/bench.py --accuracy-steps 0 ${arg:---steps 10 --warmup 3} > $R/gpurun_out/prof_$n.log 2>&1)
       rc=$? ;;
     pmc)
       # 8 SQ counters (the per-pass limit) + 1 GRBM: MFMA busy, waits, LDS conflicts and the
@@ -57,7 +57,7 @@ for step in "$@"; do
       C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C \
         --output-format csv -d $R/gpurun_out/pmc_$n -o run -- \
-        python3 $R/bench.py --steps 3 --warmup 1 --no-graph $arg > $R/gpurun_out/pmc_$n.log 2>&1)
+        python3 $R/bench.py --steps 3 --warmup 1 --no-graph --accuracy-steps 0 $arg > $R/gpurun_out/pmc_$n.log 2>&1)
       rc=$?
       if [ $rc = 0 ]; then
         f=$(find gpurun_out/pmc_$n -name '*counter_collection.csv' | head -1)
