@@ -628,22 +628,33 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
       if constexpr (EPI == EPI_DGRAD && (MODE & 32) != 0)
         sr_lane = sr_seed + (uint32_t)(l + 1) * 0x85EBCA6Bu +
                   (uint32_t)((b * NPTS + wn * NF * 16 + lr) * C + 128 * hp + wm * 64 + lq * 4);
-      if (C == 128 && !last) {
-        // Lean epilogue (C = 128, non-last layers): straight-line — no per-fragment branch
-        // (the pixels past the board store to the dump rows, a select keeps them out of the
-        // |y| max), one XOR per fragment for its LDS address, and per value: forward
-        // fma + ReLU max + scale + clamp; backward-data mask AND (v_bfe_i32 gives the lane
-        // mask) + scale + clamp, the |dz| max taken before the (power-of-two) dequantization.
-        // Same results as the general loop below: every scale is a power of two.
+      if (!last && (C == 128 || EPI == EPI_DGRAD)) {
+        // (C = 256 forward: the general loop — its lean form spilled 20 VGPRs and measured
+        // +1.5%; the backward-data one -12%, profiles/r5_stack_f8_stag.txt)
+        // Lean epilogue (non-last layers): straight-line — no per-fragment branch (C = 128:
+        // the pixels past the board store to the dump rows; C = 256, whose LDS has no room
+        // for them: the store of fragment columns 4 and 5 only, where such pixels occur, is
+        // lane-masked; a select keeps them out of the |y| max), one XOR per fragment for its
+        // LDS address, and per value: forward fma + ReLU max + scale + clamp; backward-data
+        // mask AND (v_bfe_i32 gives the lane mask) + scale + clamp, the |dz| max taken before
+        // the dequantization.  Same results as the general loop below (the output scale is a
+        // power of two).
         const float s1 = EPI == EPI_FWD ? inv_y : deq * inv_y;
         float m_all = 0.f;
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
           uint32_t pkj = pk[j];
           asm volatile("" : "+v"(pkj));
-          // row + byte lq*4 + slot (wm*4 ^ sig) << 4; fragment i's slot is (wm*4 + i) ^ sig
-          const uint32_t a_j = ((pkj & 0xFFFFFu) + (uint32_t)(lq * 4)) |
-                               ((uint32_t)((wm * 4) ^ sig_of<C>((int)(pkj >> 20))) << 4);
+          // image: row + byte lq*4 + slot (8hp + 4wm ^ sig) << 4, fragment i's slot is
+          // (8hp + 4wm + i) ^ sig; C = 256 pass 0 parks pixel p's row (piece (cl / 16) ^
+          // (p & 7), general loop below) — the same XOR by i << 4 either way
+          const int pj = wn * NF * 16 + j * 16 + lr;
+          uint32_t a_j = ((pkj & 0xFFFFFu) + (uint32_t)(lq * 4)) |
+                         ((uint32_t)((8 * hp + 4 * wm) ^ sig_of<C>((int)(pkj >> 20))) << 4);
+          if (C == 256 && !to_image) {
+            const int pr = pj < G::PARK1 ? pj * 128 : SCRATCH + G::IMG + (pj - G::PARK1) * 128;
+            a_j = (uint32_t)(pr - SCRATCH) + (uint32_t)((wm * 64 + lq * 4) ^ ((lane & 7) << 4));
+          }
           uint32_t wx = 0, wy = 0;
           if constexpr (EPI == EPI_DGRAD) {
             wx = em[j].x >> (lq * 4);
@@ -676,12 +687,14 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
             }
             const uint32_t key = sr_lane + (uint32_t)(j * 16 * C + i * 16);
             const uint32_t q8 = pack8x4q<EPI, MODE>(x[0], x[1], x[2], x[3], key);
-            *(LDS_AS uint32_t*)((LDS_AS char*)sIe + img_wr + (a_j ^ (uint32_t)(i << 4))) = q8;
+            // (C = 256: columns 0..3 hold board pixels only, wn * 96 + 63 < 361)
+            if (C == 128 || j < 4 || pj < NPTS)
+              *(LDS_AS uint32_t*)((LDS_AS char*)sIe + img_wr + (a_j ^ (uint32_t)(i << 4))) = q8;
           }
-          m_all = fmaxf(m_all, wn * NF * 16 + j * 16 + lr < NPTS ? mj : 0.f);
+          m_all = fmaxf(m_all, pj < NPTS ? mj : 0.f);
           __builtin_amdgcn_sched_barrier(0);   // (one fragment column at a time)
         }
-        vmax = EPI == EPI_FWD ? m_all : m_all * deq;
+        vmax = fmaxf(vmax, EPI == EPI_FWD ? m_all : m_all * deq);
       } else
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
