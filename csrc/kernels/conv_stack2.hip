@@ -596,17 +596,19 @@ hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
 
 int g_stack2_mode = 0;  // ablation MODE of the forward (0 = production)
 // the staggered schedule: -1 = not yet read from DG_STACK2_STAG ("MODE[,PRIO[,DELAY]]"), else
-// 0 off, 1 both stacks, 2 the backward-data stack only; its co-half-0 priority and co-half-1
+// 0 off, 1 both stacks, 2 the backward-data stack only (default: 12x128 bf16 step 303.8-304.3k
+// vs 302.1-302.6k with neither, 4 interleaved rounds on one box, profiles/r5_stack2_stag.txt;
+// the forward measured slower, kbench 244 vs 228 us); its co-half-0 priority and co-half-1
 // start delay
 int g_stack2_stag = -1, g_stack2_prio = 1, g_stack2_delay = 0;
 void stack2_sched_from_env() {
   if (g_stack2_stag >= 0) return;
   const char* e = getenv("DG_STACK2_STAG");
-  g_stack2_stag = 0;
+  g_stack2_stag = 2;
   if (e && *e) {
     int v = 0, p = g_stack2_prio, d = g_stack2_delay;
     const int n = sscanf(e, "%d,%d,%d", &v, &p, &d);
-    g_stack2_stag = n >= 1 && v >= 0 && v <= 2 ? v : 0;
+    g_stack2_stag = n >= 1 && v >= 0 && v <= 2 ? v : 2;
     if (n >= 2) g_stack2_prio = p;
     if (n >= 3) g_stack2_delay = d;
   }

@@ -89,7 +89,7 @@ def main():
                 times.setdefault(f"{name}_stag{v}", []).append(timeit(run(epi, v)))
             times.setdefault(f"{name}_stag_noepi", []).append(timeit(run(epi, (1, 1, 0), 16)))
     h.conv_stack2_set_mode(0)
-    h.conv_stack2_set_sched(0, 1, 0)
+    h.conv_stack2_set_sched(2, 1, 0)
     out["us"] = {k: round(min(v), 1) for k, v in times.items()}
     out["fp8"] = fp8_stag(h, B, NL, s, a.rounds)
     print(json.dumps(out))
