@@ -4,6 +4,8 @@ Inputs are rounded to bf16 first so the oracle sees exactly what the MFMA sees; 
 remaining error is fp32-accumulation order + the bf16 rounding of the output.  The conv
 oracle itself is computed on the CPU (conv_ref).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -337,6 +339,42 @@ def test_bias_grad():
     ref_p = dz.sum(0).reshape(128, 361).t()
     assert rel_err(gp, ref_p) < 1e-5
     assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_bias_grad_multi_units(C):
+    """Multi-layer bias partials (elementwise.hip bias_partial_units_kernel: 16-board
+    sub-chunk units summed in order through LDS; and the per-item kernel it replaces,
+    bias_set_units(0)) vs the fp32 per-chunk sums of the same bf16 frames."""
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    torch.manual_seed(C)
+    B, nl, P = 128, 2, 361
+    dz = [bf(torch.randn(B, C, 19, 19, device=DEV)) for _ in range(nl)]
+    frames = [LY.to_frame(d, 1) for d in dz]
+    nch = h.bias_chunks_multi(B)
+    parts = [torch.empty(nch * (P + 19) * C, device=DEV) for _ in range(nl)]
+    tab = np.array([[f.data_ptr(), q.data_ptr(), 0] for f, q in zip(frames, parts)],
+                   dtype=np.int64)
+    res = {}
+    try:
+        for units in (1, 0):
+            h.bias_set_units(units)
+            for q in parts:
+                q.fill_(float("nan"))
+            h.bias_grad_partial_multi(tab.ctypes.data, nl, B, C, 1, 0, stream_handle())
+            torch.cuda.synchronize()
+            res[units] = [q.clone() for q in parts]
+    finally:
+        h.bias_set_units(1 if os.environ.get("DG_BIAS_UNITS") == "1" else 0)
+    for i in range(nl):
+        ref = dz[i].view(nch, B // nch, C, P).sum(1).transpose(1, 2)     # [chunk][p][C]
+        ref_r = ref.reshape(nch, 19, 19, C).sum(2)                       # [chunk][h][C]
+        for units in (1, 0):
+            got = res[units][i]
+            assert rel_err(got[:nch * P * C].view(nch, P, C), ref) < 1e-5, (units, i)
+            assert rel_err(got[nch * P * C:].view(nch, 19, C), ref_r) < 1e-5, (units, i)
 
 
 def test_sgd_and_lr_decay():
