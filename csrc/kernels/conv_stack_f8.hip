@@ -468,9 +468,10 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
   if constexpr (C != 128) make_pk();
   // The layer loop.  The body is conv_stack_f8_layer.inc.h (why it is a textual include:
-  // there).  C = 256 keeps one rolled loop: split, its backward-data variant went 248 -> 256
-  // VGPRs + 1 spill and its kernel time up to +4%, the forward no faster (lean epilogue too).
-  if constexpr (!STAG && C == 128) {
+  // there).  C = 256 backward-data keeps one rolled loop: split, it went 248 -> 256 VGPRs + 1
+  // spill and its kernel time up to +4%; the C = 256 forward splits (256 + 14 spills -> 255 +
+  // 0) with the general epilogue in both copies (its lean form measured no faster).
+  if constexpr (!STAG && (C == 128 || EPI == EPI_FWD)) {
     for (int l = 0; l + 1 < a.nl; ++l) {
       constexpr bool last = false;
 #include "conv_stack_f8_layer.inc.h"
