@@ -169,6 +169,9 @@ class HipGoNet:
             splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
                                            self.h.conv_wgrad_wgs_per_cu_for(KPw),
                                            self.h.conv_wgrad_ktile(KPw))
+            if spec.index == 0 and os.environ.get("DG_L0_SPLITS"):
+                # (A/B knob: the first layer's split-K count; its slab reduce reads them all)
+                splits = max(1, min(int(os.environ["DG_L0_SPLITS"]), npix // 256))
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
                          Mpad, KPw, Mpad_w, splits, board=board)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
