@@ -468,10 +468,10 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 
   if constexpr (C != 128) make_pk();
   // The layer loop.  The body is conv_stack_f8_layer.inc.h (why it is a textual include:
-  // there).  C = 256 backward-data keeps one rolled loop: split, it went 248 -> 256 VGPRs + 1
-  // spill and its kernel time up to +4%; the C = 256 forward splits (256 + 14 spills -> 255 +
-  // 0) with the general epilogue in both copies (its lean form measured no faster).
-  if constexpr (!STAG && (C == 128 || EPI == EPI_FWD)) {
+  // there).  Every variant but C = 256 backward-data splits it; that one keeps one rolled loop
+  // (split, it went 248 -> 256 VGPRs + 1 spill and its kernel time up to +4%).  The C = 256
+  // forward keeps the general epilogue in both copies (its lean form measured no faster).
+  if constexpr (!(C == 256 && EPI == EPI_DGRAD)) {
     for (int l = 0; l + 1 < a.nl; ++l) {
       constexpr bool last = false;
 #include "conv_stack_f8_layer.inc.h"
@@ -531,19 +531,20 @@ __global__ void __launch_bounds__(NT) conv_stack_f8_kernel(F8Args a) {
 int g_f8_mode = 0;
 
 // The staggered schedule (C = 128): -1 = not yet read from DG_STACK_F8_STAG ("MODE[,DELAY]"),
-// else 0 off, 1 both stacks, 2 the backward-data stack only (default since the barrier
-// forward's layer body is split in two, conv_stack_f8_layer.inc.h: 12x128 fp8 step 412.0-412.4k
-// vs 408.3-408.5k with both, same box; 10-layer forward 148.4 us barrier vs 153.8 staggered,
-// profiles/r5_stack_f8_stag.txt); co-half-1 start delay
+// else 0 off, 1 both stacks (default: with every C = 128 variant's layer body split in two,
+// conv_stack_f8_layer.inc.h, the staggered forward is the faster one again — 144.2 vs 147.3 us
+// per 10 layers; 12x128 fp8 step 416.9-419.6k vs 410.0-414.4k with the backward-data stack
+// only, same box, profiles/r5_stack_f8_stag.txt §10), 2 the backward-data stack only;
+// co-half-1 start delay
 int g_f8_stag = -1, g_f8_delay = 0;
 void f8_sched_from_env() {
   if (g_f8_stag >= 0) return;
   const char* e = getenv("DG_STACK_F8_STAG");
-  g_f8_stag = 2;
+  g_f8_stag = 1;
   if (e && *e) {
     int v = 0, d = g_f8_delay;
     const int n = sscanf(e, "%d,%d", &v, &d);
-    g_f8_stag = n >= 1 && v >= 0 && v <= 2 ? v : 2;
+    g_f8_stag = n >= 1 && v >= 0 && v <= 2 ? v : 1;
     if (n >= 2) g_f8_delay = d;
   }
 }

@@ -1,11 +1,10 @@
 // The layer body of conv_stack_f8_kernel (conv_stack_f8.hip), included textually in the
-// kernel's layer loops: by the C = 128 barrier schedule twice — the non-last layers' loop (lean
-// epilogue, compile-time last = false) and the last layer (general epilogue) then get their own
-// register allocation instead of one for the union of both in one rolled loop (forward 256
-// VGPRs + 8 spills -> 238 + 0: 153.0 -> 148.4 us per 10-layer launch, faster than the staggered
-// schedule's 153.8) — and once, as a single rolled loop, by the staggered schedule (split, its
-// K loops spilled 5-11 VGPRs per K-step; wrapped in a lambda instead of included, the same text
-// cost its backward-data variant 23) and by C = 256 (conv_stack_f8.hip).  Expects the
+// kernel's layer loops, twice by every variant but C = 256 backward-data: the non-last layers'
+// loop (lean epilogue, compile-time last = false) and the last layer (general epilogue) then
+// get their own register allocation instead of one for the union of both in one rolled loop
+// (C = 128 barrier forward 256 VGPRs + 8 spills -> 238 + 0, staggered forward 256 + 8 -> 242 +
+// 0: 10 layers 153.8 -> 144.2 us).  Why an include: the same text wrapped in an always_inline
+// lambda allocated differently — the staggered variants spilled 5-23 VGPRs inside the K loop.  Expects the
 // kernel's locals in scope and `l` (layer index) and `last` (last layer) defined.
 // Not a header: no include guard, included only inside conv_stack_f8_kernel.
   if constexpr (C == 128) make_pk();

@@ -152,7 +152,7 @@ def fp8_stag(h, B, NL, s, rounds, timeline=False):
                 h.conv_stack_f8_set_mode(0)
                 out[f"{name}_stag{stag}_mode{mode}"] = summarize(
                     dbg.view(8, 8, 24, 8).cpu().numpy(), NL)
-        h.conv_stack_f8_set_sched(2, 0)
+        h.conv_stack_f8_set_sched(1, 0)
         return out
     for fwd, name in ((True, "fwd"), (False, "dgrad")):
         outs = []
@@ -169,7 +169,7 @@ def fp8_stag(h, B, NL, s, rounds, timeline=False):
             times.setdefault(f"{name}_barrier", []).append(timeit(run(fwd, 0)))
             times.setdefault(f"{name}_stag", []).append(timeit(run(fwd, 1)))
             times.setdefault(f"{name}_stag_delay1", []).append(timeit(run(fwd, 1, 1)))
-    h.conv_stack_f8_set_sched(2, 0)
+    h.conv_stack_f8_set_sched(1, 0)
     out["us"] = {k: round(min(v), 1) for k, v in times.items()}
     return out
 
