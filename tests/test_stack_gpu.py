@@ -228,3 +228,82 @@ def test_fp8_dgrad_stochastic_rounding_is_unbiased(C):
     print(f"C={C}: rne {e_rne:.4f} single-SR {np.mean(errs):.4f} mean-of-32 {e_mean:.4f}")
     assert max(errs) < 3 * e_rne               # one SR draw: same order as nearest-even
     assert e_mean < 0.4 * e_rne                 # the mean converges: unbiased
+
+
+@pytest.mark.parametrize("kind", ["bf16", "fp8"])
+def test_staggered_schedules_bit_identical(kind):
+    """The staggered two-group schedules (conv_stack2.hip / conv_stack_f8.hip STAG: LDS
+    counters instead of the per-layer barriers; fp8 C = 128 with a double-buffered image) give
+    exactly the barrier schedules' outputs: every layer's frame, the forward's ReLU bits and
+    (fp8) the |y| maxima, forward and backward-data (e5m2 with stochastic rounding)."""
+    from deep_go_amd.ops import layouts as LY
+    from deep_go_amd.ops.native import hip, stream_handle
+    h = hip()
+    torch.manual_seed(21)
+    B, NL = 8, 4
+    x = LY.alloc_frame(B, C, 1, DEV)
+    LY.frame_interior(x, 1).copy_(torch.randn(B, 19, 19, C, device=DEV).relu())
+    ys = [LY.alloc_frame(B, C, 1, DEV) for _ in range(NL)]
+    ms = [torch.randint(0, 256, (B, 361, C // 8), dtype=torch.uint8, device=DEV)
+          for _ in range(NL)]
+    md = [m.clone() for m in ms]
+    pbs = [(0.01 * torch.randn(24 * 2 * 4 * 64 * 4, device=DEV)).to(torch.bfloat16)
+           for _ in range(NL)]
+    s = stream_handle()
+    if kind == "bf16":
+        ops = [LY.stack_frag((torch.randn(C, 9 * C, device=DEV) / (3 * C ** 0.5))
+                             .to(torch.bfloat16)) for _ in range(NL)]
+
+        def run(fwd, stag):
+            h.conv_stack2_set_sched(stag, 1, 0)
+            tab = np.array([[ops[i].data_ptr(), pbs[i].data_ptr() if fwd else 0,
+                             ys[i].data_ptr(), (ms if fwd else md)[i].data_ptr()]
+                            for i in range(NL)], dtype=np.int64)
+            h.conv_stack2(h.EPI_FWD if fwd else h.EPI_DGRAD, tab.ctypes.data, NL,
+                          x.data_ptr(), 0, B, s)
+        default = (2, 1, 0)
+        outs = lambda fwd: ys + (ms if fwd else [])  # noqa: E731
+    else:
+        w8 = [LY.stack_frag_f8(torch.randint(0, 0x78, (C, 9, C), dtype=torch.uint8,
+                                             device=DEV)) for _ in range(NL)]
+        sc = torch.full((NL + 1,), 2.0 ** -6, device=DEV)
+        amax = torch.zeros(NL + 1, dtype=torch.int32, device=DEV)
+        step = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+        # the production variants (as the training step): fp8 copies of every non-last output
+        # (y8), the last layer's bf16 frame only
+        x8 = [torch.zeros(B * 448 * C, dtype=torch.uint8, device=DEV) for _ in range(NL)]
+        y8 = np.array([x8[0].data_ptr()] + [x8[i + 1].data_ptr() if i + 1 < NL else 0
+                                            for i in range(NL)], dtype=np.int64)
+
+        def run(fwd, stag):
+            h.conv_stack_f8_set_sched(stag, 0)
+            tab = np.array([[w8[i].data_ptr(), pbs[i].data_ptr() if fwd else 0,
+                             ys[i].data_ptr() if i == NL - 1 else 0,
+                             (ms if fwd else md)[i].data_ptr(), sc.data_ptr() + 4 * i,
+                             sc.data_ptr() + 4 * i, sc.data_ptr() + 4 * (i + 1),
+                             amax.data_ptr() + 4 * (i + 1)] for i in range(NL)], dtype=np.int64)
+            if fwd:
+                h.conv_stack_f8_y8(C, h.EPI_FWD, tab.ctypes.data, NL, x.data_ptr(),
+                                   sc.data_ptr(), amax.data_ptr(), B, y8.ctypes.data, s)
+            else:
+                h.conv_stack_f8_dgrad(C, tab.ctypes.data, NL, x.data_ptr(), sc.data_ptr(),
+                                      amax.data_ptr(), B, y8.ctypes.data, step.data_ptr(), s)
+        default = (1, 0)
+        outs = lambda fwd: x8 + [ys[-1], amax] + (ms if fwd else [])  # noqa: E731
+    try:
+        for fwd in (True, False):
+            got = []
+            for stag in (0, 1):
+                for t in outs(fwd):
+                    t.zero_()
+                run(fwd, stag)
+                torch.cuda.synchronize()
+                got.append([t.clone() for t in outs(fwd)])
+            for k, (a, b) in enumerate(zip(*got)):
+                assert torch.equal(a, b), (kind, "fwd" if fwd else "dgrad", k)
+            assert any(t.abs().sum().item() > 0 for t in got[0][:NL])
+    finally:
+        if kind == "bf16":
+            h.conv_stack2_set_sched(*default)
+        else:
+            h.conv_stack_f8_set_sched(*default)
