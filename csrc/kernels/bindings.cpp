@@ -81,6 +81,7 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
                                hipStream_t stream);
 int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
 int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad);
+void dg_conv_l1_frag_set_half(int on);
 hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
                            void* Y, void* mask, const void* planes, const void* player,
                            const void* rank, hipStream_t stream);
@@ -576,6 +577,8 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_l1_frag_ok", [](int kw, int x_pad, int x_C, int M, int y_pad) {
     return dg_conv_l1_frag_ok(kw, x_pad, x_C, M, y_pad);
   });
+  m.def("conv_l1_frag_set_half", [](int on) { dg_conv_l1_frag_set_half(on); },
+        "conv_l1_frag: 1 two half-board workgroups per board (two per CU), 0 one per board");
   m.def("conv_layer2", [](int epi, uintptr_t A, uintptr_t pbias, uintptr_t X, uintptr_t Y,
                          uintptr_t mask, int C, int B, uintptr_t stream) {
     check(dg_conv_layer2(epi, P<void>(A), P<void>(pbias), P<void>(X), P<void>(Y), P<void>(mask),

@@ -241,13 +241,18 @@ struct L1FragArgs {
   const uint8_t* in_rank;     // [B]
 };
 
-__global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
+// NFX = 6: one workgroup per board (4 x 96 pixels); NFX = 3: two per board, each 4 x 48 of
+// its pixels (fragments 12 h .. 12 h + 11), <= 128 VGPRs so two fit on a CU and one's prologue
+// (frame staging / feature expansion) and epilogue overlap the other's MFMAs
+template <int NFX>
+__global__ void __launch_bounds__(512, NFX == 6 ? 1 : 2) conv_l1_frag_kernel(L1FragArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const int b = blockIdx.x;
+  const int b = NFX == 6 ? blockIdx.x : blockIdx.x >> 1;
+  const int f0 = NFX == 6 ? 0 : (blockIdx.x & 1) * 4 * NFX;   // first pixel fragment
 
   if (a.in_planes) {
     // fused expansion (dg_features.h, as expand_features): border pixels zero, interior
@@ -267,7 +272,7 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
         for (int c8 = 0; c8 < 5; ++c8) {
           cell[c8] = uint4{pack_bf16x2(v[8 * c8], v[8 * c8 + 1]), pack_bf16x2(v[8 * c8 + 2], v[8 * c8 + 3]),
                            pack_bf16x2(v[8 * c8 + 4], v[8 * c8 + 5]), pack_bf16x2(v[8 * c8 + 6], v[8 * c8 + 7])};
-          *(uint4*)(Xw + f * PF_XB + c8 * 16) = cell[c8];
+          if (f0 == 0) *(uint4*)(Xw + f * PF_XB + c8 * 16) = cell[c8];
         }
       }
 #pragma unroll
@@ -286,10 +291,10 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
     }
   }
   const int lr = lane & 15, lq = lane >> 4;
-  int pbase[NF];   // this lane's pixel centre in the plane layout (bytes)
+  int pbase[NFX];   // this lane's pixel centre in the plane layout (bytes)
 #pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    int p = wn * NF * 16 + j * 16 + lr;
+  for (int j = 0; j < NFX; ++j) {
+    int p = (f0 + wn * NFX + j) * 16 + lr;
     if (p >= NPTS) p = 0;
     const int hh = p / BOARD, w = p - (p / BOARD) * BOARD;
     pbase[j] = ((hh + 2) * PF_RP + (w + 2)) * 16;
@@ -300,13 +305,13 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
 #pragma unroll
     for (int i = 0; i < MF; ++i) r[i] = *(const bf16x8*)(p + i * 1024);
   };
-  auto read_B = [&](int s, int kk, bf16x8 (&bfr)[NF]) {
+  auto read_B = [&](int s, int kk, bf16x8 (&bfr)[NFX]) {
     int kc = s * 8 + kk * 4 + lq;          // this lane group's (tap, c8) chunk
     if (kc >= PF_CHUNKS) kc = 0;           // padding chunks: zero weights
     const int t = kc / 5, c8 = kc - (kc / 5) * 5;
     const int koff = (c8 * PF_PS + (t / 5 - 2) * PF_RP + (t % 5 - 2)) * 16;
 #pragma unroll
-    for (int j = 0; j < NF; ++j)
+    for (int j = 0; j < NFX; ++j)
       bfr[j] = lds_read_b128((const LDS_AS char*)(smem + pbase[j] + koff));
   };
   __syncthreads();   // frame landed
@@ -317,21 +322,21 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
   for (int h = 0; h < a.nh; ++h) {
     const char* Ah = a.A + (size_t)h * PF_STEPS * PF_STEP_BYTES;
     const char* A_next = h + 1 < a.nh ? Ah + PF_STEPS * PF_STEP_BYTES : Ah;
-    f32x4 acc[MF][NF];
+    f32x4 acc[MF][NFX];
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NFX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int s = 0; s < PF_STEPS; ++s) {
       // (past the last step of the last pass: a harmless re-load of its step 0)
       const char* An = s + 1 < PF_STEPS ? Ah + (s + 1) * PF_STEP_BYTES : A_next;
-      bf16x8 bfr[NF];
+      bf16x8 bfr[NFX];
       read_B(s, 0, bfr);
 #pragma unroll
       for (int i = 0; i < MF; ++i)
 #pragma unroll
-        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(Ak[0][i], bfr[j], acc[i][j]);
+        for (int j = 0; j < NFX; ++j) acc[i][j] = mfma16(Ak[0][i], bfr[j], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
       load_A(An, 0, Ak[0]);
       read_B(s, 1, bfr);
@@ -339,7 +344,7 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
 #pragma unroll
       for (int i = 0; i < MF; ++i)
 #pragma unroll
-        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(Ak[1][i], bfr[j], acc[i][j]);
+        for (int j = 0; j < NFX; ++j) acc[i][j] = mfma16(Ak[1][i], bfr[j], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
       load_A(An, 1, Ak[1]);
       __builtin_amdgcn_sched_barrier(0);
@@ -348,11 +353,11 @@ __global__ void __launch_bounds__(512) conv_l1_frag_kernel(L1FragArgs a) {
     int z0 = 0;
     asm volatile("" : "+v"(z0));
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int p = wn * NF * 16 + j * 16 + lr;
+    for (int j = 0; j < NFX; ++j) {
+      const int p = (f0 + wn * NFX + j) * 16 + lr;
       const int pc = p < NPTS ? p : NPTS - 1;
       const int hh = pc / BOARD, w = pc - (pc / BOARD) * BOARD;
-      const uint2* pf = a.pbias + (((size_t)(h * 24 + wn * NF + j) * 2 + wm) * 4) * 64 + lane + z0;
+      const uint2* pf = a.pbias + (((size_t)(h * 24 + f0 + wn * NFX + j) * 2 + wm) * 4) * 64 + lane + z0;
       char* yrow = a.Y + (((size_t)b * 21 + hh + 1) * 21 + (w + 1)) * a.M * 2;
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
@@ -420,6 +425,13 @@ int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad) {
   return kw == 5 && x_pad == 2 && x_C == 40 && M % 128 == 0 && M <= 512 && y_pad == 1;
 }
 
+// conv_l1_frag's workgroups per board: 2 (half-board, two per CU; DG_L1_HALF=1) or 1
+int g_l1_half = [] {
+  const char* e = getenv("DG_L1_HALF");
+  return e && *e == '1' ? 1 : 0;
+}();
+void dg_conv_l1_frag_set_half(int on) { g_l1_half = on ? 1 : 0; }
+
 hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
                            void* Y, void* mask, const void* planes, const void* player,
                            const void* rank, hipStream_t stream) {
@@ -428,13 +440,18 @@ hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int
     return hipErrorInvalidValue;
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel,
+    (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel<6>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
+    (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel<3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
     done = true;
   }
   L1FragArgs a{(const char*)A, (const uint2*)pbias, (char*)X, (char*)Y, (uint8_t*)mask, M,
                M / 128, (const uint8_t*)planes, (const uint8_t*)player, (const uint8_t*)rank};
-  hipLaunchKernelGGL(conv_l1_frag_kernel, dim3(B), dim3(512), PF_LDS, stream, a);
+  if (g_l1_half)
+    hipLaunchKernelGGL(conv_l1_frag_kernel<3>, dim3(2 * B), dim3(512), PF_LDS, stream, a);
+  else
+    hipLaunchKernelGGL(conv_l1_frag_kernel<6>, dim3(B), dim3(512), PF_LDS, stream, a);
   return hipGetLastError();
 }
 
