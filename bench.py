@@ -80,9 +80,12 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic batches")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--host-pool", action="store_true",
-                    help="synthetic batches in pinned host memory (each step's copy is an H2D "
-                         "copy, as from the trainer's loader) instead of device memory")
+    ap.add_argument("--device-pool", action="store_true",
+                    help="synthetic batches in device memory (each step's copy a D2D blit) "
+                         "instead of the default pinned host pool (each step's batch an H2D "
+                         "copy prefetched beside the previous step, as the trainer's loader "
+                         "does; the reference copies host->device every step, train.lua:99-100)")
+    ap.add_argument("--host-pool", action="store_true", help="(the default; kept for scripts)")
     ap.add_argument("--bucket-mb", type=float, default=3.0,
                     help="DP gradient bucket size; with --wgrad-group splitting the hidden "
                          "layers, 3 MB gives one bucket per weight-gradient group (head + top "
@@ -94,13 +97,15 @@ def parse(argv=None):
                          "proxy), at d = 128 one launch (the split doubles the split-K slab "
                          "traffic: +6%% compute for ~5 us less exposed comm); "
                          "profiles/r3_dp_overlap_proxy.txt")
-    ap.add_argument("--grad-dtype", default="bf16", choices=["fp32", "bf16"],
-                    help="DP gradient wire format (the bucket all-reduces): bf16 halves the "
-                         "bytes on xGMI; every gradient pass 2 writes the bf16 twin itself "
-                         "and the fused update reads it (no conversion kernels).  Bounded "
-                         "against the fp32 wire at world 8 (per-hop ring rounding) by "
-                         "tests/test_wire_cpu.py and tests/test_train_gpu.py "
-                         "test_bf16_gradient_wire_world8_memorisation_curve")
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="DP gradient wire format (the bucket all-reduces).  fp32 (default) is "
+                         "the reference's precision (DataParallelTable, experiments.lua:155-168). "
+                         "bf16 halves the bytes on xGMI (every gradient pass 2 writes the bf16 "
+                         "twin itself, the fused update reads it); bounded against fp32 at "
+                         "world 8 by tests/test_wire_cpu.py and tests/test_train_gpu.py.  Under "
+                         "N > 1 the bf16 wire is also measured, labelled, as secondary "
+                         "'dp-bf16-wire' (--no-bf16-wire-secondary: skip)")
+    ap.add_argument("--no-bf16-wire-secondary", action="store_true")
     ap.add_argument("--comm", default="auto", choices=["auto", "native", "torch", "proxy"],
                     help="DP collectives: native = in-graph RCCL communicator (csrc/comm), "
                          "torch = torch.distributed between graph segments, proxy = world-1 "
@@ -118,8 +123,10 @@ def parse(argv=None):
                          "overhead")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: hidden-layer forwards on e4m3 MX-MFMA (BASELINE config 5)")
-    ap.add_argument("--secondary", default="128:fp8,256:bf16,256:fp8",
-                    help="after the headline: other configs as CHANNELS:DTYPE,... ('' = none)")
+    ap.add_argument("--secondary", default="128:fp8,256:bf16,256:fp8,256:bf16:fixture",
+                    help="after the headline: other configs as CHANNELS:DTYPE[:fixture],... "
+                         "('' = none; fixture = the reference's bundled games through the C++ "
+                         "loader, BASELINE config 4)")
     ap.add_argument("--no-report", action="store_true",
                     help="skip the post-timing DP report (isolated collectives, no-comm step)")
     ap.add_argument("--spinup-steps", type=int, default=300,
@@ -141,7 +148,7 @@ def parse(argv=None):
                          "run may use the budget minus a 150-s reserve; if a rank's guard "
                          "reports a hang while it was on the native communicator, the "
                          "fallback run gets what is left.  Worst case: %(default)s s")
-    ap.add_argument("--accuracy-steps", type=int, default=1000,
+    ap.add_argument("--accuracy-steps", type=int, default=3000,
                     help="after the timed phases (untimed): train the bench's network this many "
                          "SGD steps (batch 64) on the reference's bundled training games and "
                          "report top-1 / NLL on the held-out validation and test games "
@@ -403,16 +410,31 @@ def run_cpu_dry(args) -> int:
     return 0
 
 
-class _Case:
-    """One configuration's network, input pool, optional DP bucketer and step graph."""
+FIXTURE_TRAIN = os.path.join(HERE, "tests", "fixtures", "train.dgpack.npz")
 
-    def __init__(self, args, channels, dtype, world, info, dev, comm, use_dp):
+
+class _Case:
+    """One configuration's network, input source, optional DP bucketer and step graph.
+
+    Input sources: the synthetic pool (``data="synthetic"``: --pool packed batches in pinned
+    host memory, each step's batch an H2D copy prefetched beside the previous step — the
+    reference's per-step host->device copy, train.lua:99-100 — or, with --device-pool, in
+    device memory) or ``data="fixture"``: the reference's bundled training games
+    (tests/fixtures/train.dgpack.npz, 4139 real positions) sampled game-uniformly by the C++
+    loader threads into pinned ring slots, one prefetched H2D copy per step, the 37 planes
+    expanded on the GPU (BASELINE config 4: data.lua:82-96, dataloader.lua:113-125)."""
+
+    def __init__(self, args, channels, dtype, world, info, dev, comm, use_dp,
+                 grad_dtype=None, data="synthetic"):
         import torch
         from deep_go_amd.config import get_preset
         from deep_go_amd.data.synthetic import random_planes
         from deep_go_amd.models.hip_model import HipGoNet, SegmentedStep, pack_batch
         from deep_go_amd.parallel import dp
         self.args, self.channels, self.dtype = args, channels, dtype
+        self.grad_dtype = grad_dtype or args.grad_dtype
+        self.data = data
+        self.loader = None
         B = args.batch
         self.cfg = get_preset("12x128-bf16", numLayers=args.layers, channelSize=channels,
                               batchSize=B * world, seed=1234, dtype=dtype)
@@ -429,34 +451,52 @@ class _Case:
         # (--grad-dtype bf16: the gradient reduces write the bf16 wire twin themselves)
         self.net = net = HipGoNet(self.cfg, B, device=dev, global_batch=B * world,
                                   wgrad_group=wg,
-                                  grad_wire=args.grad_dtype if use_dp else "fp32")
+                                  grad_wire=self.grad_dtype if use_dp else "fp32")
+        host = data == "fixture" or not args.device_pool
         # input prefetch (the next batch's copy on a load stream beside the previous step):
-        # on for the pinned host pool (SDMA copies, +1.1%), off for the device pool (its
-        # blit-kernel copy beside the step measured -1%; profiles/r2_input_prefetch_ab.txt)
+        # on for host sources (SDMA copies), off for the device pool (its blit-kernel copy
+        # beside the step measured -1%; profiles/r2_input_prefetch_ab.txt)
         pf = os.environ.get("DG_PREFETCH", "auto")
-        self.prefetch = (pf == "1" or (pf != "0" and args.host_pool)) and net.enable_prefetch()
+        self.prefetch = (pf == "1" or (pf != "0" and host)) and net.enable_prefetch()
+        self.input = ("host pinned, prefetched H2D" if host and self.prefetch else
+                      "host pinned, H2D in the step" if host else "device-resident pool")
         if world > 1:
             comm.broadcast_(net.params, 0)
             net.refresh_weights()
-        # synthetic data pool (different per rank), packed [planes | player | rank | labels]
-        # batches: one copy per step
-        planes, player, rank, labels = random_planes(B * args.pool, seed=1000 + info.rank)
-        pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
-                                       rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
-                            for j in range(args.pool)])
-        self.pool = pool.pin_memory() if args.host_pool else pool.to(dev)
+        self.pool = None
+        if data == "fixture":
+            from deep_go_amd.data.dataset import PackedDataset
+            from deep_go_amd.data.loader import BatchLoader
+            self.loader = BatchLoader(PackedDataset.load(FIXTURE_TRAIN), B, threads=4,
+                                      prefetch=6, seed=7 + 1009 * info.rank)
+        else:
+            # synthetic data pool (different per rank), packed [planes | player | rank |
+            # labels] batches: one copy per step
+            planes, player, rank, labels = random_planes(B * args.pool, seed=1000 + info.rank)
+            pool = torch.stack([pack_batch(planes[j * B:(j + 1) * B], player[j * B:(j + 1) * B],
+                                           rank[j * B:(j + 1) * B], labels[j * B:(j + 1) * B])
+                                for j in range(args.pool)])
+            self.pool = pool.pin_memory() if host else pool.to(dev)
         self.bucketer = None
         if use_dp:
             lay = net.layout
             ranges = [lay.layer_range(i) for i in range(len(lay.layers))]
             buckets = dp.make_buckets(ranges, int(args.bucket_mb * 2 ** 20), groups=net.wgroups)
-            self.bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=args.grad_dtype,
+            self.bucketer = dp.GradBucketer(net.grads, buckets, grad_dtype=self.grad_dtype,
                                             comm=comm, shadow=net.grads16)
         self.load(0)
         self.step = SegmentedStep(net, self.bucketer, use_graphs=not args.no_graph)
 
     def load(self, i):
-        self.net.set_batch_packed(self.pool[i % self.args.pool])
+        if self.loader is not None:
+            self.net.set_batch_packed_from(self.loader)
+        else:
+            self.net.set_batch_packed(self.pool[i % self.args.pool])
+
+    def close(self):
+        if self.loader is not None:
+            self.loader.close()
+            self.loader = None
 
     def run(self, n):
         for i in range(n):
@@ -630,7 +670,7 @@ def run_gpu(args) -> int:
         raise SystemExit(f"rank {info.rank}: parameters diverged across ranks")
     extra = {"last_loss": round(loss, 4), "graphs": not args.no_graph,
              "step_mode": case.step.mode, "spinup_steps": args.spinup_steps,
-             "input_prefetch": bool(case.prefetch)}
+             "input_prefetch": bool(case.prefetch), "input": case.input}
     step_ms = 1000.0 * max(elapsed_all) / args.steps
     # gradient precision of the step: single-GPU gradients are reduced in fp32 (split-K slabs
     # + fused update); under DP the bucket all-reduces run in --grad-dtype
@@ -644,36 +684,64 @@ def run_gpu(args) -> int:
     if phases:
         extra["profile_host_ms_per_step"] = phases
     headline = _record(args, world, elapsed_all, case.cfg.train_flops_per_board(), extra)
+    case.close()
     del case
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
 
-    # secondary configurations (never inside the headline's timed region)
+    # secondary configurations (never inside the headline's timed region): CH:DTYPE[:fixture]
+    # (fixture = the reference's games through the C++ loader, BASELINE config 4), and under
+    # DP the headline network on the bf16 gradient wire (labelled: the headline is fp32)
+    items = [x.split(":") for x in args.secondary.split(",") if x]
+    if (use_dp and world > 1 and args.grad_dtype == "fp32"
+            and not args.no_bf16_wire_secondary):
+        items.append([str(args.channels), args.dtype, "wire16"])
     sec = {}
-    for item in [x for x in args.secondary.split(",") if x]:
-        ch, dt = item.split(":")
-        if int(ch) == args.channels and dt == args.dtype:
+    for it in items:
+        ch, dt = it[0], it[1]
+        var = it[2] if len(it) > 2 else ""
+        if var not in ("", "fixture", "wire16"):
+            raise SystemExit(f"--secondary {':'.join(it)}: unknown variant {var!r}")
+        if int(ch) == args.channels and dt == args.dtype and not var:
             continue
-        tag = item.replace(":", "-")     # (the status file is colon-separated)
+        tag = "-".join(it)     # (the status file is colon-separated)
         guard.phase(f"sec-{tag}-capture", args.phase_timeout)
-        c2 = _Case(args, int(ch), dt, world, info, dev, comm, use_dp)
+        c2 = _Case(args, int(ch), dt, world, info, dev, comm, use_dp,
+                   grad_dtype="bf16" if var == "wire16" else None,
+                   data="fixture" if var == "fixture" else "synthetic")
         guard.phase(f"sec-{tag}-warmup", args.phase_timeout)
         c2.run(100)
         c2.run(args.warmup)
         guard.phase(f"sec-{tag}-timed", args.phase_timeout)
+        if c2.loader is not None:
+            c2.loader.wait_s = 0.0
         t = c2.timed(args.steps, dev)
         ok = c2.params_identical(world)
         if not ok:
-            raise SystemExit(f"rank {info.rank}: parameters diverged across ranks ({item})")
+            raise SystemExit(f"rank {info.rank}: parameters diverged across ranks ({tag})")
         el = max(t)
-        sec[f"12x{ch}-{dt}" if args.layers == 12 else f"{args.layers}x{ch}-{dt}"] = {
+        name = (f"12x{ch}-{dt}" if args.layers == 12 else f"{args.layers}x{ch}-{dt}")
+        name = {"fixture": name + "-fixture", "wire16": "dp-bf16-wire"}.get(var, name)
+        rec = {
             "value": round(args.batch * world * args.steps / el, 1), "unit": "boards/s",
             "ms_per_step": round(1000.0 * el / args.steps, 4), "steps": args.steps,
             "warmup": args.warmup, "spinup_steps": 100, "dtype": dt,
             "model": _model_name(args.layers, int(ch)), "global_batch": args.batch * world,
-            "parallelism": f"dp{world}", "step_mode": c2.step.mode,
+            "parallelism": f"dp{world}", "step_mode": c2.step.mode, "input": c2.input,
             "achieved_tflops": round(c2.cfg.train_flops_per_board() * args.batch * world
                                      * args.steps / el / 1e12, 2)}
+        if use_dp:
+            rec["grad_dtype"] = c2.grad_dtype
+        if var == "wire16":
+            rec["label"] = ("the headline network with the bf16 gradient wire (NOT the "
+                            "reference's fp32 gradient reduce)")
+        if c2.loader is not None:
+            rec["data"] = ("fixture (C++ loader): the reference's 20 bundled training games, "
+                           "4139 real positions, game-uniform sampling, 4 loader threads")
+            rec["loader_wait_us_per_step"] = round(1e6 * c2.loader.wait_s / args.steps, 1)
+            rec["loader_errors"] = c2.loader.errors()
+        sec[name] = rec
+        c2.close()
         del c2
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

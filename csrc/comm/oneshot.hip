@@ -102,7 +102,12 @@ __global__ void __launch_bounds__(256) oneshot_allreduce_kernel(OneShotArgs a) {
     }
   }
   __syncthreads();
-  // 4. sum in rank order (a timed-out block: NaN over its share, never a stale sum)
+  // 4. sum in rank order (a timed-out block: NaN over its share, never a stale sum).  The NaN
+  // only reaches THIS rank: a late peer that still finds this rank's flag sums normally and
+  // applies its step, so the replicas can differ for the step in flight.  What keeps them
+  // consistent is the error word (state[3]): the host's async-error poll (NativeComm.async_error
+  // reads dp.IpcOneShot.error; the step watchdog polls it) aborts the whole job on any rank's timeout
+  // before further steps are issued — the NaN only keeps this rank from applying a stale sum.
   const bool timed_out = s_timeout != 0u;
   for (long long i = gid; i < a.nvec; i += stride) {
     if (timed_out) {

@@ -50,13 +50,6 @@ hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, cons
                                      const long long* y8, hipStream_t stream);
 hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                           hipStream_t stream);
-hipError_t dg_conv_stack2_dgrad_sig(const long long* table, int nl, const void* X0, int B,
-                                    unsigned* sig, hipStream_t stream);
-int dg_bias_follow_tasks(int nl, int B, int C);
-void dg_bias_follow_set_variant(int aux, int sleep);
-hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned* sig, int nsig,
-                          unsigned* done, int mode, int grid, double timeout_us, long long* sf,
-                          hipStream_t s);
 hipError_t dg_conv_stack2_fwd_head(const long long* table, int nl, const void* X0, int l1, int B,
                                    const float* w, const float* bias, const float* posb,
                                    const int* labels, float* loss, int* pred, void* dZ,
@@ -81,7 +74,6 @@ hipError_t dg_conv_wgrad_multi(int kw, const long long* table, int nl, int dz_pa
                                hipStream_t stream);
 int dg_conv_l1_ok(int kw, int x_pad, int x_C, int Mpad, int KP);
 int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad);
-void dg_conv_l1_frag_set_half(int on);
 hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
                            void* Y, void* mask, const void* planes, const void* player,
                            const void* rank, hipStream_t stream);
@@ -341,24 +333,6 @@ PYBIND11_MODULE(_dghip, m) {
     check(dg_conv_stack2(epi, P<long long>(table), nl, P<void>(X0), l1, B, S(stream)),
           "conv_stack2");
   }, "conv_stack2: EPI_FWD forward or EPI_DGRAD backward-data chain (fragment-ordered A)");
-  m.def("conv_stack2_dgrad_sig", [](uintptr_t table, int nl, uintptr_t X0, int B, uintptr_t sig,
-                                    uintptr_t stream) {
-    check(dg_conv_stack2_dgrad_sig(P<long long>(table), nl, P<void>(X0), B, P<unsigned>(sig),
-                                   S(stream)),
-          "conv_stack2_dgrad_sig");
-  }, "conv_stack2 backward-data chain storing each row write-through and counting it in sig[row] "
-     "(the bias-gradient follower's arrival counters)");
-  m.def("bias_follow_tasks", [](int nl, int B, int C) { return dg_bias_follow_tasks(nl, B, C); });
-  m.def("bias_follow_set_variant", [](int aux, int sleep) { dg_bias_follow_set_variant(aux, sleep); },
-        "kbench A/B: the follower's dZ load cache policy (0 / 2 nt / 16 sc1) and poll interval");
-  m.def("bias_follow", [](uintptr_t table, int nl, int B, int C, uintptr_t sig, int nsig,
-                          uintptr_t done, int mode, int grid, double timeout_us, uintptr_t sf,
-                          uintptr_t stream) {
-    check(dg_bias_follow(P<long long>(table), nl, B, C, P<unsigned>(sig), nsig,
-                         P<unsigned>(done), mode, grid, timeout_us, P<long long>(sf), S(stream)),
-          "bias_follow");
-  }, "bias-gradient partials beside the backward-data stack: mode 0 follow pass, 1 finish pass; "
-     "table rows {dZ, part, ready row (-1: ready)}");
   m.def("conv_wgrad", [](int kw, uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X,
                          int x_pad, int x_C, int B, int KP, int splits, uintptr_t slab,
                          uintptr_t stream) {
@@ -577,8 +551,6 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_l1_frag_ok", [](int kw, int x_pad, int x_C, int M, int y_pad) {
     return dg_conv_l1_frag_ok(kw, x_pad, x_C, M, y_pad);
   });
-  m.def("conv_l1_frag_set_half", [](int on) { dg_conv_l1_frag_set_half(on); },
-        "conv_l1_frag: 1 two half-board workgroups per board (two per CU), 0 one per board");
   m.def("conv_layer2", [](int epi, uintptr_t A, uintptr_t pbias, uintptr_t X, uintptr_t Y,
                          uintptr_t mask, int C, int B, uintptr_t stream) {
     check(dg_conv_layer2(epi, P<void>(A), P<void>(pbias), P<void>(X), P<void>(Y), P<void>(mask),

@@ -241,9 +241,9 @@ struct L1FragArgs {
   const uint8_t* in_rank;     // [B]
 };
 
-// NFX = 6: one workgroup per board (4 x 96 pixels); NFX = 3: two per board, each 4 x 48 of
-// its pixels (fragments 12 h .. 12 h + 11), <= 128 VGPRs so two fit on a CU and one's prologue
-// (frame staging / feature expansion) and epilogue overlap the other's MFMAs
+// NFX = 6: one workgroup per board (4 x 96 pixels).  (NFX = 3, two half-board workgroups per
+// board and two per CU, measured neutral in the step and was removed in round 6:
+// profiles/r5_l1_half_ab.txt)
 template <int NFX>
 __global__ void __launch_bounds__(512, NFX == 6 ? 1 : 2) conv_l1_frag_kernel(L1FragArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -425,13 +425,6 @@ int dg_conv_l1_frag_ok(int kw, int x_pad, int x_C, int M, int y_pad) {
   return kw == 5 && x_pad == 2 && x_C == 40 && M % 128 == 0 && M <= 512 && y_pad == 1;
 }
 
-// conv_l1_frag's workgroups per board: 2 (half-board, two per CU; DG_L1_HALF=1) or 1
-int g_l1_half = [] {
-  const char* e = getenv("DG_L1_HALF");
-  return e && *e == '1' ? 1 : 0;
-}();
-void dg_conv_l1_frag_set_half(int on) { g_l1_half = on ? 1 : 0; }
-
 hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int M,
                            void* Y, void* mask, const void* planes, const void* player,
                            const void* rank, hipStream_t stream) {
@@ -442,16 +435,11 @@ hipError_t dg_conv_l1_frag(const void* A, const void* pbias, void* X, int B, int
   if (!done) {
     (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel<6>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
-    (void)hipFuncSetAttribute((const void*)conv_l1_frag_kernel<3>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
     done = true;
   }
   L1FragArgs a{(const char*)A, (const uint2*)pbias, (char*)X, (char*)Y, (uint8_t*)mask, M,
                M / 128, (const uint8_t*)planes, (const uint8_t*)player, (const uint8_t*)rank};
-  if (g_l1_half)
-    hipLaunchKernelGGL(conv_l1_frag_kernel<3>, dim3(2 * B), dim3(512), PF_LDS, stream, a);
-  else
-    hipLaunchKernelGGL(conv_l1_frag_kernel<6>, dim3(B), dim3(512), PF_LDS, stream, a);
+  hipLaunchKernelGGL(conv_l1_frag_kernel<6>, dim3(B), dim3(512), PF_LDS, stream, a);
   return hipGetLastError();
 }
 

@@ -94,12 +94,6 @@ struct StackArgs {
   // (s_sleep 127 rounds)
   int stag_prio;
   int stag_delay;
-  // EPI_DGRAD with the bias-gradient follower (SIG): per-row arrival counters.  Row r's output
-  // frame is stored write-through (sc1) and, once every wave of the workgroup has drained its
-  // stores (s_waitcnt vmcnt(0) + barrier), one lane adds 1 to sig[r] (agent scope): the
-  // follower kernel (elementwise.hip bias_follow_kernel), co-resident on the side stream, reads
-  // a row's frame as soon as all B boards have arrived, instead of after this launch.
-  unsigned* sig;
 };
 
 DG_DEV int fsig(int f) { return ((f % F) + 3 * (f / F)) & 7; }
@@ -164,11 +158,10 @@ DG_DEV uint32_t pair_mask(uint32_t nib) {
 // MODE: 0 in production; timing ablations for tools/kbench_stack.py (wrong results):
 // 2 = no A loads in the K loop, 4 = no copy-out, 8 = no B reads in the K loop, 16 = no
 // epilogue (nothing written back into the image)
-template <int EPI, int MODE, bool SIG = false, bool STAG = false>
+template <int EPI, int MODE, bool STAG = false>
 __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
   // epilogue schedule (see the K loop)
   constexpr bool TWO_GROUP = EPI == EPI_DGRAD && !STAG;
-  static_assert(!(SIG && STAG), "the follower's row signals need the barrier schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -320,16 +313,7 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     const int h = p / BOARD, w = p - (p / BOARD) * BOARD;
     const int f = (h + 1) * F + (w + 1);
     const int co_q = hf * 8 + (tid & 7);
-    if constexpr (SIG) {
-      // write-through (sc1): the follower reads the frame inside this launch (no release fence)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Lo.Y, 0, 0x7fffffff,
-                                                                          0x00020000);
-      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{v.x, v.y, v.z, v.w}, rs,
-                                             (int)(((b * FF + f) * C) * 2 + co_q * 16), 0, 16);
-    } else {
-      *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
-    }
+    *(uint4*)(Lo.Y + ((size_t)(b * FF + f) * C) * 2 + co_q * 16) = v;
     if (EPI == EPI_FWD && Lo.mask) {
       // bit per nonzero bf16 half (post-ReLU: every half is in [0, 0x7fff]): h + 0x7fff has
       // bit 15 set iff h != 0, with no carry out of the half; gather bits 15 / 31 of the
@@ -533,12 +517,7 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     }
     if constexpr (TWO_GROUP) {
       if (wm == 0) write_out();  // image 0: dead since barrier A
-      // SIG: every wave's copy-out stores of the previous row's output (K-steps 0..14 of this
-      // row) drained before barrier B; then one lane signals that row for this board
-      if (SIG && l > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();             // B
-      if (SIG && l > 0 && tid == 0)
-        __hip_atomic_fetch_add(a.sig + (l - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (wm == 1) write_out();  // image 1 (the next layer's barrier A publishes it)
       continue;
     }
@@ -567,29 +546,23 @@ __global__ void __launch_bounds__(NT) conv_stack2_kernel(StackArgs a) {
     for (int s_ = 0; s_ < CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
     for (int s_ = T; s_ < T + CO_STEPS; ++s_) co_store(s_, co_read(s_), Ll);
   }
-  if constexpr (SIG) {   // the last row's output
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-      __hip_atomic_fetch_add(a.sig + (a.nl - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   // the policy head on the board image that is already in LDS (no re-staging, no launch)
   if constexpr (EPI == EPI_FWD) {
     if (a.fuse_head) dghead::head_body<C>(a.head, b, sH, smem, [](int) {});
   }
 }
 
-template <int EPI, int MODE, bool SIG = false, bool STAG = false>
+template <int EPI, int MODE, bool STAG = false>
 hipError_t launch_stack2(const StackArgs& a, int B, hipStream_t stream) {
   constexpr size_t lds = SCRATCH + 2 * (size_t)H_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)conv_stack2_kernel<EPI, MODE, SIG, STAG>,
+    (void)hipFuncSetAttribute((const void*)conv_stack2_kernel<EPI, MODE, STAG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     done = true;
   }
-  hipLaunchKernelGGL((conv_stack2_kernel<EPI, MODE, SIG, STAG>), dim3(B), dim3(NT), lds, stream,
+  hipLaunchKernelGGL((conv_stack2_kernel<EPI, MODE, STAG>), dim3(B), dim3(NT), lds, stream,
                      a);
   return hipGetLastError();
 }
@@ -617,7 +590,7 @@ void stack2_sched_from_env() {
 hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                          const dghead::HeadMArgs* head, hipStream_t stream,
                          const uint8_t* in_planes = nullptr, const uint8_t* in_player = nullptr,
-                         const uint8_t* in_rank = nullptr, unsigned* sig = nullptr) {
+                         const uint8_t* in_rank = nullptr) {
   if (nl <= 0 || nl > MAXL || B <= 0) return hipErrorInvalidValue;
   if (epi != EPI_FWD && epi != EPI_DGRAD) return hipErrorInvalidValue;
   if (l1 && (epi != EPI_FWD || nl < 2)) return hipErrorInvalidValue;
@@ -630,14 +603,10 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
   a.in_rank = in_rank;
   a.fuse_head = 0;
   a.head = dghead::HeadMArgs{};
-  a.sig = sig;
   stack2_sched_from_env();
   a.stag_prio = g_stack2_prio;
   a.stag_delay = g_stack2_delay;
-  const bool stag = (g_stack2_stag == 1 || (g_stack2_stag == 2 && epi == EPI_DGRAD)) && !sig;
-  if (sig && epi != EPI_DGRAD) return hipErrorInvalidValue;
-  // (the buffer stores address a row's frame with 32-bit offsets)
-  if (sig && (size_t)B * FF * C * 2 > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool stag = g_stack2_stag == 1 || (g_stack2_stag == 2 && epi == EPI_DGRAD);
   a.X0 = (const char*)X0;
   a.nl = nl;
   for (int i = 0; i < nl; ++i) {
@@ -655,17 +624,16 @@ hipError_t stack2_launch(int epi, const long long* table, int nl, const void* X0
     a.head = *head;
   }
   if (epi == EPI_DGRAD) {
-    if (sig) return launch_stack2<EPI_DGRAD, 0, true>(a, B, stream);
     if (stag) {
-      if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16, false, true>(a, B, stream);
-      return launch_stack2<EPI_DGRAD, 0, false, true>(a, B, stream);
+      if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16, true>(a, B, stream);
+      return launch_stack2<EPI_DGRAD, 0, true>(a, B, stream);
     }
     if (g_stack2_mode == 16) return launch_stack2<EPI_DGRAD, 16>(a, B, stream);
     return launch_stack2<EPI_DGRAD, 0>(a, B, stream);
   }
   if (stag) {
-    if (g_stack2_mode == 16) return launch_stack2<EPI_FWD, 16, false, true>(a, B, stream);
-    return launch_stack2<EPI_FWD, 0, false, true>(a, B, stream);
+    if (g_stack2_mode == 16) return launch_stack2<EPI_FWD, 16, true>(a, B, stream);
+    return launch_stack2<EPI_FWD, 0, true>(a, B, stream);
   }
   switch (g_stack2_mode) {  // forward: the MODE ablations too (kbench_stack.py)
     case 2: return launch_stack2<EPI_FWD, 2>(a, B, stream);
@@ -700,15 +668,6 @@ void dg_conv_stack2_set_sched(int stag, int prio, int delay) {
 hipError_t dg_conv_stack2(int epi, const long long* table, int nl, const void* X0, int l1, int B,
                           hipStream_t stream) {
   return stack2_launch(epi, table, nl, X0, l1, B, nullptr, stream);
-}
-
-// Backward-data chain signalling each row's output to the bias-gradient follower: sig[r] +=
-// 1 per board once row r's frame is stored (write-through); sig must hold nl zeroed counters.
-hipError_t dg_conv_stack2_dgrad_sig(const long long* table, int nl, const void* X0, int B,
-                                    unsigned* sig, hipStream_t stream) {
-  if (!sig) return hipErrorInvalidValue;
-  return stack2_launch(EPI_DGRAD, table, nl, X0, 0, B, nullptr, stream, nullptr, nullptr,
-                       nullptr, sig);
 }
 
 // Forward stack + the 3x3 / 128-channel policy head fused after its last layer.

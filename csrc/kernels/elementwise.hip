@@ -276,181 +276,6 @@ bias_partial_units_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
 }
 
 // ------------------------------------------------------------------------------------
-// Bias-gradient pass 1 BESIDE the backward-data stack ("follower").  The partials above read
-// 289 MB of dZ frames (12x128) and are HBM-bound; beside the MFMA-bound window weight
-// gradient they stretched 3x (65 -> 200 us) and pushed the first layer's 5x5 weight gradient
-// past the window kernel's end: the step's critical tail.  The backward-data stack
-// (conv_stack2.hip EPI_DGRAD) is MFMA-bound too but produces the dZ frames one layer at a
-// time and leaves HBM mostly idle, so the partials of a layer can run as soon as the stack has
-// stored it — here, co-resident with the stack: 256-thread workgroups of <= 32 VGPRs (the
-// stack's 2 x 240-VGPR waves leave 32 per SIMD) and 9 KB of LDS (the stack leaves 36 KB).
-//
-// Work: per layer, tasks (board chunk c of 64, board row h, 64-channel block q).  A task's
-// 256 threads are 8 board sub-chunks k (8 boards each) x 32 lanes; per pass, lane j owns item
-// (pixel w, 4 channels) and sums its 8 boards in order (8 x 8-B loads in flight), then the 8
-// sub-chunk sums of an item are added in k order through LDS: a fixed order for every element
-// (the finish pass runs the same routine, so who computes a task never changes the bits).
-// Output: the layout of bias_grad_partial_kernel (part[chunk][p][C] + row partials
-// [chunk][h][C]), read unchanged by the pass 2 (wgrad_reduce_multi, grad_update).
-//
-// Protocol (follow pass, one workgroup per CU; MI355X_MICROARCH.md "Valid forms", row 1): the
-// stack stores a row's frame write-through (sc1), drains (vmcnt(0)) in every wave, crosses a
-// barrier and ONE lane adds 1 to sig[row] (agent scope).  A follower workgroup polls that
-// counter from one lane (relaxed agent loads, s_sleep) until all B boards arrived, takes ONE
-// agent acquire (buffer_inv sc1: this CU's L1), drains it and barriers, then reads with plain
-// loads.  Every wait is BOUNDED (timeout_ticks of s_memrealtime): a workgroup that times out —
-// the stack not running beside it (AMD_SERIALIZE_KERNEL, a full machine) — simply exits and
-// its remaining tasks fall to the finish pass.  A processed task sets done[task].
-// Finish pass (after the stack; same stream as the follow pass): every task whose done flag is
-// 0 is computed now; every flag and the stack's counters are reset for the next step.
-// Reference: nn.Add / conv bias backward (experiments.lua:138,144).
-constexpr int BF_MAXL = 16;
-constexpr int BF_SUB = 8;                 // boards per thread (one sub-chunk)
-constexpr int BF_CQ = 64;                 // channels per task (128 contiguous bytes per pixel)
-constexpr int BF_ITEMS = BOARD * BF_CQ / 4;   // (pixel, 4-channel group) items per task: 304
-constexpr int BF_PASSES = (BF_ITEMS + 31) / 32;
-struct BiasFollowArgs {
-  const char* dZ[BF_MAXL];    // bf16 frames [B][21][21][C]
-  float* part[BF_MAXL];       // [nchunks][361][C] + [nchunks][19][C]
-  int ready[BF_MAXL];         // sig index of the stack row that writes the frame; -1: ready
-  int nl, B, C, nchunks;
-  unsigned* sig;              // the stack's per-row arrival counters
-  int nsig;
-  unsigned* done;             // [nl * tasks per layer]
-  long long timeout_ticks;    // follow pass: per-wait limit (s_memrealtime, 100 MHz)
-  int sleep;                  // follow pass: poll interval in s_sleep(16) units (~0.45 us)
-  long long* sf;              // the fused update's step tag (dg_common.h)
-};
-
-__host__ __device__ inline int bf_tasks_per_layer(int nchunks, int C) {
-  return nchunks * BOARD * (C / BF_CQ);
-}
-
-// one task, all 256 threads (contains barriers).  Written for the 32-VGPR budget beside the
-// stack: lane values are recomputed from threadIdx each pass, global traffic goes through
-// buffer resources (uniform bases in SGPRs, one VGPR offset per lane).
-template <int AUX>
-DG_DEV void bias_follow_task(const BiasFollowArgs& a, int l, int t, f32x4* s_comb,
-                             float* s_row) {
-  const int nq = a.C / BF_CQ;
-  const int c = t / (BOARD * nq);
-  const int rem = t - c * (BOARD * nq);
-  const int h = rem / nq, q = rem - (rem / nq) * nq;
-  const int C = a.C;
-  constexpr int F = BOARD + 2;
-  const int bstride = F * F * C * 2;       // (< 2^31 for the whole frame: host-checked)
-  // 8 boards' strides as uniform soffsets; boards past B read out of range -> 0
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.dZ[l], 0, a.B * bstride, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.part[l], 0, 0x7fffffff, 0x00020000);
-  // uniform byte offsets: this task's row of board 0 / its part row / its row partial
-  const int row0 = ((h + 1) * F + 1) * C * 2 + q * BF_CQ * 2 + c * BG_BT_MULTI * bstride;
-  const int prow = ((c * NPTS + h * BOARD) * C + q * BF_CQ) * 4;
-  const int rrow = ((a.nchunks * NPTS + c * BOARD + h) * C + q * BF_CQ) * 4;
-#pragma unroll 1
-  for (int pass = 0; pass < BF_PASSES; ++pass) {
-    const int tid = threadIdx.x;
-    const int item = pass * 32 + (tid & 31);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (item < BF_ITEMS) {
-      // item = (pixel w, 4-channel group g): w * C * 2 + g * 8 bytes into the row; the
-      // thread's 8 boards start at sub-chunk k = tid >> 5
-      const int voff = row0 + (item >> 4) * C * 2 + (item & 15) * 8 + (tid >> 5) * BF_SUB * bstride;
-      u32x2v v[BF_SUB];
-#pragma unroll
-      for (int i = 0; i < BF_SUB; ++i)
-        v[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, i * bstride, AUX);
-      // one board at a time (sched barriers): unpacked all at once the 8 loads' halves need
-      // 32 more VGPRs than the budget beside the stack
-      float m = 0.f;
-#pragma unroll
-      for (int i = 0; i < BF_SUB; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
-        const float x0 = __uint_as_float(v[i].x << 16), x1 = __uint_as_float(v[i].x & 0xFFFF0000u);
-        const float x2 = __uint_as_float(v[i].y << 16), x3 = __uint_as_float(v[i].y & 0xFFFF0000u);
-        acc[0] += x0;
-        acc[1] += x1;
-        acc[2] += x2;
-        acc[3] += x3;
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(x0), fabsf(x1)), fmaxf(fabsf(x2), fabsf(x3))));
-      }
-      // the step tag (NaN shows in the sums); rare, so the branch stays cheap
-      if (a.sf && (!(m < DZ_BOUND) || !__builtin_isfinite(acc[0] + acc[1] + acc[2] + acc[3])))
-        flag_bad_step(a.sf);
-    }
-    f32x4* cb = s_comb + (pass & 1) * (BF_SUB * 32);   // double-buffered: one barrier a pass
-    cb[tid] = acc;                                      // [k][j]
-    __syncthreads();
-    if (tid < 128) {
-      const int jj = tid >> 2, e = tid & 3;
-      const int it2 = pass * 32 + jj;
-      if (it2 < BF_ITEMS) {
-        float s2 = cb[jj][e];
-#pragma unroll
-        for (int kk = 1; kk < BF_SUB; ++kk) s2 += cb[kk * 32 + jj][e];
-        const int chp = (it2 >> 4) * C + (it2 & 15) * 4 + e;   // w * C + channel in block
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s2), ws, prow + chp * 4, 0, 0);
-        s_row[(it2 >> 4) * BF_CQ + (it2 & 15) * 4 + e] = s2;
-      }
-    }
-  }
-  __syncthreads();
-  const int tid = threadIdx.x;
-  if (tid < BF_CQ) {
-    float sc = 0.f;
-    for (int w = 0; w < BOARD; ++w) sc += s_row[w * BF_CQ + tid];
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sc), ws, rrow + tid * 4, 0, 0);
-  }
-  __syncthreads();   // s_row / s_comb free for the next task
-}
-
-// mode 0: follow pass (beside the stack); 1: finish pass
-template <int MODE, int AUX>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16)))
-bias_follow_kernel(BiasFollowArgs a) {
-  __shared__ f32x4 s_comb[2 * BF_SUB * 32];
-  __shared__ float s_row[BOARD * BF_CQ];
-  __shared__ int s_ok;
-  const int tid = threadIdx.x;
-  const int T = bf_tasks_per_layer(a.nchunks, a.C);
-  const int total = a.nl * T;
-  if (MODE == 1 && blockIdx.x == 0 && tid < a.nsig) a.sig[tid] = 0u;   // (the stack has ended)
-  for (int g = blockIdx.x; g < total; g += gridDim.x) {
-    const int l = g / T, t = g - l * T;
-    if constexpr (MODE == 0) {
-      const int ri = a.ready[l];
-      if (ri >= 0) {
-        if (tid == 0) {
-          int ok = 1;
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(a.sig + ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                 (unsigned)a.B) {
-            for (int z = 0; z < a.sleep; ++z) __builtin_amdgcn_s_sleep(16);
-            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-              ok = 0;
-              break;
-            }
-          }
-          if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          s_ok = ok;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (holds the barrier for the inv)
-        __syncthreads();
-        if (!s_ok) return;   // not ready in time: the finish pass takes the rest
-      }
-      bias_follow_task<AUX>(a, l, t, s_comb, s_row);
-      if (tid == 0) a.done[g] = 1u;
-    } else {
-      const unsigned d = a.done[g];   // (uniform: every thread reads the same word)
-      if (!d) bias_follow_task<AUX>(a, l, t, s_comb, s_row);
-      __syncthreads();                // every thread read the flag before it is reset
-      if (tid == 0 && d) a.done[g] = 0u;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // gradient element i as fp32: the flat fp32 gradient, or its bf16 twin (the data-parallel
 // bf16 wire format: the all-reduced bucket is read as it came off the wire)
 DG_DEV float grad_at(const float* g, size_t i) { return g[i]; }
@@ -1364,58 +1189,6 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
   hipLaunchKernelGGL(bias_grad_partial_kernel<2>, dim3(BOARD, nchunks, nl), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);
   return hipGetLastError();
-}
-// The bias-gradient follower (see bias_follow_kernel).  table: nl rows of {dZ frame, part,
-// ready row (-1: ready at launch)}, in the order the stack produces them.  mode 0: the follow
-// pass (grid = one workgroup per CU, launched beside the stack; timeout_us bounds each wait);
-// mode 1: the finish pass (after the stack).  done: >= dg_bias_follow_tasks(nl, B, C) zeroed
-// words; sig: the stack's nsig counters.
-int g_bf_aux = 0;     // load cache policy of the follower's dZ stream
-int g_bf_sleep = 4;   // poll interval (s_sleep(16) units)
-int dg_bias_follow_tasks(int nl, int B, int C) {
-  return nl * bf_tasks_per_layer((B + BG_BT_MULTI - 1) / BG_BT_MULTI, C);
-}
-hipError_t dg_bias_follow(const long long* table, int nl, int B, int C, unsigned* sig, int nsig,
-                          unsigned* done, int mode, int grid, double timeout_us, long long* sf,
-                          hipStream_t s) {
-  if (nl <= 0 || nl > BF_MAXL || C % BF_CQ != 0 || C > 1024 || !sig || !done || grid < 1 ||
-      nsig < 1 || nsig > 256 || (size_t)B * 441 * C * 2 > 0x7fffffffull)
-    return hipErrorInvalidValue;
-  BiasFollowArgs a{};
-  for (int i = 0; i < nl; ++i) {
-    a.dZ[i] = (const char*)table[3 * i];
-    a.part[i] = (float*)table[3 * i + 1];
-    a.ready[i] = (int)table[3 * i + 2];
-    if (!a.dZ[i] || !a.part[i] || a.ready[i] >= nsig) return hipErrorInvalidValue;
-  }
-  a.nl = nl;
-  a.B = B;
-  a.C = C;
-  a.nchunks = (B + BG_BT_MULTI - 1) / BG_BT_MULTI;
-  a.sig = sig;
-  a.nsig = nsig;
-  a.done = done;
-  a.timeout_ticks = (long long)(timeout_us * 100.0);
-  a.sleep = g_bf_sleep;
-  a.sf = sf;
-  // load cache policy of the dZ stream (kbench A/B: tools/kbench_follow.py): 0 default,
-  // 2 nt, 16 sc1
-#define BF_LAUNCH(M, X) hipLaunchKernelGGL((bias_follow_kernel<M, X>), dim3(grid), dim3(256), 0, s, a)
-  if (mode == 0) {
-    if (g_bf_aux == 2) BF_LAUNCH(0, 2);
-    else if (g_bf_aux == 16) BF_LAUNCH(0, 16);
-    else BF_LAUNCH(0, 0);
-  } else {
-    if (g_bf_aux == 2) BF_LAUNCH(1, 2);
-    else if (g_bf_aux == 16) BF_LAUNCH(1, 16);
-    else BF_LAUNCH(1, 0);
-  }
-#undef BF_LAUNCH
-  return hipGetLastError();
-}
-void dg_bias_follow_set_variant(int aux, int sleep) {
-  g_bf_aux = aux;
-  g_bf_sleep = sleep < 1 ? 1 : sleep;
 }
 int dg_bias_chunks(int B) { return (B + BG_BT - 1) / BG_BT; }
 int dg_bias_chunks_multi(int B) { return (B + BG_BT_MULTI - 1) / BG_BT_MULTI; }

@@ -57,9 +57,10 @@ class ExperimentConfig:
     optimizer: str = "sgd"         # sgd | rmsprop (the reference's misnamed AdagradOptimizer)
     rmsprop_decay: float = 0.9
     bucket_mb: float = 6.0         # DP gradient bucket size (12x128: head + hidden layers | layer 0)
-    # DP all-reduce dtype: bf16 (the wire twin every gradient pass 2 writes; half the xGMI
-    # bytes; tests/test_train_gpu.py bounds its training curve against fp32) | fp32
-    grad_dtype: str = "bf16"
+    # DP all-reduce dtype: fp32 (the reference's DataParallelTable reduces fp32 gradients,
+    # experiments.lua:155-168) | bf16 (opt-in: the wire twin every gradient pass 2 writes; half
+    # the xGMI bytes; tests/test_wire_cpu.py and tests/test_train_gpu.py bound it against fp32)
+    grad_dtype: str = "fp32"
     # DP gradient collectives in the trainer: auto (the native in-graph RCCL communicator when
     # every rank's set-up and in-graph self-test pass, else torch — a collective decision,
     # parallel/dp.py make_communicator; what bench.py measures) | native | torch

@@ -8,6 +8,7 @@ HIP event, so a slot is never refilled while its DMA is in flight).
 """
 from __future__ import annotations
 
+import time
 from typing import Optional
 
 import numpy as np
@@ -53,10 +54,13 @@ class BatchLoader:
                                   sampling == "position", *pk, int(start_seq))
         self.consumed = int(start_seq)
         self._pending = []  # (slot, event) awaiting release
+        self.wait_s = 0.0   # host time spent blocked on the workers (next_host)
 
     def next_host(self):
         """Blocks until the next batch is ready; returns (slot, seq) — caller releases."""
+        t0 = time.perf_counter()
         slot, seq = self._impl.next()
+        self.wait_s += time.perf_counter() - t0
         if slot < 0:
             raise RuntimeError("loader stopped")
         self.consumed = seq + 1

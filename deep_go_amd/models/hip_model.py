@@ -169,9 +169,6 @@ class HipGoNet:
             splits = LY.pick_wgrad_splits(npix, KPw, Mpad_w, num_cus,
                                            self.h.conv_wgrad_wgs_per_cu_for(KPw),
                                            self.h.conv_wgrad_ktile(KPw))
-            if spec.index == 0 and os.environ.get("DG_L0_SPLITS"):
-                # (A/B knob: the first layer's split-K count; its slab reduce reads them all)
-                splits = max(1, min(int(os.environ["DG_L0_SPLITS"]), npix // 256))
             p = ConvPlan(spec.index, spec.k, spec.pad, spec.cin, cinp, spec.cout, bm, bn, KP,
                          Mpad, KPw, Mpad_w, splits, board=board)
             self.wf.append(torch.zeros((Mpad, KP), dtype=torch.bfloat16, device=dev))
@@ -342,11 +339,9 @@ class HipGoNet:
         # DG_CHECK_STREAMS=1: every cross-stream hand-off bracketed by timing events, verified
         # after each eager step (utils/streamcheck.py; check_streams())
         self.sc = streamcheck.StreamCheck() if streamcheck.enabled() else None
-        # the first layer's 5x5 weight gradient on the main stream before the window launch
-        # (DG_L0_WGRAD_MAIN=1) instead of on the side stream after the bias partials
-        self._l0_main = os.environ.get("DG_L0_WGRAD_MAIN", "0") == "1"
         self._head_red_defer = False
         self._head_red_pending = False
+        self._win_first = os.environ.get("DG_WIN_FIRST", "0") == "1"
         self._refresh_table = self._build_refresh_table()
         self._step_refresh = None   # the per-step table (plain copies no launch reads dropped)
         self.launches = 0     # native launches issued through _run (SegmentedStep counts them)
@@ -791,8 +786,6 @@ class HipGoNet:
         self._l0_side_at = None    # group top whose backward also runs layer 0's chain
         self._pre_dgrads = {}      # layer -> its dgrad ops moved into _bwd_pre
         self._l0_dgrad = []        # layer 1's dgrad (-> dZ_0) when it runs on the side stream
-        self._bf_follow = None     # bias-gradient follower (see _setup_bias_follow)
-        self._bf_finish = None
         if os.environ.get("DG_DSTACK", "1") == "0":
             self._dgrads_first()
             return
@@ -870,81 +863,6 @@ class HipGoNet:
                     self._bwd[i] = self._bwd[i][:3]
             self._dgrad_first = True
         self._group_wgrads(set([run[0]] + [i - 1 for i in run]))
-        self._setup_bias_follow(run)
-
-    def _setup_bias_follow(self, run):
-        """The bias-gradient partials of the dgrad stack's layers BESIDE the stack (elementwise.hip
-        bias_follow_kernel): the stack stores each row's dZ frame write-through and counts it per
-        board; a follower launch on the side stream, co-resident with the stack (<= 32 VGPRs,
-        13 KB LDS), computes a layer's partials as soon as all boards have stored it, instead of
-        an HBM-bound launch beside the window weight gradient after the stack (where it
-        stretched 65 -> 200 us and delayed the first layer's 5x5 weight gradient past the window
-        kernel: VERDICT r4 item 1).  A finish launch after the stack (where the multi-layer
-        partials launch was) computes whatever the follower did not reach — the same task
-        routine, so the bits never depend on who ran a task — and resets the counters.
-        bf16 128-channel stack with one grouped weight-gradient launch (12x128) only.
-        DG_BIAS_FOLLOW=0: the previous partials launch; =finish: no follower (the finish launch
-        computes every task; tests compare it bit for bit with the follower)."""
-        self._bf_follow = None
-        self._bf_finish = None
-        mode = os.environ.get("DG_BIAS_FOLLOW", "0")
-        h = self.h
-        if (mode == "0" or self.dstack_fp8 or self.side_mode != "bias" or len(self.wgroups) != 1
-                or not hasattr(h, "bias_follow")):
-            return
-        g = self.wgroups[0]
-        op = self._bwd[g[0]][0]
-        if op[0] is not h.bias_grad_partial_multi or op[1][3] != 128 or op[1][4] != 1:
-            return
-        bt = next((t for t in self._wgroup_tables if t.ctypes.data == op[1][0]), None)
-        if bt is None or (bt[:, 2] != 0).any():
-            return
-        rows = [[int(r[0]), int(r[1])] for r in bt]
-        l0 = self._bwd[0][0]
-        l0_sep = (l0[0] is h.bias_grad_partial_multi and l0[1][3] == 128 and l0[1][4] == 1
-                  and getattr(self, "_l0_btab", None) is not None
-                  and l0[1][0] == self._l0_btab.ctypes.data)
-        if l0_sep:
-            rows.append([int(self._l0_btab[0, 0]), int(self._l0_btab[0, 1])])
-        ready = {self.dz[run[0]].data_ptr(): -1}
-        for r, i in enumerate(run):
-            ready[self.dz[i - 1].data_ptr()] = r
-        if any(dz not in ready for dz, _ in rows) or len(rows) > 16:
-            return
-        rows.sort(key=lambda r: ready[r[0]])
-        self._bf_table = np.ascontiguousarray(np.array([[dz, part, ready[dz]] for dz, part in rows],
-                                                       dtype=np.int64))
-        nl, C = len(rows), 128
-        self._bf_sig = torch.zeros(len(run), dtype=torch.int32, device=self.device)
-        ntask = int(h.bias_follow_tasks(nl, self.B, C))
-        self._bf_done = torch.zeros(ntask, dtype=torch.int32, device=self.device)
-        base = (self._bf_table.ctypes.data, nl, self.B, C, self._bf_sig.data_ptr(), len(run),
-                self._bf_done.data_ptr())
-        self._bf_finish = (h.bias_follow, base + (1, ntask, 0.0, self._sf))
-        self._bwd[g[0]][0] = self._bf_finish
-        if l0_sep:
-            self._bwd[0][0] = (self._noop, ())
-        if mode == "finish":
-            return
-        # per-wait bound of the follow pass: a stack row takes ~24 us at 12x128; a follower that
-        # does not see one within this (the stack not beside it) leaves the rest to the finish
-        self._bf_follow = (h.bias_follow, base + (0, self.num_cus, 200.0, self._sf))
-        self._bwd_pre = [(h.conv_stack2_dgrad_sig, (a[1], a[2], a[3], a[5], self._bf_sig.data_ptr()))
-                         if (f is h.conv_stack2 and a[0] == h.EPI_DGRAD) else (f, a)
-                         for f, a in self._bwd_pre]
-
-    def start_bias_follow(self):
-        """Launch the bias-gradient follower on the side stream (after the forward: the head's
-        dZ is its first layer), beside the backward-data stack the main stream runs next."""
-        if self._bf_follow is None:
-            return
-        main = torch.cuda.current_stream()
-        if self.sc:
-            self.sc.produce("fwd->follower", main)
-        self.side.wait_stream(main)
-        if self.sc:
-            self.sc.consume("fwd->follower", self.side)
-        self._run([self._bf_follow], self.side.cuda_stream)
 
     def _dgrads_first(self):
         """No board-resident dgrad stack for this shape (e.g. 256 channels): still run the
@@ -1287,7 +1205,6 @@ class HipGoNet:
         self._run(self._fwd_train, s)
         self._run([self._head_train], s)
         self.head_reduce()
-        self.start_bias_follow()
         self._run(self._bwd_pre, s)
         hooks = dict()
         for li, fn in self.grad_hooks:
@@ -1339,14 +1256,35 @@ class HipGoNet:
                 if sc:
                     sc.consume("l0-chain->main", main)
             else:
+                # the weight-gradient launch issued BEFORE the side stream's work when the step
+                # is captured (DG_WIN_FIRST): the graph executor keeps a node's first-created
+                # child on the parent's hardware queue, so the window kernel follows the
+                # backward-data stack on the same queue instead of behind a cross-queue wait
+                win_first = self._win_first and ops[1][0] is not HipGoNet._noop
                 if sc:
                     sc.produce("dz->side", main)
-                side.wait_stream(main)           # dZ of the layer (group) final
+                if win_first:
+                    fork = main.record_event()   # dZ of the layer (group) final
+                    self._run(ops[1:2], main.cuda_stream)
+                    side.wait_event(fork)
+                else:
+                    side.wait_stream(main)       # dZ of the layer (group) final
                 if sc:
                     sc.consume("dz->side", side)
                 self._flush_head_reduce(side.cuda_stream)
                 self._issue_loss_gate(side.cuda_stream)
                 self._run(ops[:1], side.cuda_stream)
+                l0 = self._l0_dgrad + self._layer_ops(0)[:3] if l0_side else None
+                if l0_side and self._defer:
+                    # layer 0's bias partial (where it is a launch of its own: d = 256) and
+                    # what produces its dZ_0 BEFORE the event the early update waits on: the
+                    # partial's |dZ_0| check is a step-tag producer, and the early update must
+                    # read the tag only after every producer (all-or-nothing).  The
+                    # 5x5 slab reduce after it cannot trip on its own: |dZ_0| < 2^100 and
+                    # x0 in {0, 1} bound the 5x5 gradient below the reduce's 2^120
+                    k = len(self._l0_dgrad) + 1
+                    self._run(l0[:k], side.cuda_stream)
+                    l0 = l0[k:]
                 ev = side.record_event()         # partials ready for the reduce
                 if sc:
                     sc.produce("partials->reduce", side)
@@ -1358,25 +1296,10 @@ class HipGoNet:
                 # gradient then starts ~50 us earlier beside it) stretched the fp8 window
                 # kernel by 100 us: -6% at 12x256 fp8, 0 elsewhere
                 # (profiles/r4_s1_l0_bias_main_ab.txt)
-                if l0_side and self._l0_main and not self._l0_dgrad:
-                    # the first layer's 5x5 weight gradient ALONE on the main stream, right
-                    # before the window launch (beside the window kernel it cannot co-reside
-                    # with its two workgroups per CU and ran stretched after it); its bias
-                    # partial (a launch of its own at d = 256) and slab reduce stay on the side
-                    # stream, the reduce after the partials
-                    l0 = self._layer_ops(0)[:3]
-                    self._run(l0[:1], side.cuda_stream)
-                    self._run(l0[1:2], main.cuda_stream)
-                    ev5 = main.record_event()
-                    if sc:
-                        sc.produce("l0-wgrad->reduce", main)
-                    side.wait_event(ev5)
-                    if sc:
-                        sc.consume("l0-wgrad->reduce", side)
-                    self._run(l0[2:3], side.cuda_stream)
-                elif l0_side:
-                    self._run(self._l0_dgrad + self._layer_ops(0)[:3], side.cuda_stream)
-                self._run(ops[1:2], main.cuda_stream)
+                if l0_side:
+                    self._run(l0, side.cuda_stream)
+                if not win_first:
+                    self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
                 if sc:
                     sc.consume("partials->reduce", main)
@@ -1734,7 +1657,6 @@ class SegmentedStep:
         emit(lambda: net._run(net._fwd_train, stream_handle()))
         emit(lambda: net._run([net._head_train], stream_handle()))
         emit(net.head_reduce)
-        emit(net.start_bias_follow)
         emit(lambda: net._run(net._bwd_pre, stream_handle()))
         if net.L - 1 in fire_after:
             emit(net.join_side)               # the head's gradients final (deferred reduce)

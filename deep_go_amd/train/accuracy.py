@@ -43,13 +43,21 @@ def _score(net, ds, B: int) -> Dict[str, float]:
 
 
 def fixture_accuracy(device, layers: int = 12, channels: int = 128, dtype: str = "bf16",
-                     steps: int = 1000, batch: int = 64, rate: float = 0.1,
+                     steps: int = 3000, batch: int = 64, rate: float = 0.05,
                      rate_decay: float = 1e-7, head_relu: Optional[bool] = None,
                      seed: int = 11, root: str = FIXTURE) -> Optional[Dict]:
     """Train ``steps`` SGD steps (one-graph training step, batch ``batch``) on the fixture's
     training games from a random init, then score the validation and test games.  Returns
     None when the packed fixture is absent.  head_relu: None = the reference's setting
-    (ReLU on the head, experiments.lua:135-151)."""
+    (ReLU on the head, experiments.lua:135-151).
+
+    Defaults (tools/acc_sweep.py, profiles/r6_accuracy_sweep.txt): with the head ReLU the
+    12x128 network sits on a plateau near ln 361 for the first ~1000 steps at rates <= 0.05
+    (at 0.1 it leaves it sooner but over-fits the 20 games: validation NLL 5.7 by step 3000);
+    3000 steps at rate 0.05 take the training loss from 5.89 to ~1.5 nats (train top-1 ~58%)
+    with validation / test top-1 ~13% on the two held-out games.  The reference's own rate
+    .512 (default-experiment.lua) kills every logit through the head ReLU (loss pinned at
+    ln 361 = 5.889)."""
     from ..config import get_preset
     from ..data.batch import pack_batch
     from ..data.dataset import PackedDataset, sample_reference
@@ -95,5 +103,60 @@ def fixture_accuracy(device, layers: int = 12, channels: int = 128, dtype: str =
         out[f"{split}_positions"] = r["positions"]
     r = _score(net, tr, batch)
     out["train_top1"] = round(r["top1"], 4)
+    out["seconds"] = round(time.perf_counter() - t0, 1)
+    return out
+
+
+def oracle_parity(device, layers: int = 6, channels: int = 64, batch: int = 64,
+                  rate: float = 0.05, steps: int = 500, head_relu: bool = True, seed: int = 5,
+                  threads: int = 16, root: str = FIXTURE) -> Optional[Dict]:
+    """The accuracy half through the HIP trainer vs the fp32 PyTorch oracle: HIPBackend (bf16
+    operands, fp32 master weights, one-graph step) and CPUBackend from the SAME init on the
+    SAME game-uniform batch stream of the fixture's training games, ``steps`` SGD steps, then
+    both scored on every position of the held-out validation and test games and on the
+    training positions (top-1 = argmax == label, NLL = mean -log p).  Default shape: the
+    reference's default-experiment.lua (6 layers, d = 64, batch 64) with its head ReLU
+    (experiments.lua:133-153), at a rate where it learns (tools/acc_sweep.py).  Returns both
+    runs' losses and scores (None without the packed fixture)."""
+    from ..config import ExperimentConfig
+    from ..data.dataset import PackedDataset, sample_reference
+    from .backends import CPUBackend, HIPBackend
+    paths = {s: os.path.join(root, f"{s}.dgpack.npz") for s in ("train", "validation", "test")}
+    if not all(os.path.exists(p) for p in paths.values()):
+        return None
+    ds = {s: PackedDataset.load(p) for s, p in paths.items()}
+    torch.set_num_threads(threads)
+    cfg = ExperimentConfig(numLayers=layers, channelSize=channels, batchSize=batch, rate=rate,
+                           rateDecay=1e-7, head_relu=head_relu, seed=seed, useCuda=True)
+    cpu_be = CPUBackend(cfg, batch)
+    gpu_be = HIPBackend(cfg, batch, flat=cpu_be.flat_params().clone(), device=device)
+    rng = np.random.default_rng(seed)
+    tr = ds["train"]
+    t0 = time.perf_counter()
+    losses = {"cpu": [], "hip": []}
+    for _ in range(steps):
+        g, mv = sample_reference(list(tr.game_count), batch, rng)
+        i = tr.game_start[g] + mv - 1
+        b = (tr.planes[i], tr.player[i], tr.rank[i], tr.label[i])
+        for name, be in (("cpu", cpu_be), ("hip", gpu_be)):
+            be.set_batch(*b)
+            be.train_step()
+            losses[name].append(be.loss_sum() / batch)
+
+    def score(be, d):
+        n = len(d)
+        correct, nll = 0, 0.0
+        for lo in range(0, n, batch):
+            idx = np.arange(lo, lo + batch) % n
+            be.set_batch(d.planes[idx], d.player[idx], d.rank[idx], d.label[idx])
+            k = min(n, lo + batch) - lo
+            be.evaluate(k)
+            correct += be.correct()
+            nll += be.loss_sum()
+        return {"correct": int(correct), "top1": correct / n, "nll": nll / n, "positions": n}
+    out = {"model": f"{layers}x{channels}", "batch": batch, "rate": rate, "steps": steps,
+           "head_relu": head_relu, "loss_cpu": losses["cpu"], "loss_hip": losses["hip"]}
+    for split in ("validation", "test", "train"):
+        out[split] = {"cpu": score(cpu_be, ds[split]), "hip": score(gpu_be, ds[split])}
     out["seconds"] = round(time.perf_counter() - t0, 1)
     return out

@@ -136,6 +136,10 @@ class CPUBackend:
         """Updates skipped for a non-finite loss / gradient so far."""
         return self.nan_skipped
 
+    def gradient_tagged(self) -> bool:
+        """(HIP only: the gradient producers' range-check tag; the fp32 oracle has none)"""
+        return False
+
     def flat_params(self) -> torch.Tensor:
         return self.params.detach()
 
@@ -245,6 +249,16 @@ class HIPBackend:
     def bad_steps(self) -> int:
         """Updates the device gate / fused update skipped so far (syncs)."""
         return int(self.net.bad_steps.item())
+
+    def gradient_tagged(self) -> bool:
+        """Whether a gradient producer tagged the step in flight (before its update: a value
+        out of range — dg_common.h grad_out_of_range; the update would skip it).  Syncs.
+        Single-GPU only: under DP the tag is rank-local and the all-reduced gradient's finite
+        gate decides, the same on every rank."""
+        if self.world > 1:
+            return False
+        step, tag = self.net._stepflag.tolist()
+        return tag == step + 1
 
     def flat_params(self) -> torch.Tensor:
         return self.net.params.detach().cpu()

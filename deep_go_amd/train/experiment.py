@@ -232,6 +232,11 @@ class Experiment:
                     loss = be.loss_sum() / self.local_batch
                     if inj == "nan":
                         loss = float("nan")
+                    if cfg.nan_policy == "raise" and be.gradient_tagged():
+                        # a gradient producer's range check fired (finite loss, |dZ| or a
+                        # gradient out of range): raise like a non-finite loss, with the dump,
+                        # instead of letting the update skip the step silently
+                        loss = float("nan")
                     if batch is None and not np.isfinite(loss):
                         batch = be.current_batch()  # only for the bad-batch dump
                     if not check_finite(loss, step, cfg.nan_policy, batch, cfg.checkpoint_dir):

@@ -12,10 +12,17 @@ each hand-off with two timing events that are recorded SEPARATELY from the wait 
   * ``consume(name, stream)`` — on the consumer stream, right before the first launch that
     reads it.
 
-A missing or misplaced wait lets the consumer's event complete while the producer still runs;
 ``check()`` (after an eager step: events inside a hipGraph capture are skipped) synchronizes
 and asserts, for every pair, that the producer's event completed no later than the consumer's
-(``elapsed_time(produce, consume) >= 0``).  The reference has no concurrency at all
+(``elapsed_time(produce, consume) >= 0``).
+
+What this verifies, and what it does not: the brackets sit at the hand-offs the code DECLARES
+(each wait_stream / wait_event has its produce / consume pair), so the check confirms that
+each declared wait is placed after the producer's launches and before the consumer's, and
+that HIP honours it.  A hand-off that has no wait at all also has no bracket and is not seen
+here — that class of bug is covered by the bit-exact comparisons of the same step run
+serialized (``AMD_SERIALIZE_KERNEL=3``) and unserialized (tests/test_model_gpu.py
+test_stream_handoffs_checked_and_serialized_run_bit_identical) instead.  The reference has no concurrency at all
 (``/root/reference/data.lua:82-96``: every mutation runs on the main Lua thread), so these
 orderings are the new build's own risk.
 """

@@ -240,13 +240,11 @@ def test_conv_l1(B, cin, cout, k):
     assert torch.equal(bits.reshape(B, 361, cout).bool(), nz)
 
 
-@pytest.mark.parametrize("half", [0, 1])
 @pytest.mark.parametrize("B,cin,cout", [(3, 37, 128), (2, 40, 256), (5, 37, 384), (1, 16, 128)])
-def test_conv_l1_frag(B, cin, cout, half):
-    """First layer on conv_l1_frag (conv_l1.hip: one board per workgroup — or two half-board
-    ones, conv_l1_frag_set_half — the input frame in conflict-free planes, fragment-ordered
-    weights, 1-3 128-channel passes) vs the fp32 reference with the same bf16-rounded bias
-    table, and its ReLU bitmask."""
+def test_conv_l1_frag(B, cin, cout):
+    """First layer on conv_l1_frag (conv_l1.hip: one board per workgroup, the input frame in
+    conflict-free planes, fragment-ordered weights, 1-3 128-channel passes) vs the fp32
+    reference with the same bf16-rounded bias table, and its ReLU bitmask."""
     torch.manual_seed(9)
     from deep_go_amd.ops import functional as Fn
     from deep_go_amd.ops.native import hip
@@ -254,12 +252,8 @@ def test_conv_l1_frag(B, cin, cout, half):
     w = bf(torch.randn(cout, 5, 5, cin, device=DEV) * 0.1)
     b = torch.randn(cout, device=DEV) * 0.1
     pb = torch.randn(361, cout, device=DEV) * 0.1
-    hip().conv_l1_frag_set_half(half)
-    try:
-        y, mask = Fn.conv_l1_frag(x, w, b, pb)
-        torch.cuda.synchronize()
-    finally:
-        hip().conv_l1_frag_set_half(1 if os.environ.get("DG_L1_HALF") == "1" else 0)
+    y, mask = Fn.conv_l1_frag(x, w, b, pb)
+    torch.cuda.synchronize()
     tab = (pb + b[None, :]).to(torch.bfloat16).float()
     ref = torch.relu(conv_ref(x, w, 5) + tab.t().reshape(1, cout, 19, 19))
     assert rel_err(y, ref) < 1e-2

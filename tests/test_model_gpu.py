@@ -650,9 +650,10 @@ def test_fused_update_matches_separate_launches(layers, ch, dtype, opt, monkeypa
     check()
 
 
-@pytest.mark.parametrize("early,where", [(True, "hidden"), (False, "hidden"), (True, "layer0"),
-                                         (False, "head")])
-def test_fused_update_all_or_nothing_on_producer_tag(early, where):
+@pytest.mark.parametrize("early,where,C", [(True, "hidden", 128), (False, "hidden", 128),
+                                           (True, "layer0", 128), (False, "head", 128),
+                                           (True, "layer0", 256)])
+def test_fused_update_all_or_nothing_on_producer_tag(early, where, C):
     """nan_policy guard / skip with the gradient pass 2 deferred into the fused update
     (ADVICE r4): the gradient does not exist before the update, so its PRODUCERS check what
     they write — the window weight-gradient slabs, the bias partials (every dZ value they read,
@@ -663,8 +664,10 @@ def test_fused_update_all_or_nothing_on_producer_tag(early, where):
     + bias partials tag); layer0: a huge finite dZ_0 (the bias bound tags before the early
     update launch, so the hidden layers it updates do not move either); head: a NaN in the
     head's dZ partials.  early: the grouped layers' update runs before the first layer's
-    chain ends."""
-    cfg, net, _ = _setup(4, 128, 4, seed=1)
+    chain ends.  C = 256: the first layer's bias partial is a launch of its own on the side
+    stream (not a row of the grouped launch), issued before the event the early update waits
+    on."""
+    cfg, net, _ = _setup(4, C, 4, seed=1)
     net._early_ok, net._early_env = early, ("1" if early else "0")
     net.forward_backward()
     torch.cuda.synchronize()
@@ -680,7 +683,6 @@ def test_fused_update_all_or_nothing_on_producer_tag(early, where):
         if where == "head":
             net.head_dzb.view(-1)[5] = float("nan")
         net.head_reduce()
-        net.start_bias_follow()
         net._run(net._bwd_pre, s)
         if where == "hidden":
             net.dz[net.wgroups[0][0]].view(-1)[3000] = float("nan")
@@ -1101,68 +1103,3 @@ def test_stream_handoffs_checked_and_serialized_run_bit_identical(args, tmp_path
     for name in ("check", "serial"):
         assert torch.equal(outs[name]["params"], outs["plain"]["params"]), name
         assert torch.equal(outs[name]["loss"], outs["plain"]["loss"]), name
-
-
-def test_bias_follow_beside_dgrad_stack_bit_identical(monkeypatch):
-    """The bias-gradient follower (elementwise.hip bias_follow_kernel, co-resident with the
-    backward-data stack) at the headline shape (12x128, B = 256):
-    (a) it really runs beside the stack — after the stack launch, most of the 11 layers'
-        partial tasks are already done by the follower (the stack signals each row through
-        write-through stores + arrival counters, the follower reads under an agent acquire);
-    (b) its gradients are BIT-IDENTICAL to the finish-pass-only run (DG_BIAS_FOLLOW=finish:
-        the same task routine, no follower) over several steps: a stale or torn read of a dZ
-        frame would change the bits;
-    (c) they match the previous multi-layer partials launch (DG_BIAS_FOLLOW=0: another
-        summation order) within fp32 rounding, and the weight gradients exactly."""
-    from deep_go_amd.config import ExperimentConfig
-    from deep_go_amd.data.synthetic import random_planes
-    from deep_go_amd.models.hip_model import HipGoNet
-    cfg = ExperimentConfig(numLayers=12, channelSize=128, batchSize=256, seed=7)
-    batches = [[torch.from_numpy(a).cuda() for a in random_planes(256, seed=70 + k)]
-               for k in range(3)]
-    grads, follow_done = {}, None
-    for mode in ("1", "finish", "0"):
-        monkeypatch.setenv("DG_BIAS_FOLLOW", mode)
-        net = HipGoNet(cfg, 256, device="cuda")
-        assert (net._bf_finish is not None) == (mode != "0")
-        assert (net._bf_follow is not None) == (mode == "1")
-        out = []
-        for k, bt in enumerate(batches):
-            net.set_batch(*bt)
-            if mode == "1" and k == 1:
-                # the forward + the stack beside the follower, then count the done tasks
-                s = torch.cuda.current_stream().cuda_stream
-                net._run(net._pre_train, s)
-                net._run(net._fwd_train, s)
-                net._run([net._head_train], s)
-                net.head_reduce()
-                net.start_bias_follow()
-                net._run(net._bwd_pre, s)
-                net.join_side()
-                torch.cuda.synchronize()
-                follow_done = int((net._bf_done != 0).sum().item()), net._bf_done.numel()
-                for i in range(net.L - 2, -1, -1):
-                    net.backward_layer(i)
-                net.join_side()
-            else:
-                net.forward_backward()
-            torch.cuda.synchronize()
-            out.append(net.grads.clone())
-            net.optimizer_step()
-        grads[mode] = out
-        del net
-    done, total = follow_done
-    # (how much the follower finishes beside the stack depends on the box's timing: 50-90%
-    # of the tasks on most boxes, 9% seen on one; it must have run concurrently at all —
-    # the rest is the finish pass's, and the gradients below must not depend on the split)
-    print("follower tasks done beside the stack", done, "of", total)
-    assert done > 0, (done, total)
-    from deep_go_amd.models.gocnn import ParamLayout
-    lay = ParamLayout(cfg)
-    for k in range(len(batches)):
-        assert torch.equal(grads["1"][k], grads["finish"][k]), k
-        a, b = grads["1"][k], grads["0"][k]
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-9), (a - b).abs().max().item()
-    a, b = grads["1"][0], grads["0"][0]
-    for L in lay.layers:   # step 1 (same weights): the weight gradients do not see the bias pass
-        assert torch.equal(a[L.w_off:L.w_off + L.w_numel], b[L.w_off:L.w_off + L.w_numel])
