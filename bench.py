@@ -453,13 +453,14 @@ class _Case:
                                   wgrad_group=wg,
                                   grad_wire=self.grad_dtype if use_dp else "fp32")
         host = data == "fixture" or not args.device_pool
-        # input prefetch (the next batch's copy on a load stream beside the previous step):
-        # on for host sources (SDMA copies), off for the device pool (its blit-kernel copy
-        # beside the step measured -1%; profiles/r2_input_prefetch_ab.txt)
+        # input prefetch (the next batch's H2D copy on a load stream beside the previous step,
+        # SDMA): on for host sources; off for the device pool (its blit-kernel copy beside the
+        # step measured -1%, profiles/r2_input_prefetch_ab.txt).  The host pool + prefetch
+        # costs 1.2-1.5% against the device pool (the step graph waits on the copy's event:
+        # ~8 us more at the step boundary than the in-stream blit,
+        # profiles/r6_host_pool_prefetch.txt).  DG_PREFETCH=0 / 1 forces
         pf = os.environ.get("DG_PREFETCH", "auto")
         self.prefetch = (pf == "1" or (pf != "0" and host)) and net.enable_prefetch()
-        self.input = ("host pinned, prefetched H2D" if host and self.prefetch else
-                      "host pinned, H2D in the step" if host else "device-resident pool")
         if world > 1:
             comm.broadcast_(net.params, 0)
             net.refresh_weights()
@@ -486,6 +487,8 @@ class _Case:
                                             comm=comm, shadow=net.grads16)
         self.load(0)
         self.step = SegmentedStep(net, self.bucketer, use_graphs=not args.no_graph)
+        self.input = ("host pinned, H2D prefetched on a load stream" if host and self.prefetch
+                      else "host pinned, H2D in the step" if host else "device-resident pool")
 
     def load(self, i):
         if self.loader is not None:

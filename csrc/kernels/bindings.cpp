@@ -130,7 +130,6 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
                                 hipStream_t s);
 int dg_bias_chunks(int B);
 int dg_bias_chunks_multi(int B);
-void dg_bias_set_units(int on);
 hipError_t dg_sgd(float* p, const float* g, size_t n, const double* lr, float gscale,
                   const float* gate, const void* g16, hipStream_t s);
 hipError_t dg_rmsprop(float* p, const float* g, float* ms, size_t n, const double* lr,
@@ -445,8 +444,6 @@ PYBIND11_MODULE(_dghip, m) {
   });
   m.def("bias_chunks", [](int B) { return dg_bias_chunks(B); });
   m.def("bias_chunks_multi", [](int B) { return dg_bias_chunks_multi(B); });
-  m.def("bias_set_units", [](int on) { dg_bias_set_units(on); },
-        "multi-layer bias partials: 1 the unit kernel, 0 the per-item kernel (default)");
   m.def("sgd", [](uintptr_t p, uintptr_t g, size_t n, uintptr_t lr, float gscale,
                   uintptr_t gate, uintptr_t stream) {
     check(dg_sgd(P<float>(p), P<float>(g), n, P<double>(lr), gscale, P<float>(gate), nullptr,

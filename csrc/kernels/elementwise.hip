@@ -166,116 +166,6 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
 }
 
 // ------------------------------------------------------------------------------------
-// Pass 1 of the multi-layer launch (dg_bias_grad_partial_multi), latency-shaped.  It runs on
-// the side stream beside the window weight gradient, whose two workgroups per CU leave one
-// 64-VGPR wave per SIMD: one 256-thread workgroup per CU.  The kernel above (2 x 16-B loads in
-// flight per lane, one item of all 64 boards per lane, a second pass on 48 of 256 lanes) then
-// ran latency-bound: 289 MB of dZ frames in 216 us beside the window kernel vs 54 us alone
-// (12x128), the step's critical side chain.  Here a unit is (item, sub-chunk of BP_SUB boards):
-// 8 loads in flight per lane (buffer loads: one VGPR offset, the board stride in soffset),
-// items x 4 units spread over all 256 lanes.  A pass covers 256 consecutive units (sub-chunk
-// major, items >= 256: an item occurs at most once per pass); each unit's 16-board sum is
-// stored (sub-chunk 0) or added into the item's LDS row sum with a barrier per pass, so every
-// element is ((s0 + s1) + s2) + s3 of sequential 16-board sums — deterministic, the output
-// layout of bias_grad_partial_kernel.
-typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-constexpr int BP_SUB = 16;   // boards per unit
-constexpr int BP_NT = 256;
-template <bool F8>
-__global__ void __launch_bounds__(BP_NT, 8)
-bias_partial_units_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks) {
-  extern __shared__ __attribute__((aligned(16))) float s_row[];  // [19][C]
-  constexpr int LD = 8;
-  const int h = blockIdx.x, chunk = blockIdx.y, z = blockIdx.z;
-  const int tid = threadIdx.x;
-  const int G = C / 8;
-  const int items = BOARD * G;
-  const int units = items * (BG_BT_MULTI / BP_SUB);
-  const int F = BOARD + 2 * pad;
-  const int esz = F8 ? 1 : 2;
-  const int bstride = (F8 ? BG_FP8_ROWS : F * F) * C * esz;   // B * bstride < 2^31: host
-  const float s8 = F8 ? *Ls.s8[z] : 1.f;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)Ls.dZ[z], 0, B * bstride, 0x00020000);
-  const int row0 = ((h + pad) * F + pad) * C * esz + chunk * BG_BT_MULTI * bstride;
-  float dzmax = 0.f;
-  bool nonfinite = false;
-#pragma unroll 1
-  for (int u0 = 0; u0 < units; u0 += BP_NT) {
-    const int u = u0 + tid;
-    if (u < units) {
-      const int sub = u / items, it = u - sub * items;
-      const int w = it / G, g = it - w * G;
-      const int voff = row0 + sub * BP_SUB * bstride + (w * C + g * 8) * esz;
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      // (rolled: unrolled, the compiler hoists the next group's loads over the sums and spills)
-#pragma unroll 1
-      for (int jb = 0; jb < BP_SUB; jb += LD) {
-        if constexpr (F8) {
-          u32x2v v[LD];
-#pragma unroll
-          for (int j = 0; j < LD; ++j)
-            v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (jb + j) * bstride, 0);
-#pragma unroll
-          for (int j = 0; j < LD; ++j) {
-            const int u2[2] = {(int)v[j].x, (int)v[j].y};
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const auto lo = __builtin_amdgcn_cvt_pk_f32_bf8(u2[e], false);
-              const auto hi = __builtin_amdgcn_cvt_pk_f32_bf8(u2[e], true);
-              acc[4 * e] += lo[0] * s8;
-              acc[4 * e + 1] += lo[1] * s8;
-              acc[4 * e + 2] += hi[0] * s8;
-              acc[4 * e + 3] += hi[1] * s8;
-              dzmax = fmaxf(dzmax, fmaxf(fmaxf(fabsf(lo[0]), fabsf(lo[1])),
-                                         fmaxf(fabsf(hi[0]), fabsf(hi[1]))) * s8);
-            }
-          }
-        } else {
-          u32x4v v[LD];
-#pragma unroll
-          for (int j = 0; j < LD; ++j)
-            v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (jb + j) * bstride, 0);
-#pragma unroll
-          for (int j = 0; j < LD; ++j) {
-            const uint32_t q[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x0 = __uint_as_float(q[e] << 16), x1 = __uint_as_float(q[e] & 0xFFFF0000u);
-              acc[2 * e] += x0;
-              acc[2 * e + 1] += x1;
-              dzmax = fmaxf(dzmax, fmaxf(fabsf(x0), fabsf(x1)));
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) nonfinite |= !__builtin_isfinite(acc[e]);
-      f32x4* sr = (f32x4*)(s_row + w * C + g * 8);
-      if (sub == 0) {
-        sr[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
-        sr[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
-      } else {
-        sr[0] += f32x4{acc[0], acc[1], acc[2], acc[3]};
-        sr[1] += f32x4{acc[4], acc[5], acc[6], acc[7]};
-      }
-    }
-    __syncthreads();
-  }
-  if (Ls.sf && (nonfinite || !(dzmax < DZ_BOUND))) flag_bad_step(Ls.sf);
-  float* part = Ls.part[z];
-  f32x4* prow = (f32x4*)(part + ((size_t)chunk * NPTS + h * BOARD) * C);
-  for (int i = tid; i < BOARD * C / 4; i += BP_NT) prow[i] = ((const f32x4*)s_row)[i];
-  float* rowpart = part + (size_t)nchunks * NPTS * C + ((size_t)chunk * BOARD + h) * C;
-  for (int c = tid; c < C; c += BP_NT) {
-    float sc = 0.f;
-    for (int w = 0; w < BOARD; ++w) sc += s_row[w * C + c];
-    rowpart[c] = sc;
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // gradient element i as fp32: the flat fp32 gradient, or its bf16 twin (the data-parallel
 // bf16 wire format: the all-reduced bucket is read as it came off the wire)
 DG_DEV float grad_at(const float* g, size_t i) { return g[i]; }
@@ -1140,17 +1030,6 @@ hipError_t dg_bias_grad_partial(const void* dZ, int B, int C, int pad, float* pa
   return hipGetLastError();
 }
 
-// the multi-layer launch's kernel: 1 = bias_partial_units_kernel where it applies
-// (DG_BIAS_UNITS=1; dg_bias_set_units), 0 = bias_grad_partial_kernel<2> (default: the units
-// kernel halves the partials beside the window kernel, but the first layer's 5x5 weight
-// gradient then starts beside it and stretches the step's critical chain — no gain at 12x128 /
-// 12x256 bf16, -7% at 12x256 fp8, profiles/r5_bias_units.txt)
-int g_bias_units = [] {
-  const char* e = getenv("DG_BIAS_UNITS");
-  return e && *e == '1' ? 1 : 0;
-}();
-void dg_bias_set_units(int on) { g_bias_units = on ? 1 : 0; }
-
 // Pass 1 for nl same-shape layers in one launch: table = nl rows of {dZ frame, part, s8}
 // (s8: 0 = bf16 frame, else the e5m2 copy's scale pointer; pad must be 1 then);
 // chunks of BG_BT_MULTI boards (dg_bias_chunks_multi).
@@ -1169,23 +1048,6 @@ hipError_t dg_bias_grad_partial_multi(const long long* table, int nl, int B, int
     if (Ls.s8[i] && pad != 1) return hipErrorInvalidValue;
   }
   Ls.sf = sf;
-  // the unit kernel: every layer of one frame type, B a whole number of sub-chunks (buffer
-  // range checks see only the VGPR offset), >= 256 items per row, 32-bit offsets
-  bool units = g_bias_units && B % BP_SUB == 0 && BOARD * (C / 8) >= BP_NT;
-  const bool f8 = Ls.s8[0] != nullptr;
-  for (int i = 0; i < nl; ++i) units = units && (Ls.s8[i] != nullptr) == f8;
-  const long long bstride = (long long)(f8 ? BG_FP8_ROWS : (BOARD + 2 * pad) * (BOARD + 2 * pad)) *
-                            C * (f8 ? 1 : 2);
-  units = units && (long long)B * bstride < (1ll << 31);
-  if (units) {
-    if (f8)
-      hipLaunchKernelGGL(bias_partial_units_kernel<true>, dim3(BOARD, nchunks, nl), dim3(BP_NT),
-                         (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
-    else
-      hipLaunchKernelGGL(bias_partial_units_kernel<false>, dim3(BOARD, nchunks, nl), dim3(BP_NT),
-                         (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(bias_grad_partial_kernel<2>, dim3(BOARD, nchunks, nl), dim3(threads),
                      (size_t)BOARD * C * sizeof(float), s, Ls, B, C, pad, nchunks, BG_BT_MULTI);
   return hipGetLastError();

@@ -290,11 +290,16 @@ __global__ void __launch_bounds__(HT) head_kernel(HeadArgs a) {
           for (int o = gcc; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
           v[t][e] = x;
         }
-      if (lane < gcc) {
+      // the 8 waves' sums added in wave order (an LDS atomicAdd made the head's weight
+      // gradient depend on wave arrival order: runs were not bit-reproducible)
+      for (int w8 = 0; w8 < HT / 64; ++w8) {
+        if (wave == w8 && lane < gcc) {
 #pragma unroll
-        for (int t = 0; t < T; ++t)
+          for (int t = 0; t < T; ++t)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) atomicAdd(s_gw + t * CCH + g * 8 + e, v[t][e]);
+            for (int e = 0; e < 8; ++e) s_gw[t * CCH + g * 8 + e] += v[t][e];
+        }
+        __syncthreads();
       }
     }
     __syncthreads();

@@ -341,7 +341,6 @@ class HipGoNet:
         self.sc = streamcheck.StreamCheck() if streamcheck.enabled() else None
         self._head_red_defer = False
         self._head_red_pending = False
-        self._win_first = os.environ.get("DG_WIN_FIRST", "0") == "1"
         self._refresh_table = self._build_refresh_table()
         self._step_refresh = None   # the per-step table (plain copies no launch reads dropped)
         self.launches = 0     # native launches issued through _run (SegmentedStep counts them)
@@ -1099,7 +1098,10 @@ class HipGoNet:
         (feature expansion, the heads: labels) exist once per buffer — the second set is the
         first with the input pointers substituted — and SegmentedStep captures one step graph
         per buffer.  Reference: the loader threads filling the next minibatch while the
-        current one trains (/root/reference/data.lua:11-27).  Call before SegmentedStep."""
+        current one trains (/root/reference/data.lua:11-27).  Call before SegmentedStep.
+        (A form with the copy as a memcpy node inside the step graph was measured and dropped
+        in round 6: HIP runs a graph's H2D memcpy node as a blit kernel, which ran after the
+        step's last kernel — +40 us per step; profiles/r6_host_pool_prefetch.txt.)"""
         if self.load_stream is not None:
             return True
         buf1 = torch.zeros_like(self.inbuf)
@@ -1256,19 +1258,9 @@ class HipGoNet:
                 if sc:
                     sc.consume("l0-chain->main", main)
             else:
-                # the weight-gradient launch issued BEFORE the side stream's work when the step
-                # is captured (DG_WIN_FIRST): the graph executor keeps a node's first-created
-                # child on the parent's hardware queue, so the window kernel follows the
-                # backward-data stack on the same queue instead of behind a cross-queue wait
-                win_first = self._win_first and ops[1][0] is not HipGoNet._noop
                 if sc:
                     sc.produce("dz->side", main)
-                if win_first:
-                    fork = main.record_event()   # dZ of the layer (group) final
-                    self._run(ops[1:2], main.cuda_stream)
-                    side.wait_event(fork)
-                else:
-                    side.wait_stream(main)       # dZ of the layer (group) final
+                side.wait_stream(main)           # dZ of the layer (group) final
                 if sc:
                     sc.consume("dz->side", side)
                 self._flush_head_reduce(side.cuda_stream)
@@ -1298,8 +1290,7 @@ class HipGoNet:
                 # (profiles/r4_s1_l0_bias_main_ab.txt)
                 if l0_side:
                     self._run(l0, side.cuda_stream)
-                if not win_first:
-                    self._run(ops[1:2], main.cuda_stream)
+                self._run(ops[1:2], main.cuda_stream)
                 main.wait_event(ev)
                 if sc:
                     sc.consume("partials->reduce", main)

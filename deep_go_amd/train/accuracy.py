@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Dict, Optional
+from typing import Dict, Optional, Sequence
 
 import numpy as np
 import torch
@@ -109,7 +109,8 @@ def fixture_accuracy(device, layers: int = 12, channels: int = 128, dtype: str =
 
 def oracle_parity(device, layers: int = 6, channels: int = 64, batch: int = 64,
                   rate: float = 0.05, steps: int = 500, head_relu: bool = True, seed: int = 5,
-                  threads: int = 16, root: str = FIXTURE) -> Optional[Dict]:
+                  threads: int = 16, root: str = FIXTURE,
+                  perturb: Sequence[float] = ()) -> Optional[Dict]:
     """The accuracy half through the HIP trainer vs the fp32 PyTorch oracle: HIPBackend (bf16
     operands, fp32 master weights, one-graph step) and CPUBackend from the SAME init on the
     SAME game-uniform batch stream of the fixture's training games, ``steps`` SGD steps, then
@@ -117,7 +118,13 @@ def oracle_parity(device, layers: int = 6, channels: int = 64, batch: int = 64,
     training positions (top-1 = argmax == label, NLL = mean -log p).  Default shape: the
     reference's default-experiment.lua (6 layers, d = 64, batch 64) with its head ReLU
     (experiments.lua:133-153), at a rate where it learns (tools/acc_sweep.py).  Returns both
-    runs' losses and scores (None without the packed fixture)."""
+    runs' losses and scores (None without the packed fixture).
+
+    ``perturb``: also run the fp32 oracle from the same init multiplied elementwise by
+    (1 + e * r), r = +-1 at random, for each relative size e — SGD's own sensitivity: once
+    the network leaves the ln 361 plateau the trajectories of any two runs separate (a 1e-5
+    difference grows to O(1) nats), so the HIP run is judged against the spread of such
+    oracle runs ("cpu~e" in the result)."""
     from ..config import ExperimentConfig
     from ..data.dataset import PackedDataset, sample_reference
     from .backends import CPUBackend, HIPBackend
@@ -129,16 +136,22 @@ def oracle_parity(device, layers: int = 6, channels: int = 64, batch: int = 64,
     cfg = ExperimentConfig(numLayers=layers, channelSize=channels, batchSize=batch, rate=rate,
                            rateDecay=1e-7, head_relu=head_relu, seed=seed, useCuda=True)
     cpu_be = CPUBackend(cfg, batch)
-    gpu_be = HIPBackend(cfg, batch, flat=cpu_be.flat_params().clone(), device=device)
+    flat0 = cpu_be.flat_params().clone()
+    runs = {"cpu": cpu_be,
+            "hip": HIPBackend(cfg, batch, flat=flat0.clone(), device=device)}
+    gen = torch.Generator().manual_seed(seed + 1)
+    for e in perturb:
+        r = torch.randint(0, 2, flat0.shape, generator=gen).float() * 2 - 1
+        runs[f"cpu~{e:g}"] = CPUBackend(cfg, batch, flat=flat0 * (1 + e * r))
     rng = np.random.default_rng(seed)
     tr = ds["train"]
     t0 = time.perf_counter()
-    losses = {"cpu": [], "hip": []}
+    losses = {name: [] for name in runs}
     for _ in range(steps):
         g, mv = sample_reference(list(tr.game_count), batch, rng)
         i = tr.game_start[g] + mv - 1
         b = (tr.planes[i], tr.player[i], tr.rank[i], tr.label[i])
-        for name, be in (("cpu", cpu_be), ("hip", gpu_be)):
+        for name, be in runs.items():
             be.set_batch(*b)
             be.train_step()
             losses[name].append(be.loss_sum() / batch)
@@ -155,8 +168,10 @@ def oracle_parity(device, layers: int = 6, channels: int = 64, batch: int = 64,
             nll += be.loss_sum()
         return {"correct": int(correct), "top1": correct / n, "nll": nll / n, "positions": n}
     out = {"model": f"{layers}x{channels}", "batch": batch, "rate": rate, "steps": steps,
-           "head_relu": head_relu, "loss_cpu": losses["cpu"], "loss_hip": losses["hip"]}
+           "head_relu": head_relu, "runs": list(runs)}
+    for name in runs:
+        out[f"loss_{name}"] = losses[name]
     for split in ("validation", "test", "train"):
-        out[split] = {"cpu": score(cpu_be, ds[split]), "hip": score(gpu_be, ds[split])}
+        out[split] = {name: score(be, ds[split]) for name, be in runs.items()}
     out["seconds"] = round(time.perf_counter() - t0, 1)
     return out

@@ -344,10 +344,9 @@ def test_bias_grad():
 
 
 @pytest.mark.parametrize("C", [128, 256])
-def test_bias_grad_multi_units(C):
-    """Multi-layer bias partials (elementwise.hip bias_partial_units_kernel: 16-board
-    sub-chunk units summed in order through LDS; and the per-item kernel it replaces,
-    bias_set_units(0)) vs the fp32 per-chunk sums of the same bf16 frames."""
+def test_bias_grad_multi(C):
+    """Multi-layer bias partials (elementwise.hip bias_grad_partial_kernel<2>, the launch
+    beside the window weight gradient) vs the fp32 per-chunk sums of the same bf16 frames."""
     from deep_go_amd.ops import layouts as LY
     from deep_go_amd.ops.native import hip, stream_handle
     h = hip()
@@ -356,27 +355,17 @@ def test_bias_grad_multi_units(C):
     dz = [bf(torch.randn(B, C, 19, 19, device=DEV)) for _ in range(nl)]
     frames = [LY.to_frame(d, 1) for d in dz]
     nch = h.bias_chunks_multi(B)
-    parts = [torch.empty(nch * (P + 19) * C, device=DEV) for _ in range(nl)]
+    parts = [torch.full((nch * (P + 19) * C,), float("nan"), device=DEV) for _ in range(nl)]
     tab = np.array([[f.data_ptr(), q.data_ptr(), 0] for f, q in zip(frames, parts)],
                    dtype=np.int64)
-    res = {}
-    try:
-        for units in (1, 0):
-            h.bias_set_units(units)
-            for q in parts:
-                q.fill_(float("nan"))
-            h.bias_grad_partial_multi(tab.ctypes.data, nl, B, C, 1, 0, stream_handle())
-            torch.cuda.synchronize()
-            res[units] = [q.clone() for q in parts]
-    finally:
-        h.bias_set_units(1 if os.environ.get("DG_BIAS_UNITS") == "1" else 0)
+    h.bias_grad_partial_multi(tab.ctypes.data, nl, B, C, 1, 0, stream_handle())
+    torch.cuda.synchronize()
     for i in range(nl):
         ref = dz[i].view(nch, B // nch, C, P).sum(1).transpose(1, 2)     # [chunk][p][C]
         ref_r = ref.reshape(nch, 19, 19, C).sum(2)                       # [chunk][h][C]
-        for units in (1, 0):
-            got = res[units][i]
-            assert rel_err(got[:nch * P * C].view(nch, P, C), ref) < 1e-5, (units, i)
-            assert rel_err(got[nch * P * C:].view(nch, 19, C), ref_r) < 1e-5, (units, i)
+        got = parts[i]
+        assert rel_err(got[:nch * P * C].view(nch, P, C), ref) < 1e-5, i
+        assert rel_err(got[nch * P * C:].view(nch, 19, C), ref_r) < 1e-5, i
 
 
 def test_sgd_and_lr_decay():

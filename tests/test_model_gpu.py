@@ -687,7 +687,7 @@ def test_fused_update_all_or_nothing_on_producer_tag(early, where, C):
         if where == "hidden":
             net.dz[net.wgroups[0][0]].view(-1)[3000] = float("nan")
         elif where == "layer0":
-            net.dz[0].view(-1)[3000] = 1e35
+            net.dz[0].view(-1)[23 * C + 5] = 1e35     # board 0, frame row 1, column 2
         for i in range(net.L - 2, -1, -1):
             net.backward_layer(i)
         net.join_side()
@@ -1103,3 +1103,4 @@ def test_stream_handoffs_checked_and_serialized_run_bit_identical(args, tmp_path
     for name in ("check", "serial"):
         assert torch.equal(outs[name]["params"], outs["plain"]["params"]), name
         assert torch.equal(outs[name]["loss"], outs["plain"]["loss"]), name
+

@@ -261,3 +261,82 @@ def test_fp8_stress_vs_bf16_memorisation(tmp_path, ch):
     wa, g = sat[:2 * L], sat[2 * L:]        # weights + activations | e5m2 gradients
     assert wa.sum() < 0.01 * N * wa.size, sat
     assert g.sum() < 0.01 * N * g.size, sat
+
+
+@pytest.mark.timeout(300)
+def test_accuracy_half_matches_fp32_oracle_with_head_relu():
+    """The metric's accuracy half through the HIP trainer against the fp32 PyTorch oracle
+    (VERDICT r5 item 5), at the reference's default-experiment shape WITH its head ReLU
+    (default-experiment.lua: 6 layers, d = 64, batch 64; experiments.lua:133-153): HIPBackend
+    and CPUBackend from the same init on the same game-uniform batch stream of the fixture's
+    training games, 500 SGD steps at rate 0.05 (where this shape learns with the head ReLU:
+    tools/acc_sweep.py; the reference's own .512 pins the loss at ln 361), then both scored
+    on EVERY held-out validation (134) and test (125) position and on the 4139 training
+    positions (train.lua:14-45).
+
+    SGD here is chaotic once the network leaves the ln 361 plateau (~step 250): two fp32
+    oracle runs whose inits differ by a relative 1e-5 separate by 0.1-0.4 nats per step and
+    end 2-5 validation positions apart (profiles/r6_accuracy_parity.txt).  So the
+    tolerances are stated against the oracle's own sensitivity, measured in the same test
+    (oracle runs from the init perturbed by 1e-5 and 1e-3):
+      * before the plateau escape the curves agree: |loss difference| < 1e-3 nats on every
+        one of the first 150 steps (measured <= 7e-5);
+      * both learn: the training loss falls by more than 1 nat;
+      * per split, the HIP run is no further from the oracle than the perturbed oracle runs
+        are, plus 2 positions (held-out games; train: + 0.5% of 4139) in top-1, and plus 1%
+        of the oracle's NLL in NLL.
+    Paper-level top-1 stays parity unpinned (one held-out game per split)."""
+    from deep_go_amd.train.accuracy import oracle_parity
+    r = oracle_parity(torch.device("cuda", 0), layers=6, channels=64, batch=64, rate=0.05,
+                      steps=500, head_relu=True, seed=5, perturb=(1e-5, 1e-3))
+    assert r is not None, "packed fixture missing"
+    import json
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/accuracy_parity_6x64_relu.json", "w") as f:
+        json.dump(r, f)
+    lc, lg = np.array(r["loss_cpu"]), np.array(r["loss_hip"])
+    assert np.isfinite(lg).all()
+    assert np.abs(lc[:150] - lg[:150]).max() < 1e-3, np.abs(lc[:150] - lg[:150]).max()
+    assert lc[-50:].mean() < lc[:50].mean() - 1.0, (lc[:50].mean(), lc[-50:].mean())
+    assert lg[-50:].mean() < lg[:50].mean() - 1.0, (lg[:50].mean(), lg[-50:].mean())
+    pert = [n for n in r["runs"] if n.startswith("cpu~")]
+    for split in ("validation", "test", "train"):
+        sc = r[split]
+        c, g = sc["cpu"], sc["hip"]
+        env_top1 = max(abs(sc[n]["correct"] - c["correct"]) for n in pert)
+        env_nll = max(abs(sc[n]["nll"] - c["nll"]) for n in pert)
+        slack = 2 if split != "train" else int(0.005 * c["positions"])
+        assert abs(g["correct"] - c["correct"]) <= env_top1 + slack, (split, sc)
+        assert abs(g["nll"] - c["nll"]) <= env_nll + 0.01 * c["nll"], (split, sc)
+
+
+@pytest.mark.parametrize("shape", [(6, 64), (12, 128)])
+def test_hip_training_is_bit_reproducible(shape):
+    """Two HIP trainer runs from the same init on the same batch stream end with bit-identical
+    parameters and losses (every reduction has a fixed order: split-K slabs, bias partials,
+    head reduce, the standalone head's per-board weight gradient — whose LDS atomicAdd over
+    the waves made d = 64 runs differ in the last bits, found by the accuracy-half parity runs
+    in round 6).  With the head ReLU (the reference's), 60 steps."""
+    from deep_go_amd.data.dataset import PackedDataset
+    from deep_go_amd.data.loader import BatchLoader
+    from deep_go_amd.train.backends import HIPBackend
+    L, C = shape
+    B = 32
+    pk = PackedDataset.load(os.path.join(FIXTURE, "train.dgpack.npz"))
+    ld = BatchLoader(pk, B, threads=2, prefetch=3, seed=21, pin=False)
+    batches = [ld.next_numpy() for _ in range(60)]
+    ld.close()
+    cfg = ExperimentConfig(numLayers=L, channelSize=C, batchSize=B, rate=0.05, seed=8,
+                           head_relu=True, useCuda=True)
+    out = []
+    for _ in range(2):
+        be = HIPBackend(cfg, B)
+        losses = []
+        for bt in batches:
+            be.set_batch(*bt)
+            be.train_step()
+            losses.append(be.loss_sum())
+        out.append((be.flat_params().clone(), losses))
+        del be
+    assert out[0][1] == out[1][1]
+    assert torch.equal(out[0][0], out[1][0])

@@ -17,12 +17,19 @@ def main():
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--perturb", default="", help="comma-separated relative init perturbations "
+                    "of extra fp32 oracle runs (SGD's own sensitivity)")
     a = ap.parse_args()
     import numpy as np
     import torch
     from deep_go_amd.train.accuracy import oracle_parity
     r = oracle_parity(torch.device("cuda", 0), layers=a.layers, channels=a.channels,
-                      batch=a.batch, rate=a.rate, steps=a.steps, seed=a.seed)
+                      batch=a.batch, rate=a.rate, steps=a.steps, seed=a.seed,
+                      perturb=[float(x) for x in a.perturb.split(",") if x])
+    for n in r["runs"][2:]:
+        lp = np.array(r.pop(f"loss_{n}"))
+        r[f"gap_{n}_vs_cpu"] = {str(k): round(float(abs(lp[k] - np.array(r["loss_cpu"])[k])), 5)
+                                for k in (100, 200, 300, 400, len(lp) - 1) if k < len(lp)}
     lc, lg = np.array(r.pop("loss_cpu")), np.array(r.pop("loss_hip"))
     r["loss_first50"] = [round(lc[:50].mean(), 4), round(lg[:50].mean(), 4)]
     r["loss_last50"] = [round(lc[-50:].mean(), 4), round(lg[-50:].mean(), 4)]
