@@ -401,7 +401,7 @@ def run_cpu_dry(args) -> int:
     if info.rank == 0:
         args.layers, args.channels = cfg.numLayers, cfg.channelSize
         rec = _record(args, world, elapsed_all, cfg.train_flops_per_board(),
-                      {"dry_run": "cpu-gloo", "dtype": "fp32",
+                      {"dry_run": "cpu-gloo", "dtype": "fp32", "grad_dtype": "fp32",
                        "comm": f"gloo ({kind} set-up rehearsed)"})
         rec["config"]["model"] = "cpu-1layer-k16 (BASELINE config 1; dry run, not a GPU number)"
         print(json.dumps(rec), flush=True)

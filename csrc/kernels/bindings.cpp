@@ -66,6 +66,7 @@ hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int 
                             const float* bias, const float* posb, const void* pbias,
                             const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
+void dg_conv_wgrad5_set_ns(int ns);
 int dg_conv_wgrad_wgs_per_cu();
 int dg_conv_wgrad_ktile(int KP);
 int dg_conv_wgrad_wgs_per_cu_for(int KP);
@@ -518,6 +519,8 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
+  m.def("conv_wgrad5_set_ns", [](int ns) { dg_conv_wgrad5_set_ns(ns); },
+        "5x5 weight gradient: 0 = conv_wgrad_kernel, 4 | 5 = conv_wgrad_pipe_kernel stages");
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });
   m.def("conv_wgrad_multi", [](int kw, uintptr_t table, int nl, int dz_pad, int M, int Mpad,
                                int x_pad, int x_C, int B, int KP, int splits, uintptr_t stream) {

@@ -453,6 +453,156 @@ conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// The same tile and the same summation order as conv_wgrad_kernel (so bit-identical slabs),
+// with a deeper LDS-DMA pipeline: 32-pixel K-steps, NS stage buffers of 16 KB (dZ 32 x 256 B
+// + X 32 x 256 B) and PD = NS - 1 steps in flight, issued from inline asm (dma16) with exact
+// vmcnt accounting (every wave issues exactly 4 DMAs per stage: 2 dZ + 2 X blocks of 4 rows).
+// Why: the first layer's 5x5 weight gradient (K = 25 taps x 40 channels, 64 pixel splits)
+// is latency-bound in conv_wgrad_kernel — one 32-KB stage in flight per workgroup, 32 MFMAs
+// (~256 cycles) per wave between a DMA issue and its wait — and it sits on the step's critical
+// tail after the window weight gradient in every configuration.  Each wave also reads half
+// as many fragments per step (one 32-row k-half), so its registers stay below
+// conv_wgrad_kernel's.
+template <int KW, int NS>
+__global__ void __launch_bounds__(256, 2)
+conv_wgrad_pipe_kernel(WgradArgs a) {
+  constexpr int BKN = 32;                      // pixels per K-step
+  constexpr int T_BYTES = BKN * 256;           // 32 rows x 256 B
+  constexpr int STAGE = 2 * T_BYTES;           // dZ tile + X tile: 16 KB
+  constexpr int PD = NS - 1;                   // K-steps in flight beyond the current one
+  static_assert(NS >= 2 && NS <= 5, "stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t smem_u = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = a.ktiles * a.mtiles * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, xslot = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + xslot;
+  const int kt = lid % a.ktiles;
+  const int rest = lid / a.ktiles;
+  const int mt = rest % a.mtiles;
+  const int zsplit = rest / a.mtiles;
+  const int k_tile = kt * 128;
+  const int m_tile = mt * 128;
+  const int n_begin = zsplit * a.px_per_split;
+  int n_end = n_begin + a.px_per_split;
+  if (n_end > a.Npix) n_end = a.Npix;
+  const int nsteps = n_end > n_begin ? (n_end - n_begin + BKN - 1) / BKN : 0;
+
+  // staging: a DMA instruction = 4 rows x 16 slots of 16 B; wave w fills rows (2w + i) * 4 ..
+  const int r_in = lane >> 4;
+  const int slot = lane & 15;
+  int koffs[2], dz_chunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 2 + i) * 4 + r_in;
+    const int c = slot ^ wg_swz(r);
+    dz_chunk[i] = (m_tile * 2) + c * 16;
+    koffs[i] = koff_wg<KW>(k_tile / 8 + c, a);
+  }
+  auto issue = [&](int buf, int step) {
+    const uint32_t base = smem_u + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wave * 2 + i) * 4 + r_in;
+      int n = n_begin + step * BKN + r;
+      const bool ok = n < n_end;
+      if (!ok) n = n_begin;  // valid address; the dZ row reads the zero border instead
+      const int b = n / NPTS;
+      const int p = n - b * NPTS;
+      const int h = p / BOARD;
+      const int w = p - h * BOARD;
+      const uint32_t dzo = frame_off(b, h, w, a.dz_pad, a.M);
+      const uint32_t xo = frame_off(b, h, w, a.x_pad, a.x_C);
+      const char* src_dz = ok ? (a.dZ + dzo + dz_chunk[i]) : (a.dZ + (slot * 16));
+      const uint32_t dst = base + (wave * 2 + i) * 1024;
+      dma16(src_dz, __builtin_amdgcn_readfirstlane(dst));
+      dma16(a.X + xo + koffs[i], __builtin_amdgcn_readfirstlane(dst + T_BYTES));
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < nsteps) issue(p % NS, p);
+  const int li = lane & 15;
+  const int g = lane >> 4;
+  const int q = li >> 2, pp = li & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    // this wave's DMAs of step st landed (those of st + 1 .. st + PD - 1 may remain), then
+    // every wave's (barrier) — which also retires every wave's reads of step st - 1, whose
+    // buffer the issue below refills
+    const int ahead = min(PD - 1, nsteps - 1 - st);
+    if (ahead >= 3) dma_wait<12>();
+    else if (ahead == 2) dma_wait<8>();
+    else if (ahead == 1) dma_wait<4>();
+    else dma_wait<0>();
+    __syncthreads();
+    if (st + PD < nsteps) issue((st + PD) % NS, st + PD);
+    const char* sA = smem + (st % NS) * STAGE;
+    const char* sB = sA + T_BYTES;
+    s16x4 ta[2][4], tb[2][4];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 8 * g + 4 * half + q;
+      const int sw = wg_swz(row);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = (wm * 64 + i * 16) / 8 + (pp >> 1);
+        ta[half][i] =
+            lds_read_tr((const LDS_AS char*)(sA + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = (wn * 64 + j * 16) / 8 + (pp >> 1);
+        tb[half][j] =
+            lds_read_tr((const LDS_AS char*)(sB + row * 256 + ((c ^ sw) * 16) + (pp & 1) * 8));
+      }
+    }
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const s16x4 lo = ta[0][i], hi = ta[1][i];
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x4 lo = tb[0][j], hi = tb[1][j];
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[j] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+  }
+
+  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m_tile + wm * 64 + i * 16 + g * 4 + r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k_tile + wn * 64 + j * 16 + li;
+        slab[(size_t)co * a.KP + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // Three-tap variant of conv_wgrad_kernel: one workgroup (8 waves) owns a 128 co x 384 k
 // tile — three consecutive 128-k slices (e.g. the three dw taps of one kernel row) — so the
 // dZ rows staged for a 64-pixel step serve three slices instead of one: 64 KB of LDS-DMA
@@ -831,6 +981,14 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
 
 static int g_wgrad_ablate = 0;
 void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
+// the 5x5 weight gradient's kernel: 0 = conv_wgrad_kernel (2 x 64-pixel stages), 4 | 5 =
+// conv_wgrad_pipe_kernel with that many 32-pixel stages (DG_WGRAD5_NS; bit-identical slabs)
+static int g_wgrad5_ns = [] {
+  const char* e = getenv("DG_WGRAD5_NS");
+  const int v = e ? atoi(e) : 0;
+  return v == 4 || v == 5 ? v : 0;
+}();
+void dg_conv_wgrad5_set_ns(int ns) { g_wgrad5_ns = ns == 4 || ns == 5 ? ns : 0; }
 int dg_conv_wgrad_wgs_per_cu() { return 2; }
 // k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K: the
 // three-slice kernel wherever K is a multiple of 384
@@ -883,8 +1041,18 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
     case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), lds, stream, a); break;
     case 5:
-      allow_lds(conv_wgrad_kernel<5>, lds);
-      hipLaunchKernelGGL(conv_wgrad_kernel<5>, grid, dim3(256), lds, stream, a);
+      if (g_wgrad5_ns == 5 && g_wgrad_ablate == 0) {
+        constexpr size_t lds5 = 5 * 16 * 1024;
+        allow_lds(conv_wgrad_pipe_kernel<5, 5>, lds5);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<5, 5>), grid, dim3(256), lds5, stream, a);
+      } else if (g_wgrad5_ns == 4 && g_wgrad_ablate == 0) {
+        constexpr size_t lds4 = 4 * 16 * 1024;
+        allow_lds(conv_wgrad_pipe_kernel<5, 4>, lds4);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<5, 4>), grid, dim3(256), lds4, stream, a);
+      } else {
+        allow_lds(conv_wgrad_kernel<5>, lds);
+        hipLaunchKernelGGL(conv_wgrad_kernel<5>, grid, dim3(256), lds, stream, a);
+      }
       break;
     default: return hipErrorInvalidValue;
   }

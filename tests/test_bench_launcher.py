@@ -32,9 +32,24 @@ def test_launcher_spawns_n_ranks_one_json_line(n):
     assert rec["config"]["parallelism"] == f"dp{n}"
     assert rec["rank_ms_per_step_max"] >= rec["rank_ms_per_step_min"] > 0
     assert rec["value"] > 0 and rec["dry_run"] == "cpu-gloo"
+    # the gradient reduce at the reference's precision (DataParallelTable: fp32)
+    assert rec["grad_dtype"] == "fp32"
     for k in ("metric", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
               "dtype", "data"):
         assert k in rec
+
+
+def test_bench_defaults_fp32_gradient_wire_and_host_pool():
+    """bench.py's defaults: the DP gradient all-reduce in fp32 (the
+    bf16 wire only as a labelled secondary), the synthetic pool in pinned host memory, and
+    the real-data (C++ loader) secondary in the default list."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse([])
+    assert a.grad_dtype == "fp32" and not a.device_pool and not a.no_bf16_wire_secondary
+    assert "256:bf16:fixture" in a.secondary.split(",")
+    from deep_go_amd.config import ExperimentConfig
+    assert ExperimentConfig().grad_dtype == "fp32"
 
 
 def test_launcher_fails_loudly_when_a_rank_fails():

@@ -218,6 +218,32 @@ def test_conv_wgrad(B, cin, cout, k, splits):
     assert rel_err(gb, dz.sum((0, 2, 3))) < 1e-4
 
 
+@pytest.mark.parametrize("B,cout,splits", [(2, 128, 3), (7, 128, None), (256, 128, 64),
+                                           (5, 256, 4)])
+def test_conv_wgrad5_pipe_bit_identical(B, cout, splits):
+    """The first layer's 5x5 weight gradient on conv_wgrad_pipe_kernel (32-pixel K-steps,
+    4 or 5 LDS-DMA stages in flight) vs conv_wgrad_kernel (two 64-pixel stages): the same
+    tiles and the same MFMA summation order, so BIT-identical gradients (B = 256: the
+    flagship shape, 64 splits) — and both against the fp32 reference."""
+    torch.manual_seed(5)
+    from deep_go_amd.ops import functional as Fn
+    from deep_go_amd.ops.native import hip
+    x = bf(torch.relu(torch.randn(B, 37, 19, 19, device=DEV)))
+    dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
+    res = {}
+    try:
+        for ns in (0, 4, 5):
+            hip().conv_wgrad5_set_ns(ns)
+            res[ns] = Fn.conv_wgrad(dz, x, 5, splits=splits, cinp=40, algo="im2col")
+            torch.cuda.synchronize()
+    finally:
+        hip().conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "0")))
+    assert torch.equal(res[0], res[4]) and torch.equal(res[0], res[5])
+    w0 = torch.zeros(cout, 5, 5, 37, device=DEV, requires_grad=True)
+    (gw,) = torch.autograd.grad(conv_ref(x, w0, 5), w0, dz)
+    assert rel_err(res[5], gw) < 1e-3
+
+
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),
                                          (4, 64, 128, 3), (5, 16, 128, 5)])
 def test_conv_l1(B, cin, cout, k):

@@ -43,6 +43,18 @@ def main():
                 h.conv_wgrad_set_ablate(mode)
                 res.setdefault(f"s{splits}_abl{mode}", []).append(round(timeit(wg), 2))
         h.conv_wgrad_set_ablate(0)
+    # conv_wgrad_pipe_kernel (32-pixel K-steps, NS LDS-DMA stages) vs conv_wgrad_kernel (ns 0)
+    for splits in sorted({plan // 2, plan, plan * 2}):
+        slab = torch.empty(splits * Mpad * KPw, device=dev)
+
+        def wgp():
+            h.conv_wgrad(5, dz.data_ptr(), 1, C, Mpad, x.data_ptr(), 2, CIN, B, KPw, splits,
+                         slab.data_ptr(), s)
+        for rnd in range(3):
+            for ns in (0, 4, 5):
+                h.conv_wgrad5_set_ns(ns)
+                res.setdefault(f"pipe_ns{ns}_s{splits}", []).append(round(timeit(wgp), 2))
+    h.conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "0")))
     # the three-slice kernel (128 co x 384 k, dZ staged once per 3 k-tiles) at K padded to
     # 1152 (12.5% more MFMA work, a third less LDS-DMA per k-tile)
     KP3 = 1152
