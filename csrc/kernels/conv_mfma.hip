@@ -470,7 +470,7 @@ conv_wgrad_pipe_kernel(WgradArgs a) {
   constexpr int T_BYTES = BKN * 256;           // 32 rows x 256 B
   constexpr int STAGE = 2 * T_BYTES;           // dZ tile + X tile: 16 KB
   constexpr int PD = NS - 1;                   // K-steps in flight beyond the current one
-  static_assert(NS >= 2 && NS <= 5, "stages");
+  static_assert(NS >= 2 && NS <= 4, "stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t smem_u = (uint32_t)(uintptr_t)(LDS_AS char*)smem;
 
@@ -543,8 +543,7 @@ conv_wgrad_pipe_kernel(WgradArgs a) {
     // every wave's (barrier) — which also retires every wave's reads of step st - 1, whose
     // buffer the issue below refills
     const int ahead = min(PD - 1, nsteps - 1 - st);
-    if (ahead >= 3) dma_wait<12>();
-    else if (ahead == 2) dma_wait<8>();
+    if (ahead >= 2) dma_wait<8>();
     else if (ahead == 1) dma_wait<4>();
     else dma_wait<0>();
     __syncthreads();
@@ -981,14 +980,15 @@ hipError_t dg_conv_nt(int epi, int kw, int bm, int bn, const void* A, int KP, in
 
 static int g_wgrad_ablate = 0;
 void dg_conv_wgrad_set_ablate(int m) { g_wgrad_ablate = m; }
-// the 5x5 weight gradient's kernel: 0 = conv_wgrad_kernel (2 x 64-pixel stages), 4 | 5 =
-// conv_wgrad_pipe_kernel with that many 32-pixel stages (DG_WGRAD5_NS; bit-identical slabs)
+// the 5x5 weight gradient's kernel: 4 = conv_wgrad_pipe_kernel with four 32-pixel stages
+// (default: 32.0 vs 32.9 us alone, +0.1..+0.7% in the four configurations' steps, 108 vs 165
+// VGPRs; five stages measured slower, 37 us: profiles/r6_wgrad5_pipe.txt), 0 =
+// conv_wgrad_kernel (two 64-pixel stages; bit-identical slabs).  DG_WGRAD5_NS=0 | 4
 static int g_wgrad5_ns = [] {
   const char* e = getenv("DG_WGRAD5_NS");
-  const int v = e ? atoi(e) : 0;
-  return v == 4 || v == 5 ? v : 0;
+  return e && atoi(e) == 0 ? 0 : 4;
 }();
-void dg_conv_wgrad5_set_ns(int ns) { g_wgrad5_ns = ns == 4 || ns == 5 ? ns : 0; }
+void dg_conv_wgrad5_set_ns(int ns) { g_wgrad5_ns = ns == 4 ? 4 : 0; }
 int dg_conv_wgrad_wgs_per_cu() { return 2; }
 // k-tile width / workgroups per CU of the kernel dg_conv_wgrad will use for this K: the
 // three-slice kernel wherever K is a multiple of 384
@@ -1041,11 +1041,7 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
     case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(conv_wgrad_kernel<3>, grid, dim3(256), lds, stream, a); break;
     case 5:
-      if (g_wgrad5_ns == 5 && g_wgrad_ablate == 0) {
-        constexpr size_t lds5 = 5 * 16 * 1024;
-        allow_lds(conv_wgrad_pipe_kernel<5, 5>, lds5);
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<5, 5>), grid, dim3(256), lds5, stream, a);
-      } else if (g_wgrad5_ns == 4 && g_wgrad_ablate == 0) {
+      if (g_wgrad5_ns == 4 && g_wgrad_ablate == 0) {
         constexpr size_t lds4 = 4 * 16 * 1024;
         allow_lds(conv_wgrad_pipe_kernel<5, 4>, lds4);
         hipLaunchKernelGGL((conv_wgrad_pipe_kernel<5, 4>), grid, dim3(256), lds4, stream, a);

@@ -95,7 +95,12 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
   float* prow = part + ((size_t)chunk * NPTS + h * BOARD) * C;
   // blockDim covers all 19*C/8 items of the row in ONE pass (the 256-thread version ran a
   // second pass on 48 threads whose load latency the whole workgroup waited for)
-  float dzmax = 0.f;   // max |dZ| read (the step tag; NaN shows in the sums)
+  float dzmax = 0.f;   // max |dZ| read, fp8 frames (the step tag; NaN shows in the sums)
+  // bf16 frames: the max |bits| of the two halves of every word read (one AND + one packed
+  // 16-bit max per word; the float fabs / fmax form doubled the VALU work of a kernel that
+  // runs beside the window weight gradient and slowed both at d = 256)
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 hmax = {0, 0};
   bool nonfinite = false;
   for (int it = tid; it < items; it += blockDim.x) {
     const int w = it / G, g = it - (it / G) * G;
@@ -140,8 +145,8 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
           for (int e = 0; e < 4; ++e) {
             acc[2 * e] += __uint_as_float(u[e] << 16);
             acc[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
-            dzmax = fmaxf(dzmax, fmaxf(fabsf(__uint_as_float(u[e] << 16)),
-                                       fabsf(__uint_as_float(u[e] & 0xFFFF0000u))));
+            hmax = __builtin_elementwise_max(hmax,
+                                             __builtin_bit_cast(u16x2, u[e] & 0x7FFF7FFFu));
           }
         }
       }
@@ -155,7 +160,9 @@ bias_grad_partial_kernel(BiasLayers Ls, int B, int C, int pad, int nchunks, int 
 #pragma unroll
     for (int e = 0; e < 8; ++e) sr[e] = acc[e];
   }
-  if (Ls.sf && (nonfinite || !(dzmax < DZ_BOUND))) flag_bad_step(Ls.sf);
+  // (bf16 bits of 2^100 = 0x7180; a NaN's or an infinity's |bits| exceed it)
+  const unsigned hm = hmax.x > hmax.y ? hmax.x : hmax.y;
+  if (Ls.sf && (nonfinite || !(dzmax < DZ_BOUND) || hm >= 0x7180u)) flag_bad_step(Ls.sf);
   __syncthreads();
   float* rowpart = part + (size_t)nchunks * NPTS * C + ((size_t)chunk * BOARD + h) * C;
   for (int c = tid; c < C; c += blockDim.x) {

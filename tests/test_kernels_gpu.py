@@ -222,7 +222,7 @@ def test_conv_wgrad(B, cin, cout, k, splits):
                                            (5, 256, 4)])
 def test_conv_wgrad5_pipe_bit_identical(B, cout, splits):
     """The first layer's 5x5 weight gradient on conv_wgrad_pipe_kernel (32-pixel K-steps,
-    4 or 5 LDS-DMA stages in flight) vs conv_wgrad_kernel (two 64-pixel stages): the same
+    four LDS-DMA stages) vs conv_wgrad_kernel (two 64-pixel stages): the same
     tiles and the same MFMA summation order, so BIT-identical gradients (B = 256: the
     flagship shape, 64 splits) — and both against the fp32 reference."""
     torch.manual_seed(5)
@@ -232,16 +232,16 @@ def test_conv_wgrad5_pipe_bit_identical(B, cout, splits):
     dz = bf(torch.randn(B, cout, 19, 19, device=DEV))
     res = {}
     try:
-        for ns in (0, 4, 5):
+        for ns in (0, 4):
             hip().conv_wgrad5_set_ns(ns)
             res[ns] = Fn.conv_wgrad(dz, x, 5, splits=splits, cinp=40, algo="im2col")
             torch.cuda.synchronize()
     finally:
-        hip().conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "0")))
-    assert torch.equal(res[0], res[4]) and torch.equal(res[0], res[5])
+        hip().conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "4")))
+    assert torch.equal(res[0], res[4])
     w0 = torch.zeros(cout, 5, 5, 37, device=DEV, requires_grad=True)
     (gw,) = torch.autograd.grad(conv_ref(x, w0, 5), w0, dz)
-    assert rel_err(res[5], gw) < 1e-3
+    assert rel_err(res[4], gw) < 1e-3
 
 
 @pytest.mark.parametrize("B,cin,cout,k", [(3, 37, 128, 5), (2, 40, 256, 5), (1, 37, 96, 5),

@@ -51,10 +51,10 @@ def main():
             h.conv_wgrad(5, dz.data_ptr(), 1, C, Mpad, x.data_ptr(), 2, CIN, B, KPw, splits,
                          slab.data_ptr(), s)
         for rnd in range(3):
-            for ns in (0, 4, 5):
+            for ns in (0, 4):
                 h.conv_wgrad5_set_ns(ns)
                 res.setdefault(f"pipe_ns{ns}_s{splits}", []).append(round(timeit(wgp), 2))
-    h.conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "0")))
+    h.conv_wgrad5_set_ns(int(os.environ.get("DG_WGRAD5_NS", "4")))
     # the three-slice kernel (128 co x 384 k, dZ staged once per 3 k-tiles) at K padded to
     # 1152 (12.5% more MFMA work, a third less LDS-DMA per k-tile)
     KP3 = 1152
