@@ -41,7 +41,6 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
                               int KP, int splits, long long* sf, hipStream_t stream);
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus);
 void dg_conv_wgrad_win8_set_ablate(int mode);
-void dg_conv_wgrad_win8_set_cot(int cot, int nw);
 hipError_t dg_conv_stack_f8_fwd_head(int C, const long long* table, int nl, const void* X0,
                                      const float* s_x0, unsigned* amax_x0, int B, const float* w,
                                      const float* bias, const float* posb, const int* labels,
@@ -270,9 +269,6 @@ PYBIND11_MODULE(_dghip, m) {
   }, "the e5m2 backward-data stack (conv_stack_f8 epi 2) with optional fp8 copies (y8, 0: "
      "none) and stochastic rounding seeded by the int64 device step counter sr_step (0: "
      "round to nearest even)");
-  m.def("conv_wgrad_win8_set_cot", [](int cot, int nw) { dg_conv_wgrad_win8_set_cot(cot, nw); },
-        "conv_wgrad_win8 workgroup co tile 64 | 128 and waves 8 | 4 (4: co tile 128 only; "
-        "overrides DG_WIN8_COT; set before sizing slabs with conv_wgrad_win8_splits)");
   m.def("conv_wgrad_win8_set_ablate", [](int mode) { dg_conv_wgrad_win8_set_ablate(mode); },
         "conv_wgrad_win8 timing ablation (tools/kbench_win8.py; 0 = production): 1 no MFMA, "
         "2 no LDS reads, 4 no LDS-DMA, 8 no slab store, 16 no barrier (sums of these)");

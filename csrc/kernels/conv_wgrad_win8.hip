@@ -100,16 +100,11 @@ DG_DEV i32x2 tr8(const LDS_AS char* p) {
 // MODE: 0 in production; timing ablations (tools/kbench_win8.py, wrong results): 1 no MFMA,
 // 2 no LDS fragment reads (register operands), 4 no LDS-DMA (nothing issued or waited for),
 // 8 no slab store, 16 no per-super-step barrier.
-// COT: the workgroup's co tile, 64 or 128.  128 (MI = 4 fragments per wave at NW = 8): the
-// X slice (64 ci) of a (layer, split) is streamed by one workgroup instead of two (C = 128;
-// 2 instead of 4 at C = 256) and a wave reads 52 tr8 fragments per 36 MFMAs instead of 44
-// per 18 (tools/kbench_win8.py ablations: the 64-co kernel is DMA- and LDS-bound, not MFMA-
-// bound); dZ rows of 128 B in LDS, 16-B chunk c at c ^ ((R >> 1) & 7) (any 16 consecutive
-// rows: 16 distinct (bank half, chunk) pairs for the tr8 reads).
+// COT: the workgroup's co tile (64; the 128-co forms were removed in round 6, see WIN8_COT).
 template <int NW, int RA, int PD, int MODE = 0, int COT = 64>
 __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Args a, Win8Layers Ls) {
   static_assert(PD >= 2 && PD <= PD_MAX, "prefetch distance");
-  static_assert(COT == 64 || COT == 128, "co tile");
+  static_assert(COT == 64, "co tile");
   constexpr int MI = COT / 16 / (NW / 4);   // 16-co accumulator fragments per wave
   constexpr int XPW = NW == 4 ? 3 : 2;   // X blocks per wave per super-step (12 | 16 >= 11)
   constexpr int DZB = 128 * COT;         // one super-step of dZ rows (8 | 16 KB)
@@ -333,19 +328,11 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) conv_wgrad_win8_kernel(Win8Ar
 }  // namespace
 
 int g_win8_ablate = 0;
-// the workgroup co tile: 0 = not yet read from DG_WIN8_COT ("64" | "128" | "128,4": 4 waves,
-// one per SIMD with the whole register file), else 64 / 128; its wave count (8 | 4)
-int g_win8_cot = 0, g_win8_nw = 8;
-int win8_cot() {
-  if (g_win8_cot == 0) {
-    const char* e = getenv("DG_WIN8_COT");
-    int c = 64, w = 8;
-    if (e) sscanf(e, "%d,%d", &c, &w);
-    g_win8_cot = c == 128 ? 128 : 64;
-    g_win8_nw = g_win8_cot == 128 && w == 4 ? 4 : 8;
-  }
-  return g_win8_cot;
-}
+// workgroup co tile: 64.  (The 128-co tiles — 8 waves with 4 fragments each, or 4 waves with
+// the whole register file — were 8-13% faster alone but 6-9% slower in the step: 128 KB of
+// LDS per workgroup left no room for the side-stream kernels; removed in round 6,
+// profiles/r5_win8_ablation.txt.)
+constexpr int WIN8_COT = 64;
 
 extern "C" {
 
@@ -356,7 +343,7 @@ extern "C" {
 // (256 + 224) of 278 super-steps; d = 128 (40 pairs): 6 splits = 1 round of 139 (1 split
 // would leave 96 CUs idle; a perfect fill at 8 / 32 splits writes 2.7x / 5x the slabs).
 int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
-  const int cot = win8_cot();
+  const int cot = WIN8_COT;
   const int pairs = nl * (M / cot) * (Cx / 64);
   const int TS = B * SPB / 4;
   if (pairs <= 0 || num_cus <= 0) return 1;
@@ -377,7 +364,7 @@ int dg_conv_wgrad_win8_splits(int nl, int M, int Cx, int B, int num_cus) {
 // e4m3), slab, s_dz, s_x} (int64)
 hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, int Cx, int B,
                               int KP, int splits, long long* sf, hipStream_t stream) {
-  const int cot = win8_cot();
+  const int cot = WIN8_COT;
   if (nl <= 0 || nl > MAXL || M % cot != 0 || Mpad < M || Cx % 64 != 0 || KP < 9 * Cx ||
       B <= 0 || B % 4 != 0 || splits <= 0 || splits > B * SPB / 4)
     return hipErrorInvalidValue;
@@ -399,41 +386,6 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
   // (B reads 2 taps ahead measured the same as 1: profiles/r4_s1_fused_update_and_fp8_bisection.txt)
   // prefetch distance 3: 4 measured equal (12x256 fp8 133.7k vs 133.9k,
   // profiles/r4_s2_sr_hash_win8_pd_ab.txt)
-  if (cot == 128 && g_win8_nw == 4) {
-    // (read-ahead experiments: ablate 64 / 65 = RA 1 / 3)
-    if (g_win8_ablate == 64) {
-      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 1, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
-      return hipGetLastError();
-    }
-    if (g_win8_ablate == 65) {
-      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 3, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
-      return hipGetLastError();
-    }
-    if (g_win8_ablate == 66) {
-      hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 4, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
-      return hipGetLastError();
-    }
-    switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
-#define DG_W8(m) \
-    case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 3, m, 128>), grid, dim3(256), 0, stream, a, Ls); break;
-      DG_W8(1) DG_W8(2) DG_W8(4) DG_W8(6) DG_W8(16)
-#undef DG_W8
-      default:
-        hipLaunchKernelGGL((conv_wgrad_win8_kernel<4, 2, 3, 0, 128>), grid, dim3(256), 0, stream, a, Ls);
-    }
-    return hipGetLastError();
-  }
-  if (cot == 128) {
-    switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
-#define DG_W8(m) \
-    case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, m, 128>), grid, dim3(512), 0, stream, a, Ls); break;
-      DG_W8(1) DG_W8(2) DG_W8(3) DG_W8(4) DG_W8(6) DG_W8(7) DG_W8(8) DG_W8(16) DG_W8(20) DG_W8(31)
-#undef DG_W8
-      default:
-        hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, 0, 128>), grid, dim3(512), 0, stream, a, Ls);
-    }
-    return hipGetLastError();
-  }
   switch (g_win8_ablate) {   // (timing ablations: tools/kbench_win8.py)
 #define DG_W8(m) \
   case m: hipLaunchKernelGGL((conv_wgrad_win8_kernel<8, 1, 3, m>), grid, dim3(512), 0, stream, a, Ls); break;
@@ -446,12 +398,5 @@ hipError_t dg_conv_wgrad_win8(const long long* table, int nl, int M, int Mpad, i
 }
 
 void dg_conv_wgrad_win8_set_ablate(int mode) { g_win8_ablate = mode; }
-
-// the workgroup co tile (64 | 128; overrides DG_WIN8_COT): the split count query and every
-// later launch follow it, so set it before sizing slabs
-void dg_conv_wgrad_win8_set_cot(int cot, int nw) {
-  g_win8_cot = cot == 128 ? 128 : 64;
-  g_win8_nw = g_win8_cot == 128 && nw == 4 ? 4 : 8;
-}
 
 }  // extern "C"

@@ -5,9 +5,9 @@ wrong results, timing only): 1 no MFMA, 2 no LDS fragment reads, 4 no LDS-DMA, 8
 store, 16 no per-super-step barrier, and sums.  Random e4m3 / e5m2 frames.  Prints one JSON
 line (us per launch, min over rounds; MFMA floor = 32 cycles x MFMAs per SIMD).
 
-  python tools/kbench_win8.py [--C 128,256] [--modes 0,1,2,4,8,16,3,6,7,20,31] [--cot 64,128]
+  python tools/kbench_win8.py [--C 128,256] [--modes 0,1,2,4,8,16,3,6,7,20,31]
 
-(--cot: the workgroup co tile, conv_wgrad_win8_set_cot; the split count follows it.)"""
+(The 128-co workgroup tiles measured in round 5 were removed in round 6.)"""
 import argparse
 import json
 import os
@@ -67,19 +67,13 @@ def main():
     ap.add_argument("--boards", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--modes", default="0,1,2,4,8,16,3,6,7,20,31")
-    ap.add_argument("--cot", default="64,128,128x4",
-                    help="workgroup co tiles to run (128x4: four waves, one per SIMD)")
     a = ap.parse_args()
     h = hip()
     s = stream_handle()
     modes = [int(m) for m in a.modes.split(",")]
     out = {"boards": a.boards, "layers": a.layers}
-    for cot in a.cot.split(","):
-        c, _, w = cot.partition("x")
-        h.conv_wgrad_win8_set_cot(int(c), int(w or 8))
-        for C in [int(c) for c in a.C.split(",")]:
-            out[f"C{C}_cot{cot}"] = bench_c(h, C, a.layers, a.boards, modes, a.rounds, s)
-    h.conv_wgrad_win8_set_cot(64, 8)
+    for C in [int(c) for c in a.C.split(",")]:
+        out[f"C{C}"] = bench_c(h, C, a.layers, a.boards, modes, a.rounds, s)
     print(json.dumps(out))
 
 
