@@ -66,11 +66,6 @@ hipError_t dg_conv_board_ex(int epi, int kw, int bm, const void* A, int KP, int 
                             const void* aux, int aux_pad, void* mask, hipStream_t stream);
 void dg_conv_wgrad_set_ablate(int mode);
 void dg_conv_wgrad5_set_ns(int ns);
-hipError_t dg_conv_wgrad_gp(const void* dZ, int dz_pad, int M, int Mpad, const void* X,
-                            int x_pad, int x_C, int B, int KP, int splits, float* slab,
-                            float* gpart, unsigned* tickets, int gsize, long long* sf,
-                            hipStream_t stream);
-int dg_conv_wgrad_gp_groups(int splits, int gsize);
 int dg_conv_wgrad_wgs_per_cu();
 int dg_conv_wgrad_ktile(int KP);
 int dg_conv_wgrad_wgs_per_cu_for(int KP);
@@ -520,18 +515,6 @@ PYBIND11_MODULE(_dghip, m) {
   m.def("conv_board_set_ablate", [](int mode) { dg_conv_board_set_ablate(mode); },
         "diagnostics: 1 skip MFMA, 2 skip LDS fragment reads, 4 skip DMA");
   m.def("conv_wgrad_set_ablate", [](int mode) { dg_conv_wgrad_set_ablate(mode); });
-  m.def("conv_wgrad_gp", [](uintptr_t dZ, int dz_pad, int M, int Mpad, uintptr_t X, int x_pad,
-                            int x_C, int B, int KP, int splits, uintptr_t slab, uintptr_t gpart,
-                            uintptr_t tickets, int gsize, uintptr_t sf, uintptr_t stream) {
-    check(dg_conv_wgrad_gp(P<void>(dZ), dz_pad, M, Mpad, P<void>(X), x_pad, x_C, B, KP, splits,
-                           P<float>(slab), P<float>(gpart), P<unsigned>(tickets), gsize,
-                           P<long long>(sf), S(stream)),
-          "conv_wgrad_gp");
-  }, "5x5 weight gradient whose last split of each group of gsize sums the group's slabs into "
-     "gpart (the fused update / reduce reads ceil(splits / gsize) groups)");
-  m.def("conv_wgrad_gp_groups", [](int splits, int gsize) {
-    return dg_conv_wgrad_gp_groups(splits, gsize);
-  });
   m.def("conv_wgrad5_set_ns", [](int ns) { dg_conv_wgrad5_set_ns(ns); },
         "5x5 weight gradient: 0 = conv_wgrad_kernel, 4 | 5 = conv_wgrad_pipe_kernel stages");
   m.def("conv_wgrad_wgs_per_cu", []() { return dg_conv_wgrad_wgs_per_cu(); });

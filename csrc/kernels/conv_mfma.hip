@@ -251,14 +251,6 @@ struct WgradArgs {
   int ablate;  // diagnostics: 1 no MFMA, 2 no LDS reads, 4 no DMA, 8 no slab store, 16 no barrier
   int ktiles, mtiles, splits;  // logical grid (launched flat, XCD-remapped)
   int nlayers;                 // t3 kernel: layers of identical geometry in one launch
-  // conv_wgrad_pipe_kernel's group reduction (null: slabs only): the last of each group of
-  // gsize consecutive splits of a tile sums the group's slabs into gpart[group] (the slab
-  // layout, ceil(splits / gsize) groups); tickets: [tiles][groups] zeroed counters, left
-  // zeroed; sf: the step tag (a group sum out of range sets it)
-  float* gpart;
-  unsigned* tickets;
-  int gsize;
-  long long* sf;
 };
 
 // Per-layer operands of a multi-layer weight-gradient launch (conv_wgrad_t3_kernel).
@@ -595,8 +587,7 @@ conv_wgrad_pipe_kernel(WgradArgs a) {
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
   }
 
-  const size_t zstride = (size_t)a.Mpad * a.KP;
-  float* slab = a.slab + (size_t)zsplit * zstride;
+  float* slab = a.slab + (size_t)zsplit * a.Mpad * a.KP;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -609,48 +600,6 @@ conv_wgrad_pipe_kernel(WgradArgs a) {
       }
     }
   }
-  if (a.gpart == nullptr) return;
-
-  // Group reduction: the split-K partial sums of gsize consecutive splits of this tile are
-  // summed by the LAST of them to finish (in split order: deterministic, whoever it is), so
-  // the update reads ceil(splits / gsize) group slabs instead of `splits` and no reduce
-  // launch runs after the kernel.  Hand-off (MI355X_MICROARCH.md, Valid forms, row 1):
-  // every storing wave drains its stores, the workgroup meets, one lane releases at agent
-  // scope and adds to the group's counter; the workgroup whose add returned gcount - 1 takes
-  // ONE agent acquire, drains, meets, then loads the group's slabs with plain loads.
-  const int grp = zsplit / a.gsize;
-  const int z0 = grp * a.gsize;
-  const int gcount = min(a.gsize, a.splits - z0);
-  const int ngrp = (a.splits + a.gsize - 1) / a.gsize;
-  unsigned* tk = a.tickets + (size_t)(mt * a.ktiles + kt) * ngrp + grp;
-  volatile LDS_AS unsigned* s_last = (volatile LDS_AS unsigned*)(LDS_AS char*)smem;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = atomicAdd(tk, 1u);
-    *s_last = old == (unsigned)(gcount - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*s_last == 0u) return;
-  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const float* src = a.slab + (size_t)z0 * zstride;
-  float* dst = a.gpart + (size_t)grp * zstride;
-  unsigned vmx = 0u;
-  // 128 rows x 32 float4 per tile: 16 float4 per thread, every split's loads in flight
-  for (int e = tid; e < 128 * 32; e += 256) {
-    const size_t off = (size_t)(m_tile + (e >> 5)) * a.KP + k_tile + (e & 31) * 4;
-    f32x4 v = *(const f32x4*)(src + off);
-    for (int z = 1; z < gcount; ++z) v += *(const f32x4*)(src + (size_t)z * zstride + off);
-    *(f32x4*)(dst + off) = v;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) vmx = max(vmx, __float_as_uint(v[c]) & 0x7FFFFFFFu);
-  }
-  if (a.sf && vmx >= __float_as_uint(GRAD_BOUND)) flag_bad_step(a.sf);
-  if (tid == 0) *tk = 0u;   // (every adder of this launch has added: ready for the next)
 }
 
 // Three-tap variant of conv_wgrad_kernel: one workgroup (8 waves) owns a 128 co x 384 k
@@ -1054,7 +1003,7 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
   const int Npix = B * NPTS;
   if (KP % 128 != 0 || Mpad % 128 != 0 || x_C % 8 != 0 || M % 8 != 0 || splits <= 0)
     return hipErrorInvalidValue;
-  WgradArgs a{};
+  WgradArgs a;
   a.dZ = (const char*)dZ;
   a.X = (const char*)X;
   a.slab = slab;
@@ -1105,52 +1054,6 @@ hipError_t dg_conv_wgrad(int kw, const void* dZ, int dz_pad, int M, int Mpad, co
   }
   return hipGetLastError();
 }
-
-// The 5x5 weight gradient with the in-kernel group reduction (conv_wgrad_pipe_kernel): the
-// slabs of gsize consecutive splits of a tile are summed into gpart[group] (the slab layout,
-// ceil(splits / gsize) groups) by the last of them to finish; tickets: ktiles x mtiles x
-// groups zeroed counters (left zeroed).  A reduce / the fused update then reads the groups.
-hipError_t dg_conv_wgrad_gp(const void* dZ, int dz_pad, int M, int Mpad, const void* X,
-                            int x_pad, int x_C, int B, int KP, int splits, float* slab,
-                            float* gpart, unsigned* tickets, int gsize, long long* sf,
-                            hipStream_t stream) {
-  const int Npix = B * NPTS;
-  if (KP % 128 != 0 || Mpad % 128 != 0 || x_C % 8 != 0 || M % 8 != 0 || splits <= 0 ||
-      !slab || !gpart || !tickets || gsize < 1)
-    return hipErrorInvalidValue;
-  WgradArgs a{};
-  a.dZ = (const char*)dZ;
-  a.X = (const char*)X;
-  a.slab = slab;
-  a.dz_pad = dz_pad;
-  a.M = M;
-  a.Mpad = Mpad;
-  a.KP = KP;
-  a.Npix = Npix;
-  int per = (Npix + splits - 1) / splits;
-  per = (per + 63) / 64 * 64;
-  a.px_per_split = per;
-  a.x_pad = x_pad;
-  a.x_C = x_C;
-  a.gpt = x_C / 8;
-  a.ngroups = 25 * a.gpt;
-  a.gpt_magic = magic_for(a.gpt);
-  if (a.ngroups * 8 > KP) return hipErrorInvalidValue;
-  a.ktiles = KP / 128;
-  a.mtiles = Mpad / 128;
-  a.splits = splits;
-  a.nlayers = 1;
-  a.gpart = gpart;
-  a.tickets = tickets;
-  a.gsize = gsize;
-  a.sf = sf;
-  constexpr size_t lds4 = 4 * 16 * 1024;
-  allow_lds(conv_wgrad_pipe_kernel<5, 4>, lds4);
-  hipLaunchKernelGGL((conv_wgrad_pipe_kernel<5, 4>), dim3(a.ktiles * a.mtiles * splits),
-                     dim3(256), lds4, stream, a);
-  return hipGetLastError();
-}
-int dg_conv_wgrad_gp_groups(int splits, int gsize) { return (splits + gsize - 1) / gsize; }
 
 // Weight gradients of nl layers of identical geometry in ONE launch (three-slice tiles):
 // table = nl rows of {dZ frame, X frame, slab} pointers; each layer gets `splits` pixel

@@ -50,7 +50,6 @@ FP8_W_MARGIN = 1.25
 FP8_G_HEADROOM = 4.0
 FP8_GHIST = 16        # gradient amax history length (conv_fp8.hip FP8_GHIST)
 REFRESH_PARTS = 512   # weight_refresh workgroups per layer (elementwise.hip)
-L0_GSIZE = 8          # the first layer's 5x5 split-K slabs summed in-kernel per group of 8
 
 
 @dataclass
@@ -375,17 +374,8 @@ class HipGoNet:
                          _ptr(self.wf8frag[p.index]), _ptr(self.wd8frag[p.index])])
         return np.ascontiguousarray(np.array(rows, dtype=np.int64))
 
-    def _l0_gp_ok(self, p: ConvPlan) -> bool:
-        """The first layer's 5x5 weight gradient with the in-kernel group reduction of its
-        split-K slabs (conv_wgrad_gp; DG_L0_GROUP_REDUCE=0: conv_wgrad + a reduce launch)."""
-        return (p.index == 0 and p.k == 5 and p.KPw % 128 == 0 and p.Mpad_w % 128 == 0
-                and p.cinp % 8 == 0 and p.cout % 8 == 0 and 25 * p.cinp <= p.KPw
-                and os.environ.get("DG_L0_GROUP_REDUCE", "1") != "0")
-
     def _build_plans(self):
         h, lay = self.h, self.layout
-        dev_ = self.device
-        self.l0_gpart = None
         P = self.params.data_ptr()
         G = self.grads.data_ptr()
         f4 = 4
@@ -579,30 +569,13 @@ class HipGoNet:
                                                   bpart)))
             # (the first layer's 5x5 as a sliding window over its 23 x 23 input frames was
             # measured slower: profiles/r4_s1_wgrad_l0_window_ab.txt)
-            rsrc, rsplits = slab, p.splits
-            if self._l0_gp_ok(p):
-                # the 5x5 weight gradient sums each group of L0_GSIZE splits of its slabs in
-                # the kernel (the group's last split to finish; conv_mfma.hip
-                # conv_wgrad_pipe_kernel): the fused update reads the groups itself, so no
-                # reduce launch follows the chain (profiles/r6_l0_group_reduce.txt)
-                ng = int(h.conv_wgrad_gp_groups(p.splits, L0_GSIZE))
-                self.l0_gpart = torch.empty(ng * p.Mpad_w * p.KPw, dtype=torch.float32,
-                                            device=dev_)
-                self.l0_tickets = torch.zeros((p.KPw // 128) * (p.Mpad_w // 128) * ng,
-                                              dtype=torch.int32, device=dev_)
-                ops.append((h.conv_wgrad_gp, (self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                              xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                              p.splits, slab, self.l0_gpart.data_ptr(),
-                                              self.l0_tickets.data_ptr(), L0_GSIZE, self._sf)))
-                rsrc, rsplits = self.l0_gpart.data_ptr(), ng
-            else:
-                ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
-                                           xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
-                                           p.splits, slab)))
-            red = (rsrc, G + spec.w_off * f4, rsplits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
+            ops.append((h.conv_wgrad, (p.k, self.dz[i].data_ptr(), dzp, p.cout, p.Mpad_w,
+                                       xin.data_ptr(), spec.pad, p.cinp, self.B, p.KPw,
+                                       p.splits, slab)))
+            red = (slab, G + spec.w_off * f4, p.splits, p.cout, p.Mpad_w, p.KPw, p.k * p.k,
                    p.cin, p.cinp, bpart, bch, G + spec.pos_off * f4,
                    G + spec.b_off * f4)
-            self._red_src[i] = (rsrc, bpart, rsplits, p.Mpad_w, p.KPw, bch)
+            self._red_src[i] = (slab, bpart, p.splits, p.Mpad_w, p.KPw, bch)
             if self.grads16 is not None:
                 ops.append((h.wgrad_reduce_w, red + (self._g16(spec.w_off),
                                                      self._g16(spec.pos_off),
@@ -1351,16 +1324,11 @@ class HipGoNet:
     def _defer_layers(self) -> set:
         """Layers whose pass 2 the fused update takes over when deferred: the grouped
         weight-gradient launch's layers (their slabs / partials are regions of their own, ~12
-        splits each), and the first layer when its 5x5 kernel sums its 64 split-K slabs into
-        8 group slabs itself (conv_wgrad_gp).  (Its 64 raw slabs were a poor fit for the
-        update's per-tile blocks — 128 us for the fused kernel with them, the reduce alone
-        10 us — so before round 6 it kept a reduce launch of its own.)"""
-        if len(self.wgroups) != 1:
-            return set()
-        d = set(self.wgroups[0])
-        if self.l0_gpart is not None and self._l0_side_at is not None and 0 in self._red_src:
-            d.add(0)
-        return d
+        splits each).  A layer outside it (the first layer's side-stream chain: 64 splits of
+        a 5x5 x 40 K) keeps its own slab reduce — its wide split-K sum is a poor fit for the
+        update's per-tile blocks (measured: 128 us for the fused kernel with it, the reduce
+        alone 10 us)."""
+        return set(self.wgroups[0]) if len(self.wgroups) == 1 else set()
 
     def can_defer(self) -> bool:
         """Whether a training step may leave its gradients as split-K slabs and bias partials
@@ -1479,7 +1447,7 @@ class HipGoNet:
         first layer: its side-stream chain ends later)."""
         sp = getattr(self, "_gu_split_tabs", None)
         if sp is None:
-            early = set(self.wgroups[0]) if len(self.wgroups) == 1 else set()
+            early = self._defer_layers()
             idx_e = [k for k, p in enumerate(self.plans) if p.index in early]
             idx_l = [k for k, p in enumerate(self.plans) if p.index not in early]
             sp = (np.ascontiguousarray(t[idx_e]), np.ascontiguousarray(t[idx_l]))

@@ -1104,44 +1104,3 @@ def test_stream_handoffs_checked_and_serialized_run_bit_identical(args, tmp_path
         assert torch.equal(outs[name]["params"], outs["plain"]["params"]), name
         assert torch.equal(outs[name]["loss"], outs["plain"]["loss"]), name
 
-
-
-@pytest.mark.parametrize("C", [128, 256])
-def test_l0_group_reduce_matches_reduce_launch(monkeypatch, C):
-    """The first layer's 5x5 weight gradient summing its split-K slabs in groups of 8 inside
-    the kernel (conv_wgrad_gp: the last split of a group to finish sums the group, after an
-    agent release / acquire hand-off; the fused update then reads 8 group slabs) vs the
-    plain kernel + its reduce launch (DG_L0_GROUP_REDUCE=0): the same gradient up to fp32
-    summation order, over several steps at the flagship batch (64 splits, 8 groups), and
-    the counters are left zeroed for the next replay."""
-    from deep_go_amd.config import ExperimentConfig
-    from deep_go_amd.data.synthetic import random_planes
-    from deep_go_amd.models.hip_model import HipGoNet
-    cfg = ExperimentConfig(numLayers=4, channelSize=C, batchSize=256, seed=2)
-    batches = [[torch.from_numpy(a).cuda() for a in random_planes(256, seed=90 + k)]
-               for k in range(3)]
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("DG_L0_GROUP_REDUCE", mode)
-        net = HipGoNet(cfg, 256, device="cuda")
-        assert (net.l0_gpart is not None) == (mode == "1")
-        net.keep_grads = True
-        gs = []
-        for bt in batches:
-            net.set_batch(*bt)
-            net.train_step()
-            torch.cuda.synchronize()
-            gs.append(net.grads.clone())
-        if mode == "1":
-            assert int(net.l0_tickets.abs().sum().item()) == 0
-            assert 0 in net._defer_layers()
-        out[mode] = (gs, net.params.clone())
-        del net
-    from deep_go_amd.models.gocnn import ParamLayout
-    l0 = ParamLayout(cfg).layers[0]
-    for k in range(len(batches)):
-        a, b = out["1"][0][k], out["0"][0][k]
-        w = slice(l0.w_off, l0.w_off + l0.w_numel)
-        assert torch.allclose(a[w], b[w], rtol=1e-4, atol=1e-7), (a[w] - b[w]).abs().max()
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-7)
-    assert torch.allclose(out["1"][1], out["0"][1], rtol=1e-5, atol=1e-7)
