@@ -26,7 +26,11 @@ def masked_stream(lib, ncu, keep):
     err = lib.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask)
     if err != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {err}")
-    return torch.cuda.ExternalStream(h.value), sum(bin(m).count("1") for m in mask)
+    back = (ctypes.c_uint32 * words)()
+    err = lib.hipExtStreamGetCUMask(h, ctypes.c_uint32(words), back)
+    readback = [int(v) for v in back] if err == 0 else f"error {err}"
+    return (torch.cuda.ExternalStream(h.value), sum(bin(m).count("1") for m in mask),
+            [int(v) for v in mask], readback)
 
 
 def timed(fn, stream, reps=10):
@@ -55,8 +59,9 @@ def main():
     out = torch.empty_like(x)
     mm = lambda: torch.matmul(x, y, out=out)  # noqa: E731
     plain = torch.cuda.Stream()
-    ms, nbits = masked_stream(lib, ncu, a.frac)
-    res = {"cus": ncu, "mask_cus": nbits, "n": a.n}
+    ms, nbits, asked, readback = masked_stream(lib, ncu, a.frac)
+    res = {"cus": ncu, "mask_cus": nbits, "n": a.n, "mask": asked, "readback": readback}
+    timed(mm, plain)   # clock ramp
     res["eager_plain_ms"] = timed(mm, plain)
     res["eager_masked_ms"] = timed(mm, ms)
 
