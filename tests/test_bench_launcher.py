@@ -2,6 +2,7 @@
 a child process), rank 0 prints ONE JSON line with n_gpus == N, the parent relays it and
 fails loudly when a rank fails (``--cpu-dry-run``: gloo + the fp32 oracle, no GPU)."""
 import json
+import re
 import os
 import subprocess
 import sys
@@ -76,7 +77,10 @@ def test_hung_rank_is_bounded_by_the_phase_guard():
     wall = time.monotonic() - t0
     assert r.returncode != 0
     assert "phase 'timed' exceeded" in r.stderr
-    assert "'rank1': ('timed'" in r.stderr   # (rank 0, waiting in the barrier, may trip too)
+    # the hung rank 1 and rank 0 (waiting for it in the barrier) enter 'timed' together, so
+    # either guard may fire first (the elastic agent then ends the other rank before its own
+    # guard reports): the launcher names whichever rank it was, in the timed phase
+    assert re.search(r"'rank[01]': \('timed'", r.stderr), r.stderr[-2000:]
     assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
     assert wall < 150
 
